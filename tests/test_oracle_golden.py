@@ -1,0 +1,118 @@
+"""Pin the CPU oracle (oracle/sed_oracle.py) against fixtures produced by the
+reference itself (oracle/make_golden.py).  CPU only."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import sed_oracle as O
+from sedx import synth
+
+GRU, TRF = 'Cnn_9layers_Gru_FrameAtt', 'Cnn_9layers_Transformer_FrameAtt'
+SEEDS = {GRU: 0, TRF: 1}
+
+
+def _sd(mt, preset='16k'):
+    return O.full_state(synth.make_state_dict(mt, seed=SEEDS[mt]), preset)
+
+
+def _close(a, b, tol, what=''):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    assert a.shape == b.shape, (what, a.shape, b.shape)
+    err = np.max(np.abs(a - b)) / max(1.0, np.max(np.abs(b)))
+    assert err <= tol, '%s: max rel err %.3g > %.3g' % (what, err, tol)
+
+
+@pytest.mark.parametrize('q', ['8k', '16k', '32k'])
+def test_frontend_construction(golden_dir, q):
+    g = np.load(os.path.join(golden_dir, 'frontend.npz'))
+    p = O.PRESETS[q]
+    melW = O.mel_filterbank(p['sample_rate'], p['window_size'], p['mel_bins'], p['fmin'], p['fmax'])
+    np.testing.assert_allclose(melW, g['melW_' + q], rtol=2e-6, atol=1e-9)
+    wr, wi = O.stft_weights(p['window_size'])
+    rows = g['rows_' + q]
+    np.testing.assert_allclose(wr[rows, 0], g['conv_real_rows_' + q], atol=2e-7)
+    np.testing.assert_allclose(wi[rows, 0], g['conv_imag_rows_' + q], atol=2e-7)
+
+
+@pytest.mark.parametrize('mt', [GRU, TRF])
+def test_stages(golden_dir, mt):
+    g = np.load(os.path.join(golden_dir, 'stages_%s.npz' % mt))
+    out, acts = O.forward(_sd(mt), mt, wave=g['wave'], return_acts=True)
+    for k in ('logmel', 'bn0', 'block1', 'block2', 'block3', 'block4', 'cnn_out', 'seq_out',
+              'norm_att'):
+        _close(acts[k], g[k], 1e-5, k)
+    for k in ('framewise_output', 'clipwise_output', 'embedding'):
+        _close(out[k], g[k], 1e-5, k)
+
+
+@pytest.mark.parametrize('mt', [GRU, TRF])
+@pytest.mark.parametrize('kind', ['ragged', 'clip10s'])
+def test_forward(golden_dir, mt, kind):
+    g = np.load(os.path.join(golden_dir, '%s_%s.npz' % (kind, mt)))
+    if kind == 'ragged':
+        wave = synth.make_waveforms(1, seconds=7777 / 16000., sample_rate=16000, seed=12)
+        np.testing.assert_array_equal(wave, g['wave'])
+    else:
+        wave = synth.make_waveforms(2, seconds=10.0, sample_rate=16000, seed=1234)
+    out = O.forward(_sd(mt), mt, wave=wave)
+    for k in ('framewise_output', 'clipwise_output', 'embedding'):
+        _close(out[k], g[k], 1e-5, k)
+
+
+@pytest.mark.parametrize('mt', [GRU, TRF])
+def test_windowed_and_events(golden_dir, mt):
+    g = np.load(os.path.join(golden_dir, 'windowed_%s.npz' % mt))
+    ev = json.load(open(os.path.join(golden_dir, 'events.json')))
+    audio = synth.make_waveforms(2, seconds=10.0, sample_rate=16000, seed=1234)[0]
+    sd = _sd(mt)
+    merged = O.predict_windows(sd, mt, audio, 16000, 5, 1, None)
+    _close(merged, g['merged_5_1'], 1e-5, 'merged_5_1')
+    merged_ms = O.predict_windows(sd, mt, audio, 16000, 6, 0.5, 160000)
+    _close(merged_ms, g['merged_6_05'], 1e-5, 'merged_6_05')
+    for which in ('default', 'synthetic'):
+        got = O.events_from_framewise(g['merged_5_1'], ev['params_' + which])
+        assert got == ev[mt][which]
+
+
+def test_merge_kat(golden_dir):
+    g = np.load(os.path.join(golden_dir, 'merge_kat.npz'))
+    for key in g.files:
+        dur, ov, n = key.split('_')
+        dur, ov, n = int(dur[1:]), float(ov[1:]), int(n[1:])
+        ov = int(ov) if ov == int(ov) else ov
+        nwin = len(O.window_starts(10.0, dur, ov))
+        merged = None
+        for s in range(1, nwin + 1):
+            curr = np.ones((1, n, 2), np.float32)
+            merged = curr if s == 1 else O.merge(merged, curr, dur, s, ov)
+        np.testing.assert_array_equal(O.avg_merge(merged, dur, ov)[0, :, 0], g[key])
+
+
+def test_vad_kat(golden_dir):
+    kat = json.load(open(os.path.join(golden_dir, 'vad_kat.json')))
+    for case in kat:
+        if 'find_bgn_fin_pairs' in case:
+            assert O.find_bgn_fin_pairs(case['find_bgn_fin_pairs']) == case['pairs']
+            continue
+        got = O.activity_detection(np.array(case['x']), case['thres'], case['low_thres'],
+                                   case['n_smooth'], case['n_salt'])
+        assert [[int(a), int(b)] for a, b in got] == case['pairs']
+
+
+def test_gamma(golden_dir):
+    g = np.load(os.path.join(golden_dir, 'gamma_%s.npz' % GRU))
+    audio = synth.make_waveforms(2, seconds=10.0, sample_rate=32000, seed=77)
+    for b in range(2):
+        gt = O.fft_gtgram(O.pad_truncate_sequence(audio[b], 320000), 32000, 1024 / 32000,
+                          320 / 32000, 64, 50)
+        np.testing.assert_allclose(gt, g['gtgram'][b], rtol=1e-5, atol=1e-12)
+        f = O.gamma_features(audio[b], '32k')
+        q = np.round(f.astype(np.float64) * 32767).astype(np.int16)
+        assert np.max(np.abs(q.astype(np.int32) - g['features_int16'][b])) <= 1
+    feats = torch.from_numpy(O.int16_to_float32(g['features_int16'])).unsqueeze(1).transpose(2, 3)
+    out = O.forward(_sd(GRU, '32k'), GRU, features=feats)
+    for k in ('framewise_output', 'clipwise_output', 'embedding'):
+        _close(out[k], g[k], 1e-5, k)
