@@ -1,0 +1,168 @@
+/*
+ * sedx.h — C ABI of the MI355X-native sound-event-detection inference path.
+ *
+ * Drop-in boundary for the reference's hot path (yazdayy/sound-event-detection,
+ * read-only at /root/reference).  The reference is pure Python/PyTorch; its
+ * "plugin API" for this path is the model classes instantiated by name
+ * (`Model = eval(model_type)`, pytorch/predict.py:229, pytorch/main_strong.py:529)
+ * with a fixed constructor, `forward()` and state_dict.  Each entry point below
+ * names the reference interface it replaces.  The host-side mirror of those
+ * classes (sound-event-detection_amd/sedx/models.py) binds these symbols with
+ * ctypes; INTEGRATION.md shows the binding a reference maintainer would add.
+ *
+ * Conventions
+ *  - Plain pointers and sizes; no torch / HIP types.  `stream` is a
+ *    hipStream_t passed as void* (NULL = the null stream).
+ *  - All `d_*` pointers are device pointers on the handle's device, fp32,
+ *    row-major, caller-owned.  `h_*` pointers are host memory.
+ *  - Every call returns sedx_status; on failure sedx_last_error(h) holds a
+ *    message (the Python shim raises RuntimeError with it), replacing the
+ *    reference's Python exceptions (e.g. pytorch/models.py:139).
+ *  - A handle is bound to one device and owns packed weights + a cached
+ *    workspace; calls on one handle must be serialised by the caller (the
+ *    reference's DataParallel uses one replica per device, one thread each).
+ */
+#ifndef SEDX_H
+#define SEDX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+  SEDX_OK = 0,
+  SEDX_EINVAL = 1,    /* bad argument / shape                     */
+  SEDX_ENOMEM = 2,    /* device allocation failed                  */
+  SEDX_EHIP = 3,      /* HIP runtime error                         */
+  SEDX_ESTATE = 4,    /* weights not finalised / wrong call order  */
+  SEDX_EKEY = 5       /* unknown or mis-shaped state_dict key      */
+} sedx_status;
+
+typedef enum {
+  SEDX_MODEL_GRU_FRAMEATT = 0,          /* Cnn_9layers_Gru_FrameAtt   pytorch/models.py:564 */
+  SEDX_MODEL_TRANSFORMER_FRAMEATT = 1   /* Cnn_9layers_Transformer_FrameAtt  :981       */
+} sedx_model;
+
+typedef enum { SEDX_FEATURE_LOGMEL = 0, SEDX_FEATURE_GAMMA = 1 } sedx_feature;
+
+/* Constructor arguments of the reference models (pytorch/models.py:565-566):
+ * (sample_rate, window_size, hop_size, mel_bins, fmin, fmax, classes_num,
+ * feature_type).  mel_bins must be 64 (bn0 is BatchNorm2d(64), models.py:607). */
+typedef struct {
+  int32_t model_type;     /* sedx_model   */
+  int32_t feature_type;   /* sedx_feature */
+  int32_t sample_rate;
+  int32_t window_size;    /* n_fft: 256, 512 or 1024 */
+  int32_t hop_size;
+  int32_t mel_bins;
+  float fmin;
+  float fmax;
+  int32_t classes_num;
+} sedx_config;
+
+typedef struct sedx_handle sedx_handle;
+
+/* Model construction: replaces Model(...) (pytorch/models.py:565-623 / :982-1024). */
+sedx_status sedx_create(const sedx_config* cfg, int device, sedx_handle** out);
+void sedx_destroy(sedx_handle* h);
+const char* sedx_last_error(const sedx_handle* h);
+const char* sedx_version(void);
+
+/* One state_dict entry (host fp32; int64 scalars such as num_batches_tracked
+ * are skipped by the caller).  Keys/shapes exactly as the reference
+ * state_dict; unused keys (att_block.bn_att.*,
+ * multihead.layer_norm.*) are accepted and ignored.  Replaces
+ * model.load_state_dict(checkpoint['model']) (pytorch/predict.py:232-233). */
+sedx_status sedx_load_param(sedx_handle* h, const char* key, const float* h_data,
+                            const int64_t* shape, int32_t ndim);
+/* Folds BN into conv weights, pre-packs GEMM layouts, uploads to the device.
+ * Must follow the last sedx_load_param and precede any forward. */
+sedx_status sedx_finalize_weights(sedx_handle* h);
+
+/* Output geometry for a batch of waveforms of L samples (logmel) or of
+ * feature matrices with T frames (gamma): frames of framewise_output
+ * (after x8 interpolation and, GRU only, padding to a multiple of 100:
+ * models.py:62-95, :678-681) and the sequence length after the CNN. */
+sedx_status sedx_output_geometry(const sedx_handle* h, int64_t L_or_T, int64_t* out_frames,
+                                 int64_t* seq_len);
+/* Bytes of device workspace sedx_forward* needs for (B, L). */
+sedx_status sedx_workspace_size(const sedx_handle* h, int64_t B, int64_t L_or_T, size_t* bytes);
+
+/* Model forward (eval mode): replaces Cnn_9layers_*_FrameAtt.forward(input)
+ * (pytorch/models.py:625-688, :1029-1077).
+ *   d_wave       [B, L]                         (logmel models)
+ *   d_framewise  [B, out_frames, classes_num]
+ *   d_clipwise   [B, classes_num]
+ *   d_embedding  GRU: [B, classes_num, seq_len]; Transformer: [B, 512, seq_len]
+ *                (may be NULL)
+ *   d_workspace  NULL = handle-owned cache, else >= sedx_workspace_size bytes. */
+sedx_status sedx_forward(sedx_handle* h, const float* d_wave, int64_t B, int64_t L,
+                         float* d_framewise, float* d_clipwise, float* d_embedding,
+                         void* d_workspace, size_t workspace_bytes, void* stream);
+
+/* Gamma branch (models.py:636-640): input is the [B, 64, T] feature matrix
+ * that the reference model receives (int16-dequantised gammatone dB). */
+sedx_status sedx_forward_features(sedx_handle* h, const float* d_feat, int64_t B, int64_t T,
+                                  float* d_framewise, float* d_clipwise, float* d_embedding,
+                                  void* d_workspace, size_t workspace_bytes, void* stream);
+
+/* Gammatone frontend (utils/gammatone/fftweight.py:126-168 + power_to_db
+ * top_db=80 + float32_to_int16 / int16_to_float32, utils/features.py:361-370,
+ * utils/utilities.py:73-79): d_audio [B, L] (already pad_truncated to 10 s)
+ * -> d_feat [B, 64, T], T = 1 + floor((L - nfft) / hop). */
+sedx_status sedx_gamma_features(sedx_handle* h, const float* d_audio, int64_t B, int64_t L,
+                                float* d_feat, int64_t* T_out, void* d_workspace,
+                                size_t workspace_bytes, void* stream);
+
+/* Windowed driver (pytorch/predict.py:297-349; main_strong.py:790-833).
+ * Slices every clip into windows of `sample_duration` s at stride
+ * `overlap_value` s (loop `while end <= audio_duration`), runs ALL windows of
+ * ALL clips as one batch, overlap-adds (utilities.py:405-423) and applies the
+ * reference's avg_merge divisor schedule (utilities.py:425-446).
+ *   d_audio       [n_clips, L_clip] (every clip has duration L_clip/sr)
+ *   pad_clip      0 = predict.py (each window pad_truncate'd),
+ *                 1 = main_strong (clip pad_truncate'd to 10 s first)
+ *   d_merged      [n_clips, merged_frames, classes_num]
+ * sedx_window_geometry returns n_windows per clip and merged_frames. */
+sedx_status sedx_window_geometry(const sedx_handle* h, int64_t L_clip, float sample_duration,
+                                 float overlap_value, int32_t pad_clip, int64_t* n_windows,
+                                 int64_t* window_samples, int64_t* merged_frames);
+sedx_status sedx_forward_windows(sedx_handle* h, const float* d_audio, int64_t n_clips,
+                                 int64_t L_clip, float sample_duration, float overlap_value,
+                                 int32_t pad_clip, float* d_merged, void* d_workspace,
+                                 size_t workspace_bytes, void* stream);
+sedx_status sedx_window_workspace_size(const sedx_handle* h, int64_t n_clips, int64_t L_clip,
+                                       float sample_duration, float overlap_value,
+                                       int32_t pad_clip, size_t* bytes);
+
+/* Per-stage device timing (the reference only wall-clocks whole loops,
+ * pytorch/main_strong.py:565-574).  When on, every forward records HIP events
+ * on its stream at the stage boundaries; sedx_stage_times waits for them and
+ * returns milliseconds for: 0 frontend, 1 conv1 of block 1, 2..8 the seven
+ * implicit-GEMM convs (b1c2, b2c1, b2c2, b3c1, b3c2, b4c1, b4c2), 9 GRU / MHA
+ * incl. projections, 10 AttBlock head. */
+#define SEDX_N_STAGES 11
+sedx_status sedx_set_profiling(sedx_handle* h, int32_t on);
+sedx_status sedx_stage_times(sedx_handle* h, float* ms, int32_t capacity, int32_t* n_stages);
+
+/* Thresholding into events: activity_detection per (clip, class)
+ * (utils/vad.py:11-199) as called by frame_prediction_to_event_prediction_v2
+ * (pytorch/predict.py:57-121).  Host-side, quirk-exact.
+ *   h_framewise [n_clips, T, C] (host), per-class parameter arrays of length C.
+ *   use_low_thres = 0 reproduces activity_detection(low_thres=None).
+ * Events are written as int32 quadruples (clip, class, bgn_frame, fin_frame)
+ * in (clip, class, time) order; onset = bgn / frames_per_second.  When
+ * *n_events > capacity the call returns SEDX_EINVAL with the required count. */
+sedx_status sedx_events(const float* h_framewise, int64_t n_clips, int64_t T, int64_t C,
+                        const double* high_thres, const double* low_thres,
+                        int32_t use_low_thres, const int64_t* n_smooth,
+                        const int64_t* n_salt, int32_t* h_events, int64_t capacity,
+                        int64_t* n_events);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SEDX_H */

@@ -1,0 +1,911 @@
+// libsedx C ABI (include/sedx.h): handle, state_dict ingestion + packing,
+// forward orchestration, windowed driver.  Host C++; kernels live in *.hip.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <complex>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/sedx.h"
+#include "sedx_internal.h"
+
+using namespace sedx;
+
+namespace {
+
+struct Tensor {
+  std::vector<int64_t> shape;
+  std::vector<float> data;
+};
+
+struct DevWeights {
+  float2* twiddle = nullptr;
+  float* window = nullptr;
+  float* mel_w = nullptr;
+  int32_t* mel_off = nullptr;
+  int32_t* mel_lo = nullptr;
+  float* bn0_scale = nullptr;
+  float* bn0_mean = nullptr;
+  float* bn0_bias = nullptr;
+  float* c1_w = nullptr;
+  float* c1_b = nullptr;
+  float* wp[8] = {};    // packed conv weights: block k conv j -> index 2(k-1)+(j-1); [0] unused
+  float* cb[8] = {};    // folded biases
+  float* w_ih = nullptr;   // [1536][512]
+  float* b_ih = nullptr;   // [1536]
+  float* whhT = nullptr;   // [2][256][768]
+  float* bhh = nullptr;    // [2][768]
+  float* wqkv = nullptr;   // [1536][512]
+  float* bqkv = nullptr;
+  float* wfc = nullptr;    // [512][512]
+  float* bfc = nullptr;
+  float* wac = nullptr;    // [nac][512]
+  float* bac = nullptr;
+  // gamma
+  float2* g_twiddle = nullptr;
+  float* g_window = nullptr;
+  float* g_weightsT = nullptr;  // [nfft/2+1][64] / nfft
+};
+
+}  // namespace
+
+struct sedx_handle {
+  sedx_config cfg;
+  int device = 0;
+  std::string err;
+  std::map<std::string, Tensor> params;
+  std::map<std::string, std::vector<int64_t>> expected;
+  bool finalized = false;
+  void* blob = nullptr;      // single device allocation for all packed weights
+  size_t blob_bytes = 0;
+  DevWeights w;
+  int nac = 64;              // rows of the att|cla projection (2C rounded up to 64)
+  int g_nfft = 0, g_nwin = 0, g_hop = 0;
+  void* ws = nullptr;        // cached workspace
+  size_t ws_bytes = 0;
+  // optional per-stage timing (sedx_set_profiling): events at stage boundaries
+  bool profiling = false;
+  hipEvent_t ev[SEDX_N_STAGES + 1] = {};
+  bool ev_recorded[SEDX_N_STAGES + 1] = {};
+};
+
+namespace {
+inline void mark(sedx_handle* h, int i, hipStream_t s) {
+  if (h->profiling && h->ev[i]) {
+    (void)hipEventRecord(h->ev[i], s);
+    h->ev_recorded[i] = true;
+  }
+}
+}  // namespace
+
+namespace {
+
+sedx_status fail(sedx_handle* h, sedx_status st, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  if (h) h->err = buf;
+  return st;
+}
+
+#define HIP_TRY(h, expr)                                                                \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess)                                                               \
+      return fail(h, SEDX_EHIP, "%s failed: %s", #expr, hipGetErrorString(e_));         \
+  } while (0)
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+bool is_gru(const sedx_handle* h) { return h->cfg.model_type == SEDX_MODEL_GRU_FRAMEATT; }
+
+void add_bn(std::map<std::string, std::vector<int64_t>>& e, const std::string& p, int64_t n) {
+  for (const char* s : {".weight", ".bias", ".running_mean", ".running_var"}) e[p + s] = {n};
+}
+
+void build_expected(sedx_handle* h) {
+  auto& e = h->expected;
+  const int64_t K = h->cfg.window_size / 2 + 1;
+  e["spectrogram_extractor.stft.conv_real.weight"] = {K, 1, h->cfg.window_size};
+  e["spectrogram_extractor.stft.conv_imag.weight"] = {K, 1, h->cfg.window_size};
+  e["logmel_extractor.melW"] = {K, h->cfg.mel_bins};
+  add_bn(e, "bn0", 64);
+  const int64_t ch[5] = {1, 64, 128, 256, 512};
+  for (int k = 1; k <= 4; ++k) {
+    const std::string p = "conv_block" + std::to_string(k);
+    e[p + ".conv1.weight"] = {ch[k], ch[k - 1], 3, 3};
+    e[p + ".conv2.weight"] = {ch[k], ch[k], 3, 3};
+    add_bn(e, p + ".bn1", ch[k]);
+    add_bn(e, p + ".bn2", ch[k]);
+  }
+  const int64_t C = h->cfg.classes_num;
+  e["att_block.att.weight"] = {C, 512, 1};
+  e["att_block.att.bias"] = {C};
+  e["att_block.cla.weight"] = {C, 512, 1};
+  e["att_block.cla.bias"] = {C};
+  add_bn(e, "att_block.bn_att", C);   // unused in forward (models.py:161-169)
+  if (is_gru(h)) {
+    for (const char* s : {"", "_reverse"}) {
+      e[std::string("gru.weight_ih_l0") + s] = {768, 512};
+      e[std::string("gru.weight_hh_l0") + s] = {768, 256};
+      e[std::string("gru.bias_ih_l0") + s] = {768};
+      e[std::string("gru.bias_hh_l0") + s] = {768};
+    }
+  } else {
+    for (const char* n : {"w_qs", "w_ks", "w_vs", "fc"}) {
+      e[std::string("multihead.") + n + ".weight"] = {512, 512};
+      e[std::string("multihead.") + n + ".bias"] = {512};
+    }
+    e["multihead.layer_norm.weight"] = {512};   // unused in forward (models.py:853-877)
+    e["multihead.layer_norm.bias"] = {512};
+  }
+}
+
+int64_t conv_T(const sedx_handle* h, int64_t L) { return L / h->cfg.hop_size + 1; }
+
+struct Geometry {
+  int64_t T, T1, T2, T3, fw_len, out_frames;
+};
+
+Geometry geometry_from_T(const sedx_handle* h, int64_t T) {
+  Geometry g;
+  g.T = T;
+  g.T1 = T / 2;
+  g.T2 = g.T1 / 2;
+  g.T3 = g.T2 / 2;
+  g.fw_len = 8 * g.T3;
+  g.out_frames = g.fw_len;
+  if (is_gru(h) && g.fw_len != 1000)   // pad_framewise_output(roundup) models.py:678-681
+    g.out_frames = (g.fw_len % 100 == 0) ? g.fw_len : g.fw_len + 100 - g.fw_len % 100;
+  return g;
+}
+
+// workspace layout (floats), 256-B aligned regions
+struct WsLayout {
+  size_t x0, bufA, bufB, total_bytes;
+};
+
+size_t align_up(size_t x) { return (x + 63) & ~size_t(63); }
+
+WsLayout ws_layout(const sedx_handle* h, int64_t B, const Geometry& g) {
+  WsLayout l;
+  size_t off = 0;
+  l.x0 = off;
+  off += align_up((size_t)B * g.T * 64);
+  size_t a = (size_t)B * g.T * 64 * 64;
+  a = std::max(a, (size_t)B * g.T1 * 32 * 128);
+  a = std::max(a, (size_t)B * g.T2 * 16 * 256);
+  a = std::max(a, (size_t)B * g.T3 * 8 * 512);
+  // head scratch (after the conv stack): G/QKV + H + O + logits
+  a = std::max(a, (size_t)B * g.T3 * (1536 + 512 + 512 + h->nac) + 4 * 64);
+  l.bufA = off;
+  off += align_up(a);
+  size_t b = (size_t)B * g.T1 * 32 * 64;
+  b = std::max(b, (size_t)B * g.T2 * 16 * 128);
+  b = std::max(b, (size_t)B * g.T3 * 8 * 256);
+  b = std::max(b, (size_t)B * g.T3 * 512);
+  l.bufB = off;
+  off += align_up(b);
+  l.total_bytes = off * sizeof(float);
+  return l;
+}
+
+sedx_status get_ws(sedx_handle* h, size_t need, void* user, size_t user_bytes, float** out) {
+  if (user) {
+    if (user_bytes < need)
+      return fail(h, SEDX_EINVAL, "workspace too small: %zu < %zu bytes", user_bytes, need);
+    *out = static_cast<float*>(user);
+    return SEDX_OK;
+  }
+  if (h->ws_bytes < need) {
+    if (h->ws) (void)hipFree(h->ws);
+    h->ws = nullptr;
+    h->ws_bytes = 0;
+    HIP_TRY(h, hipMalloc(&h->ws, need));
+    h->ws_bytes = need;
+  }
+  *out = static_cast<float*>(h->ws);
+  return SEDX_OK;
+}
+
+// CNN + head on X0 [B][T][64] already in workspace
+sedx_status run_body(sedx_handle* h, int64_t B, const Geometry& g, float* ws, const WsLayout& l,
+                     float* d_fw, float* d_clip, float* d_emb, hipStream_t s) {
+  const DevWeights& w = h->w;
+  float* X0 = ws + l.x0;
+  float* A = ws + l.bufA;
+  float* P = ws + l.bufB;
+  const int iB = (int)B;
+  mark(h, 1, s);
+  launch_conv_c1(X0, iB, (int)g.T, w.c1_w, w.c1_b, A, s);
+  mark(h, 2, s);
+  launch_conv3x3(A, iB, (int)g.T, 64, 64, 64, w.wp[1], w.cb[1], P, EPI_POOL2, s);
+  mark(h, 3, s);
+  launch_conv3x3(P, iB, (int)g.T1, 32, 64, 128, w.wp[2], w.cb[2], A, EPI_STORE, s);
+  mark(h, 4, s);
+  launch_conv3x3(A, iB, (int)g.T1, 32, 128, 128, w.wp[3], w.cb[3], P, EPI_POOL2, s);
+  mark(h, 5, s);
+  launch_conv3x3(P, iB, (int)g.T2, 16, 128, 256, w.wp[4], w.cb[4], A, EPI_STORE, s);
+  mark(h, 6, s);
+  launch_conv3x3(A, iB, (int)g.T2, 16, 256, 256, w.wp[5], w.cb[5], P, EPI_POOL2, s);
+  mark(h, 7, s);
+  launch_conv3x3(P, iB, (int)g.T3, 8, 256, 512, w.wp[6], w.cb[6], A, EPI_STORE, s);
+  mark(h, 8, s);
+  launch_conv3x3(A, iB, (int)g.T3, 8, 512, 512, w.wp[7], w.cb[7], P, EPI_FMEAN, s);
+  mark(h, 9, s);
+  float* S = P;                                   // [B][T3][512]
+  const int M = (int)(B * g.T3);
+  float* G = A;                                   // [M][1536]
+  float* Hs = A + align_up((size_t)M * 1536);     // [M][512]
+  float* O = Hs + align_up((size_t)M * 512);      // [M][512]
+  float* LG = O + align_up((size_t)M * 512);      // [M][nac]
+  if (is_gru(h)) {
+    launch_linear(S, M, 512, w.w_ih, 1536, w.b_ih, G, 0, s);
+    launch_gru(G, iB, (int)g.T3, w.whhT, w.bhh, Hs, s);
+  } else {
+    launch_linear(S, M, 512, w.wqkv, 1536, w.bqkv, G, 0, s);
+    launch_mha(G, iB, (int)g.T3, O, s);
+    launch_linear(O, M, 512, w.wfc, 512, w.bfc, Hs, 1, s);
+  }
+  mark(h, 10, s);
+  launch_linear(Hs, M, 512, w.wac, h->nac, w.bac, LG, 0, s);
+  launch_att_head(LG, iB, (int)g.T3, h->cfg.classes_num, h->nac, (int)g.out_frames, d_fw, d_clip,
+                  is_gru(h) ? d_emb : nullptr, s);
+  if (!is_gru(h) && d_emb) launch_transpose_btd(Hs, iB, (int)g.T3, 512, d_emb, s);
+  mark(h, 11, s);
+  HIP_TRY(h, hipGetLastError());
+  return SEDX_OK;
+}
+
+// -------- window geometry (predict.py:297-338 / main_strong.py:791-832) --------
+struct WinGeom {
+  int n_win = 0;
+  int64_t win_samples = 0;
+  int64_t start[64];
+  int64_t clip_len = 0;     // valid samples backing each clip
+  int step = 0, interval = 0, sd = 0;
+  int64_t Tw = 0, N = 0;
+  Geometry g;
+};
+
+sedx_status window_geometry(const sedx_handle* h, int64_t L_clip, float sample_duration,
+                            float overlap_value, int32_t pad_clip, WinGeom* wg) {
+  sedx_handle* hm = const_cast<sedx_handle*>(h);
+  const int sr = h->cfg.sample_rate;
+  const double sd = sample_duration, ov = overlap_value;
+  if (!(sd > 0) || !(ov > 0) || sd != std::floor(sd))
+    return fail(hm, SEDX_EINVAL, "sample_duration must be a positive integer number of seconds"
+                                 " and overlap_value > 0");
+  if (L_clip <= 0) return fail(hm, SEDX_EINVAL, "empty clip");
+  const double duration = (double)L_clip / sr;
+  double start = 0.0, end = 0.0;
+  int n = 0;
+  while (end <= duration) {
+    if (n >= 64) return fail(hm, SEDX_EINVAL, "more than 64 windows per clip");
+    wg->start[n++] = (int64_t)(start * sr);
+    start += ov;
+    end = start + sd;
+  }
+  wg->n_win = n;
+  wg->win_samples = (int64_t)(sd * sr);
+  if (pad_clip) {
+    const int64_t padded = (int64_t)sr * 10;
+    wg->clip_len = std::min<int64_t>(L_clip, padded);
+    for (int i = 0; i < n; ++i)
+      if (wg->start[i] + wg->win_samples > padded)
+        return fail(hm, SEDX_EINVAL, "window %d runs past the 10 s padded clip (reference feeds a "
+                                     "shorter window there)", i);
+  } else {
+    wg->clip_len = L_clip;
+  }
+  wg->g = geometry_from_T(h, conv_T(h, wg->win_samples));
+  wg->Tw = wg->g.out_frames;
+  wg->step = (int)(100 * ov);
+  wg->sd = (int)sd;
+  wg->interval = (int)(sd * 100) - wg->step;
+  if (wg->step <= 0 || wg->Tw < wg->step)
+    return fail(hm, SEDX_EINVAL, "overlap step %d frames incompatible with %lld-frame windows",
+                wg->step, (long long)wg->Tw);
+  wg->N = wg->Tw + (int64_t)(n - 1) * wg->step;
+  if (wg->g.T3 < 1) return fail(hm, SEDX_EINVAL, "window too short for the CNN");
+  return SEDX_OK;
+}
+
+template <typename T>
+T* carve(char*& p, size_t n) {
+  T* r = reinterpret_cast<T*>(p);
+  p += (n * sizeof(T) + 255) & ~size_t(255);
+  return r;
+}
+
+}  // namespace
+
+// ============================================================================
+// C ABI
+// ============================================================================
+extern "C" {
+
+const char* sedx_version(void) { return "sedx 0.1 (gfx950, fp32 MFMA)"; }
+
+const char* sedx_last_error(const sedx_handle* h) { return h ? h->err.c_str() : "null handle"; }
+
+sedx_status sedx_create(const sedx_config* cfg, int device, sedx_handle** out) {
+  if (!cfg || !out) return SEDX_EINVAL;
+  *out = nullptr;
+  if (cfg->model_type != SEDX_MODEL_GRU_FRAMEATT && cfg->model_type != SEDX_MODEL_TRANSFORMER_FRAMEATT)
+    return SEDX_EINVAL;
+  if (cfg->mel_bins != 64) return SEDX_EINVAL;
+  if (cfg->window_size != 256 && cfg->window_size != 512 && cfg->window_size != 1024) return SEDX_EINVAL;
+  if (cfg->hop_size <= 0 || cfg->sample_rate <= 0 || cfg->classes_num <= 0 || cfg->classes_num > 256)
+    return SEDX_EINVAL;
+  if (cfg->feature_type == SEDX_FEATURE_GAMMA && cfg->model_type != SEDX_MODEL_GRU_FRAMEATT)
+    return SEDX_EINVAL;
+  sedx_handle* h = new sedx_handle();
+  h->cfg = *cfg;
+  h->device = device;
+  h->nac = ((2 * cfg->classes_num + 63) / 64) * 64;
+  build_expected(h);
+  *out = h;
+  return SEDX_OK;
+}
+
+void sedx_destroy(sedx_handle* h) {
+  if (!h) return;
+  {
+    DeviceGuard g(h->device);
+    for (auto& e : h->ev)
+      if (e) (void)hipEventDestroy(e);
+    if (h->blob) (void)hipFree(h->blob);
+    if (h->ws) (void)hipFree(h->ws);
+  }
+  delete h;
+}
+
+sedx_status sedx_load_param(sedx_handle* h, const char* key, const float* h_data,
+                            const int64_t* shape, int32_t ndim) {
+  if (!h || !key || !h_data || (ndim > 0 && !shape) || ndim < 0 || ndim > 8) return SEDX_EINVAL;
+  auto it = h->expected.find(key);
+  if (it == h->expected.end()) return fail(h, SEDX_EKEY, "unexpected key in state_dict: %s", key);
+  std::vector<int64_t> sh(shape, shape + ndim);
+  if (sh != it->second) return fail(h, SEDX_EKEY, "size mismatch for %s", key);
+  int64_t n = 1;
+  for (auto d : sh) n *= d;
+  Tensor t;
+  t.shape = sh;
+  t.data.assign(h_data, h_data + n);
+  h->params[key] = std::move(t);
+  h->finalized = false;
+  return SEDX_OK;
+}
+
+sedx_status sedx_finalize_weights(sedx_handle* h) {
+  if (!h) return SEDX_EINVAL;
+  for (auto& kv : h->expected)
+    if (!h->params.count(kv.first))
+      return fail(h, SEDX_EKEY, "missing key in state_dict: %s", kv.first.c_str());
+  DeviceGuard dg(h->device);
+  const auto& P = h->params;
+  auto get = [&](const std::string& k) -> const std::vector<float>& { return P.at(k).data; };
+  const int nfft = h->cfg.window_size, K = nfft / 2 + 1;
+  const int C = h->cfg.classes_num;
+
+  // ---- STFT weights -> window (row k=0 of conv_real is the window since DFT[n,0]=1) ----
+  const auto& wr = get("spectrogram_extractor.stft.conv_real.weight");
+  const auto& wi = get("spectrogram_extractor.stft.conv_imag.weight");
+  std::vector<float> window(wr.begin(), wr.begin() + nfft);
+  {
+    // the FFT frontend requires conv_real/imag = Re/Im(DFT) * window (stft.py:209-217)
+    double maxerr = 0;
+    const int rows[6] = {1, 2, K / 3, K / 2, K - 2, K - 1};
+    for (int r : rows)
+      for (int n = 0; n < nfft; ++n) {
+        const double ang = -2.0 * M_PI * (double)((int64_t)n * r % nfft) / nfft;
+        maxerr = std::max(maxerr, std::fabs(wr[(size_t)r * nfft + n] - std::cos(ang) * window[n]));
+        maxerr = std::max(maxerr, std::fabs(wi[(size_t)r * nfft + n] - std::sin(ang) * window[n]));
+      }
+    if (maxerr > 1e-5)
+      return fail(h, SEDX_EINVAL, "STFT conv weights are not a windowed DFT (max err %.3g); "
+                                  "the FFT frontend cannot reproduce them", maxerr);
+  }
+  std::vector<float> tw(2 * nfft);
+  for (int m = 0; m < nfft; ++m) {
+    tw[2 * m] = (float)std::cos(-2.0 * M_PI * m / nfft);
+    tw[2 * m + 1] = (float)std::sin(-2.0 * M_PI * m / nfft);
+  }
+  // ---- mel bands ----
+  const auto& melW = get("logmel_extractor.melW");  // [K][64]
+  std::vector<float> mel_w;
+  std::vector<int32_t> mel_off(65), mel_lo(64);
+  for (int m = 0; m < 64; ++m) {
+    int lo = -1, hi = -1;
+    for (int k = 0; k < K; ++k)
+      if (melW[(size_t)k * 64 + m] != 0.0f) {
+        if (lo < 0) lo = k;
+        hi = k;
+      }
+    mel_off[m] = (int32_t)mel_w.size();
+    mel_lo[m] = lo < 0 ? 0 : lo;
+    if (lo >= 0)
+      for (int k = lo; k <= hi; ++k) mel_w.push_back(melW[(size_t)k * 64 + m]);
+  }
+  mel_off[64] = (int32_t)mel_w.size();
+  if (mel_w.empty()) mel_w.push_back(0.f);
+
+  auto bn_fold = [&](const std::string& p, int n, std::vector<double>& sc, std::vector<float>& mu,
+                     std::vector<float>& bi) {
+    const auto& g = get(p + ".weight");
+    const auto& b = get(p + ".bias");
+    const auto& m = get(p + ".running_mean");
+    const auto& v = get(p + ".running_var");
+    sc.resize(n);
+    mu.resize(n);
+    bi.resize(n);
+    for (int i = 0; i < n; ++i) {
+      sc[i] = (double)g[i] / std::sqrt((double)v[i] + 1e-5);
+      mu[i] = m[i];
+      bi[i] = b[i];
+    }
+  };
+  std::vector<double> s0;
+  std::vector<float> mu0, bi0, sc0f(64);
+  bn_fold("bn0", 64, s0, mu0, bi0);
+  for (int i = 0; i < 64; ++i) sc0f[i] = (float)s0[i];
+
+  // ---- conv weights: fold BN, pack [Cin/8][9][8][Cout] ----
+  const int ch[5] = {1, 64, 128, 256, 512};
+  std::vector<float> packed[8], cbias[8], c1w(64 * 9), c1b(64);
+  for (int k = 1; k <= 4; ++k)
+    for (int j = 1; j <= 2; ++j) {
+      const std::string p = "conv_block" + std::to_string(k);
+      const int cin = (j == 1) ? ch[k - 1] : ch[k], cout = ch[k];
+      const auto& wt = get(p + ".conv" + std::to_string(j) + ".weight");
+      std::vector<double> sc;
+      std::vector<float> mu, bi;
+      bn_fold(p + ".bn" + std::to_string(j), cout, sc, mu, bi);
+      std::vector<float> bias(cout);
+      for (int o = 0; o < cout; ++o) bias[o] = (float)((double)bi[o] - (double)mu[o] * sc[o]);
+      if (k == 1 && j == 1) {
+        for (int o = 0; o < 64; ++o)
+          for (int t = 0; t < 9; ++t) c1w[o * 9 + t] = (float)(wt[(size_t)o * 9 + t] * sc[o]);
+        c1b = bias;
+        continue;
+      }
+      const int idx = 2 * (k - 1) + (j - 1);
+      std::vector<float>& pk = packed[idx];
+      pk.assign((size_t)cin * 9 * cout, 0.f);
+      for (int o = 0; o < cout; ++o)
+        for (int i = 0; i < cin; ++i)
+          for (int t = 0; t < 9; ++t) {
+            const int chunk = i / 8, kc = i % 8;
+            pk[(((size_t)chunk * 9 + t) * 8 + kc) * cout + o] =
+                (float)(wt[((size_t)o * cin + i) * 9 + t] * sc[o]);
+          }
+      cbias[idx] = bias;
+    }
+
+  // ---- head ----
+  std::vector<float> w_ih, b_ih, whhT, bhh, wqkv, bqkv, wfc, bfc;
+  if (is_gru(h)) {
+    w_ih.resize(1536 * 512);
+    b_ih.resize(1536);
+    whhT.resize(2 * 256 * 768);
+    bhh.resize(2 * 768);
+    const char* sfx[2] = {"", "_reverse"};
+    for (int d = 0; d < 2; ++d) {
+      const auto& wih = get(std::string("gru.weight_ih_l0") + sfx[d]);
+      const auto& whh = get(std::string("gru.weight_hh_l0") + sfx[d]);
+      const auto& bi = get(std::string("gru.bias_ih_l0") + sfx[d]);
+      const auto& bh = get(std::string("gru.bias_hh_l0") + sfx[d]);
+      std::copy(wih.begin(), wih.end(), w_ih.begin() + (size_t)d * 768 * 512);
+      std::copy(bi.begin(), bi.end(), b_ih.begin() + d * 768);
+      std::copy(bh.begin(), bh.end(), bhh.begin() + d * 768);
+      for (int r = 0; r < 768; ++r)
+        for (int k = 0; k < 256; ++k) whhT[((size_t)d * 256 + k) * 768 + r] = whh[(size_t)r * 256 + k];
+    }
+  } else {
+    wqkv.resize(1536 * 512);
+    bqkv.resize(1536);
+    const char* nm[3] = {"w_qs", "w_ks", "w_vs"};
+    for (int i = 0; i < 3; ++i) {
+      const auto& ww = get(std::string("multihead.") + nm[i] + ".weight");
+      const auto& bb = get(std::string("multihead.") + nm[i] + ".bias");
+      std::copy(ww.begin(), ww.end(), wqkv.begin() + (size_t)i * 512 * 512);
+      std::copy(bb.begin(), bb.end(), bqkv.begin() + i * 512);
+    }
+    wfc = get("multihead.fc.weight");
+    bfc = get("multihead.fc.bias");
+  }
+  std::vector<float> wac((size_t)h->nac * 512, 0.f), bac(h->nac, 0.f);
+  {
+    const auto& wa = get("att_block.att.weight");
+    const auto& ba = get("att_block.att.bias");
+    const auto& wc = get("att_block.cla.weight");
+    const auto& bc = get("att_block.cla.bias");
+    for (int c = 0; c < C; ++c) {
+      std::copy(wa.begin() + (size_t)c * 512, wa.begin() + (size_t)(c + 1) * 512, wac.begin() + (size_t)c * 512);
+      std::copy(wc.begin() + (size_t)c * 512, wc.begin() + (size_t)(c + 1) * 512,
+                wac.begin() + (size_t)(C + c) * 512);
+      bac[c] = ba[c];
+      bac[C + c] = bc[c];
+    }
+  }
+
+  // ---- gammatone weights (computed here: utils/gammatone/fftweight.py:63-123) ----
+  std::vector<float> g_tw, g_win, g_wT;
+  if (h->cfg.feature_type == SEDX_FEATURE_GAMMA) {
+    const double fs = h->cfg.sample_rate;
+    const double win_t = (double)h->cfg.window_size / fs, hop_t = (double)h->cfg.hop_size / fs;
+    const int nfft_g = (int)std::pow(2.0, std::ceil(std::log2(2 * win_t * fs)));
+    auto rhaz = [](double x) { return (x > 0 ? 1.0 : (x < 0 ? -1.0 : 0.0)) * std::floor(std::fabs(x) + 0.5); };
+    const int nwin = (int)rhaz(win_t * fs), nhop = (int)rhaz(hop_t * fs);
+    if (nfft_g != 512 && nfft_g != 1024 && nfft_g != 2048)
+      return fail(h, SEDX_EINVAL, "gammatone nfft %d unsupported", nfft_g);
+    h->g_nfft = nfft_g;
+    h->g_nwin = nwin;
+    h->g_hop = nhop;
+    const int NB = nfft_g / 2 + 1, nf = 64;
+    const double fmin = h->cfg.fmin, fmax = fs / 2;
+    const double ear_q = 9.26449, min_bw = 24.7, T = 1.0 / fs;
+    std::vector<double> cf(nf);
+    for (int i = 0; i < nf; ++i) {
+      const double frac = (double)(i + 1) / nf;
+      cf[nf - 1 - i] = -ear_q * min_bw + std::exp(frac * (-std::log(fmax + ear_q * min_bw) +
+                                                          std::log(fmin + ear_q * min_bw))) *
+                                             (fmax + ear_q * min_bw);
+    }
+    g_wT.assign((size_t)NB * nf, 0.f);
+    typedef std::complex<double> cd;
+    for (int i = 0; i < nf; ++i) {
+      const double erb = cf[i] / ear_q + min_bw;
+      const double Bw = 1.019 * 2 * M_PI * erb;
+      const double arg = 2 * cf[i] * M_PI * T;
+      const cd vec = std::exp(cd(0, 2 * arg));
+      const double rt_pos = std::sqrt(3 + std::pow(2.0, 1.5)), rt_neg = std::sqrt(3 - std::pow(2.0, 1.5));
+      const double common = -T * std::exp(-(Bw * T));
+      const double k11 = std::cos(arg) + rt_pos * std::sin(arg), k12 = std::cos(arg) - rt_pos * std::sin(arg);
+      const double k13 = std::cos(arg) + rt_neg * std::sin(arg), k14 = std::cos(arg) - rt_neg * std::sin(arg);
+      const double A11 = common * k11, A12 = common * k12, A13 = common * k13, A14 = common * k14;
+      const cd gain_arg = std::exp(cd(-Bw * T, arg));
+      const cd den = -1.0 / std::exp(Bw * T) + 1.0 + vec * (1.0 - std::exp(Bw * T));
+      const cd q = T * std::exp(Bw * T) / den;
+      const double gain = std::abs((vec - gain_arg * k11) * (vec - gain_arg * k12) *
+                                   (vec - gain_arg * k13) * (vec - gain_arg * k14) * (q * q * q * q));
+      const double B2 = std::exp(-2 * Bw * T);
+      const double r = std::sqrt(B2), theta = 2 * M_PI * cf[i] / fs;
+      const cd pole = r * std::exp(cd(0, theta));
+      for (int k = 0; k < NB; ++k) {
+        const cd uc = std::exp(cd(0, 2 * M_PI * k / nfft_g));
+        const double v = std::abs(uc + A11 * fs) * std::abs(uc + A12 * fs) * std::abs(uc + A13 * fs) *
+                         std::abs(uc + A14 * fs) *
+                         std::pow(std::abs(fs * (pole - uc) * (std::conj(pole) - uc)), -4.0) / gain;
+        g_wT[(size_t)k * nf + i] = (float)(v / nfft_g);
+      }
+    }
+    g_tw.resize(2 * nfft_g);
+    for (int m = 0; m < nfft_g; ++m) {
+      g_tw[2 * m] = (float)std::cos(-2.0 * M_PI * m / nfft_g);
+      g_tw[2 * m + 1] = (float)std::sin(-2.0 * M_PI * m / nfft_g);
+    }
+    // specgram_window: centred Hann of width nwin in nfft (fftweight.py:15-30)
+    g_win.assign(nfft_g, 0.f);
+    const int halflen = nwin / 2, halff = nfft_g / 2;
+    const int act = std::min(halff, halflen);
+    for (int i = 0; i < act; ++i) {
+      const double v = 0.5 * (1 + std::cos(M_PI * i / halflen));
+      g_win[halff + i] = (float)v;
+      g_win[halff - i] = (float)v;
+    }
+  }
+
+  // ---- upload: one blob ----
+  struct Item {
+    void** dst;
+    const void* src;
+    size_t bytes;
+  };
+  std::vector<Item> items;
+  auto add = [&](void** dst, const void* src, size_t bytes) { items.push_back({dst, src, bytes}); };
+  DevWeights& W = h->w;
+  W = DevWeights();
+  add((void**)&W.twiddle, tw.data(), tw.size() * 4);
+  add((void**)&W.window, window.data(), window.size() * 4);
+  add((void**)&W.mel_w, mel_w.data(), mel_w.size() * 4);
+  add((void**)&W.mel_off, mel_off.data(), mel_off.size() * 4);
+  add((void**)&W.mel_lo, mel_lo.data(), mel_lo.size() * 4);
+  add((void**)&W.bn0_scale, sc0f.data(), 64 * 4);
+  add((void**)&W.bn0_mean, mu0.data(), 64 * 4);
+  add((void**)&W.bn0_bias, bi0.data(), 64 * 4);
+  add((void**)&W.c1_w, c1w.data(), c1w.size() * 4);
+  add((void**)&W.c1_b, c1b.data(), c1b.size() * 4);
+  for (int i = 1; i < 8; ++i) {
+    add((void**)&W.wp[i], packed[i].data(), packed[i].size() * 4);
+    add((void**)&W.cb[i], cbias[i].data(), cbias[i].size() * 4);
+  }
+  if (is_gru(h)) {
+    add((void**)&W.w_ih, w_ih.data(), w_ih.size() * 4);
+    add((void**)&W.b_ih, b_ih.data(), b_ih.size() * 4);
+    add((void**)&W.whhT, whhT.data(), whhT.size() * 4);
+    add((void**)&W.bhh, bhh.data(), bhh.size() * 4);
+  } else {
+    add((void**)&W.wqkv, wqkv.data(), wqkv.size() * 4);
+    add((void**)&W.bqkv, bqkv.data(), bqkv.size() * 4);
+    add((void**)&W.wfc, wfc.data(), wfc.size() * 4);
+    add((void**)&W.bfc, bfc.data(), bfc.size() * 4);
+  }
+  add((void**)&W.wac, wac.data(), wac.size() * 4);
+  add((void**)&W.bac, bac.data(), bac.size() * 4);
+  if (!g_wT.empty()) {
+    add((void**)&W.g_twiddle, g_tw.data(), g_tw.size() * 4);
+    add((void**)&W.g_window, g_win.data(), g_win.size() * 4);
+    add((void**)&W.g_weightsT, g_wT.data(), g_wT.size() * 4);
+  }
+  size_t total = 0;
+  for (auto& it : items) total += (it.bytes + 255) & ~size_t(255);
+  if (h->blob) {
+    (void)hipFree(h->blob);
+    h->blob = nullptr;
+  }
+  HIP_TRY(h, hipMalloc(&h->blob, total));
+  h->blob_bytes = total;
+  std::vector<char> host(total, 0);
+  size_t off = 0;
+  for (auto& it : items) {
+    std::memcpy(host.data() + off, it.src, it.bytes);
+    *it.dst = static_cast<char*>(h->blob) + off;
+    off += (it.bytes + 255) & ~size_t(255);
+  }
+  HIP_TRY(h, hipMemcpy(h->blob, host.data(), total, hipMemcpyHostToDevice));
+  h->finalized = true;
+  return SEDX_OK;
+}
+
+sedx_status sedx_set_profiling(sedx_handle* h, int32_t on) {
+  if (!h) return SEDX_EINVAL;
+  DeviceGuard dg(h->device);
+  if (on && !h->ev[0])
+    for (auto& e : h->ev) HIP_TRY(h, hipEventCreate(&e));
+  h->profiling = on != 0;
+  for (auto& r : h->ev_recorded) r = false;
+  return SEDX_OK;
+}
+
+sedx_status sedx_stage_times(sedx_handle* h, float* ms, int32_t capacity, int32_t* n_stages) {
+  if (!h || !n_stages) return SEDX_EINVAL;
+  *n_stages = SEDX_N_STAGES;
+  if (!h->profiling) return fail(h, SEDX_ESTATE, "profiling is off");
+  DeviceGuard dg(h->device);
+  for (int i = 0; i < SEDX_N_STAGES && i < capacity; ++i) {
+    float v = 0.f;
+    if (h->ev_recorded[i] && h->ev_recorded[i + 1]) {
+      HIP_TRY(h, hipEventSynchronize(h->ev[i + 1]));
+      HIP_TRY(h, hipEventElapsedTime(&v, h->ev[i], h->ev[i + 1]));
+    }
+    ms[i] = v;
+  }
+  return SEDX_OK;
+}
+
+sedx_status sedx_output_geometry(const sedx_handle* h, int64_t L_or_T, int64_t* out_frames,
+                                 int64_t* seq_len) {
+  if (!h || !out_frames || !seq_len) return SEDX_EINVAL;
+  const int64_t T = (h->cfg.feature_type == SEDX_FEATURE_GAMMA) ? L_or_T : conv_T(h, L_or_T);
+  const Geometry g = geometry_from_T(h, T);
+  *out_frames = g.out_frames;
+  *seq_len = g.T3;
+  return SEDX_OK;
+}
+
+sedx_status sedx_workspace_size(const sedx_handle* h, int64_t B, int64_t L_or_T, size_t* bytes) {
+  if (!h || !bytes || B <= 0) return SEDX_EINVAL;
+  const int64_t T = (h->cfg.feature_type == SEDX_FEATURE_GAMMA) ? L_or_T : conv_T(h, L_or_T);
+  *bytes = ws_layout(h, B, geometry_from_T(h, T)).total_bytes;
+  return SEDX_OK;
+}
+
+sedx_status sedx_forward(sedx_handle* h, const float* d_wave, int64_t B, int64_t L,
+                         float* d_framewise, float* d_clipwise, float* d_embedding,
+                         void* d_workspace, size_t workspace_bytes, void* stream) {
+  if (!h) return SEDX_EINVAL;
+  if (!h->finalized) return fail(h, SEDX_ESTATE, "weights not finalised");
+  if (h->cfg.feature_type != SEDX_FEATURE_LOGMEL)
+    return fail(h, SEDX_EINVAL, "gamma models take features: use sedx_forward_features");
+  if (!d_wave || !d_framewise || !d_clipwise || B <= 0)
+    return fail(h, SEDX_EINVAL, "null pointer or empty batch");
+  const int n2 = h->cfg.window_size / 2;
+  if (L <= n2)
+    return fail(h, SEDX_EINVAL, "input of %lld samples is too short for reflect padding of %d",
+                (long long)L, n2);
+  const Geometry g = geometry_from_T(h, conv_T(h, L));
+  if (g.T3 < 1) return fail(h, SEDX_EINVAL, "input too short for the 3 pooling stages");
+  if (B * g.T > INT32_MAX / 64) return fail(h, SEDX_EINVAL, "batch too large");
+  DeviceGuard dg(h->device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const WsLayout l = ws_layout(h, B, g);
+  float* ws = nullptr;
+  sedx_status st = get_ws(h, l.total_bytes, d_workspace, workspace_bytes, &ws);
+  if (st != SEDX_OK) return st;
+  FrontendParams p{};
+  p.audio = d_wave;
+  p.clip_stride = L;
+  p.n_clips = (int32_t)B;
+  p.n_win = 1;
+  p.win_start[0] = 0;
+  p.clip_len = L;
+  p.sig_len = L;
+  p.T = (int32_t)g.T;
+  p.hop = h->cfg.hop_size;
+  p.twiddle = h->w.twiddle;
+  p.window = h->w.window;
+  p.mel_w = h->w.mel_w;
+  p.mel_off = h->w.mel_off;
+  p.mel_lo = h->w.mel_lo;
+  p.bn_scale = h->w.bn0_scale;
+  p.bn_mean = h->w.bn0_mean;
+  p.bn_bias = h->w.bn0_bias;
+  p.out = ws + l.x0;
+  mark(h, 0, s);
+  launch_logmel(p, h->cfg.window_size, s);
+  return run_body(h, B, g, ws, l, d_framewise, d_clipwise, d_embedding, s);
+}
+
+sedx_status sedx_forward_features(sedx_handle* h, const float* d_feat, int64_t B, int64_t T,
+                                  float* d_framewise, float* d_clipwise, float* d_embedding,
+                                  void* d_workspace, size_t workspace_bytes, void* stream) {
+  if (!h) return SEDX_EINVAL;
+  if (!h->finalized) return fail(h, SEDX_ESTATE, "weights not finalised");
+  if (!d_feat || !d_framewise || !d_clipwise || B <= 0 || T <= 0)
+    return fail(h, SEDX_EINVAL, "null pointer or empty batch");
+  const Geometry g = geometry_from_T(h, T);
+  if (g.T3 < 1) return fail(h, SEDX_EINVAL, "input too short for the 3 pooling stages");
+  DeviceGuard dg(h->device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const WsLayout l = ws_layout(h, B, g);
+  float* ws = nullptr;
+  sedx_status st = get_ws(h, l.total_bytes, d_workspace, workspace_bytes, &ws);
+  if (st != SEDX_OK) return st;
+  mark(h, 0, s);
+  launch_features_bn0(d_feat, (int)B, (int)T, h->w.bn0_scale, h->w.bn0_mean, h->w.bn0_bias,
+                      ws + l.x0, s);
+  return run_body(h, B, g, ws, l, d_framewise, d_clipwise, d_embedding, s);
+}
+
+sedx_status sedx_gamma_features(sedx_handle* h, const float* d_audio, int64_t B, int64_t L,
+                                float* d_feat, int64_t* T_out, void* d_workspace,
+                                size_t workspace_bytes, void* stream) {
+  if (!h) return SEDX_EINVAL;
+  if (!h->finalized) return fail(h, SEDX_ESTATE, "weights not finalised");
+  if (h->cfg.feature_type != SEDX_FEATURE_GAMMA)
+    return fail(h, SEDX_EINVAL, "handle was not created with feature_type=gamma");
+  if (L < h->g_nfft) return fail(h, SEDX_EINVAL, "clip shorter than the gammatone FFT");
+  const int64_t T = 1 + (L - h->g_nfft) / h->g_hop;
+  if (T_out) *T_out = T;
+  if (!d_feat) return SEDX_OK;   // geometry query
+  if (!d_audio || B <= 0) return fail(h, SEDX_EINVAL, "null pointer or empty batch");
+  const int64_t fill = (L - h->g_nfft + h->g_hop - 1) / h->g_hop;   // len(range(0, s-n, h))
+  DeviceGuard dg(h->device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const size_t need = ((size_t)B * 64 * T + 256 + 2 * (size_t)B) * sizeof(float);
+  float* ws = nullptr;
+  sedx_status st = get_ws(h, need, d_workspace, workspace_bytes, &ws);
+  if (st != SEDX_OK) return st;
+  GammaParams p{};
+  p.audio = d_audio;
+  p.L = L;
+  p.B = (int32_t)B;
+  p.T = (int32_t)T;
+  p.T_fill = (int32_t)std::min<int64_t>(fill, T);
+  p.hop = h->g_hop;
+  p.nfft = h->g_nfft;
+  p.twiddle = h->w.g_twiddle;
+  p.window = h->w.g_window;
+  p.weights = h->w.g_weightsT;
+  p.gt = ws;
+  p.maxbuf = ws + (((size_t)B * 64 * T + 63) & ~size_t(63));
+  p.out = d_feat;
+  launch_gamma(p, s);
+  HIP_TRY(h, hipGetLastError());
+  return SEDX_OK;
+}
+
+sedx_status sedx_window_geometry(const sedx_handle* h, int64_t L_clip, float sample_duration,
+                                 float overlap_value, int32_t pad_clip, int64_t* n_windows,
+                                 int64_t* window_samples, int64_t* merged_frames) {
+  if (!h) return SEDX_EINVAL;
+  WinGeom wg;
+  sedx_status st = window_geometry(h, L_clip, sample_duration, overlap_value, pad_clip, &wg);
+  if (st != SEDX_OK) return st;
+  if (n_windows) *n_windows = wg.n_win;
+  if (window_samples) *window_samples = wg.win_samples;
+  if (merged_frames) *merged_frames = wg.N;
+  return SEDX_OK;
+}
+
+static size_t window_ws_bytes(const sedx_handle* h, int64_t n_clips, const WinGeom& wg) {
+  const int64_t items = n_clips * wg.n_win;
+  const WsLayout l = ws_layout(h, items, wg.g);
+  const size_t extra = (size_t)items * (wg.Tw * h->cfg.classes_num + h->cfg.classes_num) + 128;
+  return l.total_bytes + extra * sizeof(float);
+}
+
+sedx_status sedx_window_workspace_size(const sedx_handle* h, int64_t n_clips, int64_t L_clip,
+                                       float sample_duration, float overlap_value,
+                                       int32_t pad_clip, size_t* bytes) {
+  if (!h || !bytes || n_clips <= 0) return SEDX_EINVAL;
+  WinGeom wg;
+  sedx_status st = window_geometry(h, L_clip, sample_duration, overlap_value, pad_clip, &wg);
+  if (st != SEDX_OK) return st;
+  *bytes = window_ws_bytes(h, n_clips, wg);
+  return SEDX_OK;
+}
+
+sedx_status sedx_forward_windows(sedx_handle* h, const float* d_audio, int64_t n_clips,
+                                 int64_t L_clip, float sample_duration, float overlap_value,
+                                 int32_t pad_clip, float* d_merged, void* d_workspace,
+                                 size_t workspace_bytes, void* stream) {
+  if (!h) return SEDX_EINVAL;
+  if (!h->finalized) return fail(h, SEDX_ESTATE, "weights not finalised");
+  if (h->cfg.feature_type != SEDX_FEATURE_LOGMEL)
+    return fail(h, SEDX_EINVAL, "windowed inference needs a logmel model");
+  if (!d_audio || !d_merged || n_clips <= 0) return fail(h, SEDX_EINVAL, "null pointer or empty batch");
+  WinGeom wg;
+  sedx_status st = window_geometry(h, L_clip, sample_duration, overlap_value, pad_clip, &wg);
+  if (st != SEDX_OK) return st;
+  if (wg.win_samples <= h->cfg.window_size / 2)
+    return fail(h, SEDX_EINVAL, "window too short for reflect padding");
+  DeviceGuard dg(h->device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int64_t items = n_clips * wg.n_win;
+  const WsLayout l = ws_layout(h, items, wg.g);
+  float* ws = nullptr;
+  st = get_ws(h, window_ws_bytes(h, n_clips, wg), d_workspace, workspace_bytes, &ws);
+  if (st != SEDX_OK) return st;
+  float* fw = ws + l.total_bytes / sizeof(float);
+  float* clip = fw + align_up((size_t)items * wg.Tw * h->cfg.classes_num);
+  FrontendParams p{};
+  p.audio = d_audio;
+  p.clip_stride = L_clip;
+  p.n_clips = (int32_t)n_clips;
+  p.n_win = wg.n_win;
+  for (int i = 0; i < wg.n_win; ++i) p.win_start[i] = wg.start[i];
+  p.clip_len = wg.clip_len;
+  p.sig_len = wg.win_samples;
+  p.T = (int32_t)wg.g.T;
+  p.hop = h->cfg.hop_size;
+  p.twiddle = h->w.twiddle;
+  p.window = h->w.window;
+  p.mel_w = h->w.mel_w;
+  p.mel_off = h->w.mel_off;
+  p.mel_lo = h->w.mel_lo;
+  p.bn_scale = h->w.bn0_scale;
+  p.bn_mean = h->w.bn0_mean;
+  p.bn_bias = h->w.bn0_bias;
+  p.out = ws + l.x0;
+  mark(h, 0, s);
+  launch_logmel(p, h->cfg.window_size, s);
+  st = run_body(h, items, wg.g, ws, l, fw, clip, nullptr, s);
+  if (st != SEDX_OK) return st;
+  launch_merge(fw, (int)n_clips, wg.n_win, (int)wg.Tw, h->cfg.classes_num, wg.step, (int)wg.N,
+               wg.interval, wg.sd, d_merged, s);
+  HIP_TRY(h, hipGetLastError());
+  return SEDX_OK;
+}
+
+}  // extern "C"

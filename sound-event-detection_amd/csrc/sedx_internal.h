@@ -1,0 +1,93 @@
+// Internal declarations shared by the HIP translation units of libsedx.
+// Layout conventions (all fp32, row-major, device memory):
+//   wave      [items][L]                       (or per-item descriptors, window mode)
+//   X0        [items][T][64]                   log-mel after bn0 (conv input, Cin=1, F=64)
+//   act NHWC  [items][T][F][C]                 conv activations, channels innermost
+//   seq       [items][T4][512]                 CNN output after freq-mean (GRU/MHA input)
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace sedx {
+
+// ---- frontend -------------------------------------------------------------
+struct FrontendParams {
+  const float* audio;       // base pointer
+  int64_t clip_stride;      // samples between clips
+  int32_t n_clips;          // items = n_clips * n_win
+  int32_t n_win;            // windows per clip (1 in clip mode)
+  int64_t win_start[64];    // sample offset of each window (by value; n_win <= 64)
+  int64_t clip_len;         // valid samples per clip (beyond => zeros; pad_truncate)
+  int64_t sig_len;          // samples per item fed to the STFT (L or window length)
+  int32_t T;                // frames per item = sig_len / hop + 1
+  int32_t hop;
+  const float2* twiddle;    // [n_fft] exp(-2 pi i m / n_fft)
+  const float* window;      // [n_fft]
+  const float* mel_w;       // packed band weights
+  const int32_t* mel_off;   // [65] offsets into mel_w
+  const int32_t* mel_lo;    // [64] first fft bin of each band
+  const float* bn_scale;    // [64] bn0 folded
+  const float* bn_mean;     // [64]
+  const float* bn_bias;     // [64]
+  float* out;               // X0 [items][T][64]
+};
+void launch_logmel(const FrontendParams& p, int n_fft, hipStream_t s);
+
+// gamma features [B][64][T] -> X0 [B][T][64] with bn0
+void launch_features_bn0(const float* feat, int B, int T, const float* bn_scale,
+                         const float* bn_mean, const float* bn_bias, float* out,
+                         hipStream_t s);
+
+struct GammaParams {
+  const float* audio;     // [B][L]
+  int64_t L;
+  int32_t B, T, hop, nfft;
+  int32_t T_fill;          // frames actually filled by specgram's range(0, s-n, h)
+  const float2* twiddle;  // [nfft]
+  const float* window;    // [nfft] centred hann (specgram_window)
+  const float* weights;   // [64][nfft/2+1] ERB weights / nfft
+  float* gt;              // [B][64][T] workspace (linear magnitude)
+  float* maxbuf;          // [B] workspace
+  float* out;             // [B][64][T] dequantised features
+};
+void launch_gamma(const GammaParams& p, hipStream_t s);
+
+// ---- conv stack -----------------------------------------------------------
+// block-1 conv1: Cin=1 -> 64, BN folded, ReLU.  X0 [B][T][64] -> A [B][T][64][64]
+void launch_conv_c1(const float* x0, int B, int T, const float* w /*[64][9]*/,
+                    const float* bias /*[64]*/, float* out, hipStream_t s);
+
+enum ConvEpi { EPI_STORE = 0, EPI_POOL2 = 1, EPI_FMEAN = 2 };
+// 3x3 conv (pad 1) + folded BN + ReLU (+ epilogue), implicit GEMM on fp32 MFMA.
+//  in [B][T][F][Cin] -> EPI_STORE: [B][T][F][Cout], EPI_POOL2: [B][T/2][F/2][Cout],
+//  EPI_FMEAN: [B][T][Cout].  wp = packed [Cin/8][9][8][Cout], bias [Cout].
+void launch_conv3x3(const float* in, int B, int T, int F, int Cin, int Cout,
+                    const float* wp, const float* bias, float* out, int epi,
+                    hipStream_t s);
+
+// ---- sequence / head ------------------------------------------------------
+// C[M][N] = act(A[M][K] . W[N][K]^T + bias[N]);  act: 0 none, 1 relu
+void launch_linear(const float* A, int M, int K, const float* W, int N, const float* bias,
+                   float* C, int act, hipStream_t s);
+
+// bi-GRU recurrence.  G [B][T][1536] = x W_ih^T + b_ih (both dirs);
+// whhT [2][256][768]; bhh [2][768]; H [B][T][512]
+void launch_gru(const float* G, int B, int T, const float* whhT, const float* bhh, float* H,
+                hipStream_t s);
+
+// MHA core: QKV [B][T][1536] (q|k|v, head h = cols 64h..64h+63) -> O [B][T][512]
+void launch_mha(const float* QKV, int B, int T, float* O, hipStream_t s);
+
+// AttBlock finish + framewise expansion.  logits [B][T][ldl] (0..C-1 att, C..2C-1 cla)
+void launch_att_head(const float* logits, int B, int T, int C, int ldl, int out_frames,
+                     float* framewise, float* clipwise, float* emb_cla, hipStream_t s);
+// embedding for the Transformer model: E [B][T][D] -> emb [B][D][T]
+void launch_transpose_btd(const float* E, int B, int T, int D, float* out, hipStream_t s);
+
+// window overlap-add + avg_merge schedule.  fw [n_clips*n_win][Tw][C] ->
+// merged [n_clips][N][C]; step = int(100*overlap) frames, interval =
+// sample_duration*100 - step, sd = sample_duration (utilities.py:425-446).
+void launch_merge(const float* fw, int n_clips, int n_win, int Tw, int C, int step, int N,
+                  int interval, int sd, float* merged, hipStream_t s);
+
+}  // namespace sedx

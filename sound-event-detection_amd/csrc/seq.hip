@@ -1,0 +1,308 @@
+// Sequence + head kernels for gfx950:
+//   linear_kernel   C = act(A W^T + b) on fp32 MFMA 32x32x2 (GRU input projection
+//                   both directions, MHA q|k|v projection, MHA fc + ReLU, AttBlock
+//                   att|cla 1x1 convs)
+//   gru_kernel      bi-GRU recurrence, one workgroup per (clip, direction)
+//                   (torch nn.GRU semantics, pytorch/models.py:614-615,670)
+//   mha_kernel      per (clip, head) softmax(q k^T / 8) v, exact two-pass softmax
+//                   (ScaledDotProductAttention, pytorch/models.py:805-820)
+//   att_head_kernel AttBlock finish (clamp, exp, normalise over T, sigmoid,
+//                   weighted sum) + x8 frame repeat + GRU last-frame padding
+//                   (pytorch/models.py:161-175, :84-95, :65-81)
+//   merge_kernel    overlap-add of window predictions + avg_merge divisors
+//                   (utils/utilities.py:405-446)
+#include "sedx_internal.h"
+
+namespace sedx {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// ---------------------------------------------------------------------------
+template <int ACT>
+__global__ __launch_bounds__(256) void linear_kernel(const float* __restrict__ A, int M, int K,
+                                                     const float* __restrict__ W, int N,
+                                                     const float* __restrict__ bias,
+                                                     float* __restrict__ C) {
+  constexpr int BM = 128, BN = 64, BK = 16;
+  __shared__ float As[BK][BM + 4];
+  __shared__ float Ws[BK][BN + 4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int kh = lane >> 5;
+  f32x16 acc[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[j][r] = 0.0f;
+  for (int k0 = 0; k0 < K; k0 += BK) {
+    // A tile: 128 rows x 16 k  (512 float4)
+    for (int i = tid; i < BM * BK / 4; i += 256) {
+      const int m = i % BM, q = i / BM;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (m0 + m < M) v = *reinterpret_cast<const float4*>(A + (int64_t)(m0 + m) * K + k0 + 4 * q);
+      As[4 * q + 0][m] = v.x; As[4 * q + 1][m] = v.y; As[4 * q + 2][m] = v.z; As[4 * q + 3][m] = v.w;
+    }
+    for (int i = tid; i < BN * BK / 4; i += 256) {
+      const int n = i % BN, q = i / BN;
+      const float4 v = *reinterpret_cast<const float4*>(W + (int64_t)(n0 + n) * K + k0 + 4 * q);
+      Ws[4 * q + 0][n] = v.x; Ws[4 * q + 1][n] = v.y; Ws[4 * q + 2][n] = v.z; Ws[4 * q + 3][n] = v.w;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < BK / 2; ++ks) {
+      const float a = As[2 * ks + kh][wave * 32 + (lane & 31)];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const float bb = Ws[2 * ks + kh][j * 32 + (lane & 31)];
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bb, acc[j], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n = n0 + j * 32 + (lane & 31);
+    const float bv = bias ? bias[n] : 0.0f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = m0 + wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
+      if (m < M) {
+        float v = acc[j][r] + bv;
+        if (ACT == 1) v = fmaxf(v, 0.0f);
+        C[(int64_t)m * N + n] = v;
+      }
+    }
+  }
+}
+
+void launch_linear(const float* A, int M, int K, const float* W, int N, const float* bias,
+                   float* C, int act, hipStream_t s) {
+  dim3 grid((M + 127) / 128, N / 64);
+  if (act == 1)
+    hipLaunchKernelGGL(linear_kernel<1>, grid, dim3(256), 0, s, A, M, K, W, N, bias, C);
+  else
+    hipLaunchKernelGGL(linear_kernel<0>, grid, dim3(256), 0, s, A, M, K, W, N, bias, C);
+}
+
+// ---------------------------------------------------------------------------
+// bi-GRU: thread j owns hidden unit j of one (clip, direction); W_hh^T is
+// streamed from L2 each step (coalesced across j), h lives in LDS.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+__global__ __launch_bounds__(256) void gru_kernel(const float* __restrict__ G, int T,
+                                                  const float* __restrict__ whhT,
+                                                  const float* __restrict__ bhh,
+                                                  float* __restrict__ H) {
+  __shared__ float h[256];
+  const int j = threadIdx.x;
+  const int b = blockIdx.x;
+  const int dir = blockIdx.y;
+  const float* W = whhT + (int64_t)dir * 256 * 768;
+  const float br = bhh[dir * 768 + j], bz = bhh[dir * 768 + 256 + j], bn = bhh[dir * 768 + 512 + j];
+  h[j] = 0.0f;
+  float hj = 0.0f;
+  __syncthreads();
+  for (int s = 0; s < T; ++s) {
+    const int t = dir == 0 ? s : T - 1 - s;
+    const float* g = G + ((int64_t)b * T + t) * 1536 + dir * 768;
+    const float gr = g[j], gz = g[256 + j], gn = g[512 + j];
+    float ar = 0.f, az = 0.f, an = 0.f;
+#pragma unroll 8
+    for (int k = 0; k < 256; ++k) {
+      const float hk = h[k];
+      const float* wk = W + k * 768;
+      ar = fmaf(hk, wk[j], ar);
+      az = fmaf(hk, wk[256 + j], az);
+      an = fmaf(hk, wk[512 + j], an);
+    }
+    const float r = sigmoidf_(gr + (ar + br));
+    const float z = sigmoidf_(gz + (az + bz));
+    const float n = tanhf(gn + r * (an + bn));
+    hj = n + z * (hj - n);                 // ATen GRU cell: (1-z) n + z h
+    __syncthreads();
+    h[j] = hj;
+    H[((int64_t)b * T + t) * 512 + dir * 256 + j] = hj;
+    __syncthreads();
+  }
+}
+
+void launch_gru(const float* G, int B, int T, const float* whhT, const float* bhh, float* H,
+                hipStream_t s) {
+  hipLaunchKernelGGL(gru_kernel, dim3(B, 2), dim3(256), 0, s, G, T, whhT, bhh, H);
+}
+
+// ---------------------------------------------------------------------------
+// MHA core.  grid (ceil(T/128), B*8); thread = query row.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(128) void mha_kernel(const float* __restrict__ QKV, int T,
+                                                  float* __restrict__ O) {
+  constexpr int KC = 64;
+  __shared__ float Ks[KC][64];
+  __shared__ float Vs[KC][64];
+  const int bh = blockIdx.y;
+  const int b = bh >> 3, head = bh & 7;
+  const int qi = blockIdx.x * 128 + threadIdx.x;
+  const bool valid = qi < T;
+  const float* base = QKV + (int64_t)b * T * 1536;
+  float q[64], o[64];
+#pragma unroll
+  for (int d = 0; d < 64; ++d) {
+    q[d] = valid ? base[(int64_t)qi * 1536 + head * 64 + d] : 0.0f;
+    o[d] = 0.0f;
+  }
+  // pass 1: row max of q.k / 8
+  float mx = -INFINITY;
+  for (int c0 = 0; c0 < T; c0 += KC) {
+    const int nk = min(KC, T - c0);
+    __syncthreads();
+    for (int i = threadIdx.x; i < nk * 64; i += 128)
+      Ks[i >> 6][i & 63] = base[(int64_t)(c0 + (i >> 6)) * 1536 + 512 + head * 64 + (i & 63)];
+    __syncthreads();
+    for (int jj = 0; jj < nk; ++jj) {
+      float s = 0.f;
+#pragma unroll
+      for (int d = 0; d < 64; ++d) s = fmaf(q[d], Ks[jj][d], s);
+      mx = fmaxf(mx, s / 8.0f);
+    }
+  }
+  // pass 2: exp, sum, p.v
+  float l = 0.f;
+  for (int c0 = 0; c0 < T; c0 += KC) {
+    const int nk = min(KC, T - c0);
+    __syncthreads();
+    for (int i = threadIdx.x; i < nk * 64; i += 128) {
+      const int64_t r = (int64_t)(c0 + (i >> 6)) * 1536 + head * 64 + (i & 63);
+      Ks[i >> 6][i & 63] = base[r + 512];
+      Vs[i >> 6][i & 63] = base[r + 1024];
+    }
+    __syncthreads();
+    for (int jj = 0; jj < nk; ++jj) {
+      float s = 0.f;
+#pragma unroll
+      for (int d = 0; d < 64; ++d) s = fmaf(q[d], Ks[jj][d], s);
+      const float p = expf(s / 8.0f - mx);
+      l += p;
+#pragma unroll
+      for (int d = 0; d < 64; ++d) o[d] = fmaf(p, Vs[jj][d], o[d]);
+    }
+  }
+  if (valid) {
+    const float inv = 1.0f / l;
+    float* dst = O + ((int64_t)b * T + qi) * 512 + head * 64;
+#pragma unroll
+    for (int d = 0; d < 64; ++d) dst[d] = o[d] * inv;
+  }
+}
+
+void launch_mha(const float* QKV, int B, int T, float* O, hipStream_t s) {
+  hipLaunchKernelGGL(mha_kernel, dim3((T + 127) / 128, B * 8), dim3(128), 0, s, QKV, T, O);
+}
+
+// ---------------------------------------------------------------------------
+// AttBlock finish.  grid B, block 64 (thread = class).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void att_head_kernel(const float* __restrict__ logits, int T,
+                                                      int C, int ldl, int out_frames,
+                                                      float* __restrict__ fw,
+                                                      float* __restrict__ clip,
+                                                      float* __restrict__ emb) {
+  const int b = blockIdx.x;
+  const float* lg = logits + (int64_t)b * T * ldl;
+  for (int c = threadIdx.x; c < C; c += 64) {
+    float sum = 0.f;
+    for (int t = 0; t < T; ++t) {
+      const float a = fminf(fmaxf(lg[(int64_t)t * ldl + c], -10.0f), 10.0f);
+      sum += expf(a) + 1e-6f;
+    }
+    float acc = 0.f, last = 0.f;
+    for (int t = 0; t < T; ++t) {
+      const float a = fminf(fmaxf(lg[(int64_t)t * ldl + c], -10.0f), 10.0f);
+      const float na = (expf(a) + 1e-6f) / sum;
+      const float cla = sigmoidf_(lg[(int64_t)t * ldl + C + c]);
+      acc += na * cla;
+      last = cla;
+      if (emb) emb[((int64_t)b * C + c) * T + t] = cla;
+      float* dst = fw + ((int64_t)b * out_frames + 8 * t) * C + c;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) dst[(int64_t)r * C] = cla;
+    }
+    for (int f = 8 * T; f < out_frames; ++f) fw[((int64_t)b * out_frames + f) * C + c] = last;
+    clip[(int64_t)b * C + c] = acc;
+  }
+}
+
+void launch_att_head(const float* logits, int B, int T, int C, int ldl, int out_frames,
+                     float* framewise, float* clipwise, float* emb_cla, hipStream_t s) {
+  hipLaunchKernelGGL(att_head_kernel, dim3(B), dim3(64), 0, s, logits, T, C, ldl, out_frames,
+                     framewise, clipwise, emb_cla);
+}
+
+__global__ __launch_bounds__(256) void transpose_btd_kernel(const float* __restrict__ E, int T,
+                                                            int D, float* __restrict__ out) {
+  __shared__ float tile[32][33];
+  const int b = blockIdx.z;
+  const int t0 = blockIdx.x * 32, d0 = blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+  for (int i = ty; i < 32; i += 8) {
+    const int t = t0 + i, d = d0 + tx;
+    tile[i][tx] = (t < T && d < D) ? E[((int64_t)b * T + t) * D + d] : 0.f;
+  }
+  __syncthreads();
+  for (int i = ty; i < 32; i += 8) {
+    const int d = d0 + i, t = t0 + tx;
+    if (t < T && d < D) out[((int64_t)b * D + d) * T + t] = tile[tx][i];
+  }
+}
+
+void launch_transpose_btd(const float* E, int B, int T, int D, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(transpose_btd_kernel, dim3((T + 31) / 32, (D + 31) / 32, B), dim3(256), 0, s,
+                     E, T, D, out);
+}
+
+// ---------------------------------------------------------------------------
+// merge: merged[c][f][k] = (sum_w fw[c,w][f - w*step][k]) / div[f], summed in
+// window order exactly like the reference's incremental merge().
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void merge_kernel(const float* __restrict__ fw, int n_clips,
+                                                    int n_win, int Tw, int C, int step, int N,
+                                                    int interval, int sd,
+                                                    float* __restrict__ merged) {
+  const int64_t total = (int64_t)n_clips * N * C;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * 256) {
+    const int k = (int)(i % C);
+    const int64_t cf = i / C;
+    const int f = (int)(cf % N);
+    const int64_t c = cf / N;
+    float s = 0.f;
+    bool first = true;
+    for (int w = 0; w < n_win; ++w) {
+      const int lf = f - w * step;
+      if (lf < 0 || lf >= Tw) continue;
+      const float v = fw[((c * n_win + w) * Tw + lf) * C + k];
+      s = first ? v : s + v;
+      first = false;
+    }
+    // avg_merge: blocks [i, i+step) for i in range(step, N-step, step)
+    const int blk = (f / step) * step;
+    int d = 1;
+    if (blk >= step && blk < N - step) {
+      if (blk < interval) d = blk / step + 1;
+      else if (blk >= N - interval) d = (N - blk) / step + 1;
+      else d = sd;
+    }
+    merged[i] = d > 1 ? s / (float)d : s;
+  }
+}
+
+void launch_merge(const float* fw, int n_clips, int n_win, int Tw, int C, int step, int N,
+                  int interval, int sd, float* merged, hipStream_t s) {
+  const int64_t total = (int64_t)n_clips * N * C;
+  int64_t blocks = (total + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(merge_kernel, dim3(blocks), dim3(256), 0, s, fw, n_clips, n_win, Tw, C, step,
+                     N, interval, sd, merged);
+}
+
+}  // namespace sedx

@@ -1,0 +1,84 @@
+"""ctypes binding of libsedx.so (C ABI declared in include/sedx.h).
+
+torch is imported first on purpose: the PyTorch-ROCm wheel ships its own
+libamdhip64.so with the same SONAME (libamdhip64.so.7) as /opt/rocm's, so
+loading libsedx after torch binds it to the HIP runtime torch already runs
+(one runtime per process, device pointers shared)."""
+import ctypes
+import os
+
+import torch  # noqa: F401  (see module docstring)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, 'libsedx.so')
+
+SEDX_OK = 0
+STATUS = {0: 'OK', 1: 'EINVAL', 2: 'ENOMEM', 3: 'EHIP', 4: 'ESTATE', 5: 'EKEY'}
+
+EXPORTS = ['sedx_create', 'sedx_destroy', 'sedx_last_error', 'sedx_version', 'sedx_load_param',
+           'sedx_finalize_weights', 'sedx_output_geometry', 'sedx_workspace_size',
+           'sedx_forward', 'sedx_forward_features', 'sedx_gamma_features',
+           'sedx_window_geometry', 'sedx_forward_windows', 'sedx_window_workspace_size',
+           'sedx_events', 'sedx_set_profiling', 'sedx_stage_times']
+STAGES = ['frontend', 'b1c1', 'b1c2', 'b2c1', 'b2c2', 'b3c1', 'b3c2', 'b4c1', 'b4c2', 'seq', 'head']
+
+
+class SedxConfig(ctypes.Structure):
+    _fields_ = [('model_type', ctypes.c_int32), ('feature_type', ctypes.c_int32),
+                ('sample_rate', ctypes.c_int32), ('window_size', ctypes.c_int32),
+                ('hop_size', ctypes.c_int32), ('mel_bins', ctypes.c_int32),
+                ('fmin', ctypes.c_float), ('fmax', ctypes.c_float),
+                ('classes_num', ctypes.c_int32)]
+
+
+_lib = None
+
+P = ctypes.c_void_p
+I64 = ctypes.c_int64
+I32 = ctypes.c_int32
+F32 = ctypes.c_float
+SZ = ctypes.c_size_t
+PI64 = ctypes.POINTER(ctypes.c_int64)
+PSZ = ctypes.POINTER(ctypes.c_size_t)
+
+
+def lib():
+    """Load libsedx.so (fails loudly if it was not built: there is no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError('libsedx.so not found at %s: build it with `make -C '
+                           'sound-event-detection_amd` or __graft_entry__.build()' % LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH)
+    sig = {
+        'sedx_create': ([ctypes.POINTER(SedxConfig), ctypes.c_int, ctypes.POINTER(P)], I32),
+        'sedx_destroy': ([P], None),
+        'sedx_last_error': ([P], ctypes.c_char_p),
+        'sedx_version': ([], ctypes.c_char_p),
+        'sedx_load_param': ([P, ctypes.c_char_p, P, PI64, I32], I32),
+        'sedx_finalize_weights': ([P], I32),
+        'sedx_output_geometry': ([P, I64, PI64, PI64], I32),
+        'sedx_workspace_size': ([P, I64, I64, PSZ], I32),
+        'sedx_forward': ([P, P, I64, I64, P, P, P, P, SZ, P], I32),
+        'sedx_forward_features': ([P, P, I64, I64, P, P, P, P, SZ, P], I32),
+        'sedx_gamma_features': ([P, P, I64, I64, P, PI64, P, SZ, P], I32),
+        'sedx_window_geometry': ([P, I64, F32, F32, I32, PI64, PI64, PI64], I32),
+        'sedx_forward_windows': ([P, P, I64, I64, F32, F32, I32, P, P, SZ, P], I32),
+        'sedx_window_workspace_size': ([P, I64, I64, F32, F32, I32, PSZ], I32),
+        'sedx_events': ([P, I64, I64, I64, P, P, I32, P, P, P, I64, PI64], I32),
+        'sedx_set_profiling': ([P, I32], I32),
+        'sedx_stage_times': ([P, ctypes.POINTER(ctypes.c_float), I32, ctypes.POINTER(I32)], I32),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = res
+    _lib = L
+    return L
+
+
+def check(status, handle=None, what=''):
+    if status != SEDX_OK:
+        msg = lib().sedx_last_error(handle).decode() if handle else ''
+        raise RuntimeError('libsedx %s failed (%s): %s' % (what, STATUS.get(status, status), msg))

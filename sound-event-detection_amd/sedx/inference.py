@@ -1,0 +1,178 @@
+"""Drivers around the model: windowed inference (predict.py), batched clip
+inference (main_strong.py inference_prob), gammatone features and event
+extraction.  All compute goes through libsedx.
+
+ - predict_windows   pytorch/predict.py:297-349 (pad_clip=False) and
+                     pytorch/main_strong.py:790-833 (pad_clip=True): every
+                     window of every clip in ONE native batch, GPU overlap-add
+                     + avg_merge divisor schedule (utils/utilities.py:405-446).
+ - events_from_framewise   frame_prediction_to_event_prediction_v2
+                     (pytorch/predict.py:57-121; utils/utilities.py:155-214)
+                     over native activity_detection (utils/vad.py).
+ - gamma_features    utils/gammatone/fftweight.py:126-168 + utils/features.py:361-370
+                     + utils/utilities.py:73-79, on the GPU.
+ - inference_prob    pytorch/pytorch_utils.py:25-78 loop (batches of clips).
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+
+FRAMES_PER_SECOND = 100   # utils/config.py:13
+LABELS = ['Applause', 'Breathing', 'Chatter', 'Cheering', 'Child_speech_kid_speaking',
+          'Clapping', 'Conversation', 'Cough', 'Crowd', 'Crying_sobbing',
+          'Female_speech_woman_speaking', 'Laughter', 'Male_speech_man_speaking', 'Run',
+          'Screaming', 'Shout', 'Sneeze', 'Walk_footsteps', 'Whispering',
+          'Air_horn_truck_horn', 'Car_alarm', 'Emergency_vehicle', 'Explosion',
+          'Gunshot_gunfire', 'Siren']   # utils/config.py:31
+
+DEFAULT_PREDICT_PARAMS = {'audio_tagging_threshold': 0.099, 'sed_high_threshold': 0.5,
+                          'sed_low_threshold': 0.3, 'n_smooth': 10, 'n_salt': 10}
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def window_geometry(model, clip_samples, sample_duration=5, overlap_value=1, pad_clip=False):
+    nat = model.native(torch.device('cuda', torch.cuda.current_device()))
+    nw, ws, nf = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+    _lib.check(_lib.lib().sedx_window_geometry(nat.h, int(clip_samples), float(sample_duration),
+                                               float(overlap_value), int(bool(pad_clip)),
+                                               ctypes.byref(nw), ctypes.byref(ws), ctypes.byref(nf)),
+               nat.h, 'window_geometry')
+    return nw.value, ws.value, nf.value
+
+
+def predict_windows(model, audio, sample_duration=5, overlap_value=1, pad_clip=False):
+    """audio: [n_clips, L] (HIP tensor, every clip L samples long).  Returns the
+    merged + averaged framewise predictions [n_clips, N, classes]."""
+    if model.training:
+        raise RuntimeError('call model.eval() first')
+    if audio.device.type != 'cuda':
+        raise RuntimeError('predict_windows needs a HIP tensor (no CPU fallback)')
+    x = audio.to(torch.float32).contiguous()
+    if x.dim() == 1:
+        x = x[None]
+    nat = model.native(x.device)
+    L = _lib.lib()
+    n_clips, clip_len = x.shape
+    nw, wsamp, nf = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+    _lib.check(L.sedx_window_geometry(nat.h, clip_len, float(sample_duration), float(overlap_value),
+                                      int(bool(pad_clip)), ctypes.byref(nw), ctypes.byref(wsamp),
+                                      ctypes.byref(nf)), nat.h, 'window_geometry')
+    wsz = ctypes.c_size_t()
+    _lib.check(L.sedx_window_workspace_size(nat.h, n_clips, clip_len, float(sample_duration),
+                                            float(overlap_value), int(bool(pad_clip)),
+                                            ctypes.byref(wsz)), nat.h, 'window_workspace_size')
+    ws = torch.empty(wsz.value, dtype=torch.uint8, device=x.device)
+    merged = torch.empty((n_clips, nf.value, model.classes_num), dtype=torch.float32, device=x.device)
+    stream = ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
+    _lib.check(L.sedx_forward_windows(nat.h, _ptr(x), n_clips, clip_len, float(sample_duration),
+                                      float(overlap_value), int(bool(pad_clip)), _ptr(merged),
+                                      _ptr(ws), wsz.value, stream), nat.h, 'forward_windows')
+    return merged
+
+
+def gamma_features(model, audio):
+    """audio [B, L] HIP tensor (pad_truncated to 10 s) -> [B, 64, T] model input."""
+    if model.feature_type != 'gamma':
+        raise ValueError('model was not built with feature_type="gamma"')
+    x = audio.to(torch.float32).contiguous()
+    nat = model.native(x.device)
+    L = _lib.lib()
+    B, n = x.shape
+    T = ctypes.c_int64()
+    _lib.check(L.sedx_gamma_features(nat.h, ctypes.c_void_p(0), B, n, ctypes.c_void_p(0),
+                                     ctypes.byref(T), ctypes.c_void_p(0), 0, ctypes.c_void_p(0)),
+               nat.h, 'gamma geometry')
+    out = torch.empty((B, 64, T.value), dtype=torch.float32, device=x.device)
+    ws = torch.empty((B * 64 * T.value + 256 + 2 * B + 64) * 4, dtype=torch.uint8, device=x.device)
+    stream = ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
+    _lib.check(L.sedx_gamma_features(nat.h, _ptr(x), B, n, _ptr(out), ctypes.byref(T), _ptr(ws),
+                                     ws.numel(), stream), nat.h, 'gamma_features')
+    return out
+
+
+def _as_list(v, C):
+    if isinstance(v, (list, tuple, np.ndarray)):
+        return list(v)
+    return [v] * C
+
+
+def event_pairs(framewise, params):
+    """Native activity_detection over every (clip, class).  framewise [N, T, C]
+    (numpy or tensor).  Returns int32 array [n_events, 4] = (clip, class, bgn, fin)."""
+    fw = framewise.detach().cpu().numpy() if isinstance(framewise, torch.Tensor) else np.asarray(framewise)
+    fw = np.ascontiguousarray(fw, dtype=np.float32)
+    N, T, C = fw.shape
+    hi = np.ascontiguousarray(_as_list(params['sed_high_threshold'], C), dtype=np.float64)
+    lo_v = params.get('sed_low_threshold', None)
+    use_lo = lo_v is not None
+    lo = np.ascontiguousarray(_as_list(lo_v if use_lo else 0.0, C), dtype=np.float64)
+    ns = np.ascontiguousarray(_as_list(params['n_smooth'], C), dtype=np.int64)
+    nsalt = np.ascontiguousarray(_as_list(params['n_salt'], C), dtype=np.int64)
+    L = _lib.lib()
+    n = ctypes.c_int64()
+    cap = max(16, N * C * 4)
+    while True:
+        ev = np.zeros((cap, 4), dtype=np.int32)
+        st = L.sedx_events(fw.ctypes.data_as(ctypes.c_void_p), N, T, C,
+                           hi.ctypes.data_as(ctypes.c_void_p), lo.ctypes.data_as(ctypes.c_void_p),
+                           int(use_lo), ns.ctypes.data_as(ctypes.c_void_p),
+                           nsalt.ctypes.data_as(ctypes.c_void_p), ev.ctypes.data_as(ctypes.c_void_p),
+                           cap, ctypes.byref(n))
+        if st == _lib.SEDX_OK:
+            return ev[:n.value]
+        if n.value > cap:
+            cap = n.value
+            continue
+        raise RuntimeError('sedx_events failed: a run begins at the last frame after the '
+                           'find_bgn_fin_pairs quirk (the reference raises IndexError there)')
+
+
+def events_from_framewise(framewise, params, audio_name='test', frames_per_second=FRAMES_PER_SECOND,
+                          labels=LABELS, sort=True):
+    """List of {'filename','onset','offset','event_label'} exactly like
+    frame_prediction_to_event_prediction_v2 (+ the stable onset sort of
+    predict.py:353)."""
+    pairs = event_pairs(framewise, params)
+    names = audio_name if isinstance(audio_name, (list, tuple)) else None
+    out = []
+    for clip, k, b, f in pairs.tolist():
+        out.append({'filename': names[clip] if names else audio_name,
+                    'onset': b / float(frames_per_second), 'offset': f / float(frames_per_second),
+                    'event_label': labels[k]})
+    if sort:
+        out = sorted(out, key=lambda e: e['onset'])
+    return out
+
+
+def inference_prob(model, waveforms, batch_size=32, device=None):
+    """pytorch_utils.forward (pytorch/pytorch_utils.py:25-78): batched clip
+    inference; returns numpy {'clipwise_output', 'framewise_output'}."""
+    device = device or torch.device('cuda', torch.cuda.current_device())
+    outs = {'clipwise_output': [], 'framewise_output': []}
+    with torch.no_grad():
+        for i in range(0, len(waveforms), batch_size):
+            x = torch.as_tensor(waveforms[i:i + batch_size], dtype=torch.float32).to(device)
+            o = model(x)
+            outs['clipwise_output'].append(o['clipwise_output'].cpu().numpy())
+            outs['framewise_output'].append(o['framewise_output'].cpu().numpy())
+    return {k: np.concatenate(v, axis=0) for k, v in outs.items()}
+
+
+def write_xml(audio_name, events, start=0, end=0):
+    """XML document of pytorch/predict.py:264-407 (SoundCaptionList)."""
+    s = ['<AudioDoc name="{}">\n'.format(audio_name), '\t<SoundCaptionList>\n']
+    if events:
+        for e in events:
+            s.append('\t\t<SoundSegment stime="{}" dur="{}" event="{}">{}</SoundSegment>\n'.format(
+                e['onset'], e['offset'] - e['onset'], e['event_label'], e['event_label']))
+    else:
+        s.append('\t\t<SoundSegment stime="{}" dur="{}">Others</SoundSegment>\n'.format(start, end - start))
+    s.append('\t</SoundCaptionList>\n')
+    s.append('</AudioDoc>')
+    return ''.join(s)

@@ -1,0 +1,163 @@
+"""HIP path (libsedx through the C ABI) vs the golden fixtures / CPU oracle.
+
+Tolerance: north_star requires framewise_output within 1e-3 (fp32) of the
+reference CPU path and identical event segments.  TOL below is that bound;
+the fp32-MFMA path is expected to land near 1e-6, which the tests print.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import sed_oracle as O
+from sedx import synth
+
+pytestmark = pytest.mark.gpu
+
+GRU, TRF = 'Cnn_9layers_Gru_FrameAtt', 'Cnn_9layers_Transformer_FrameAtt'
+SEEDS = {GRU: 0, TRF: 1}
+TOL = 1e-3          # north_star: |framewise - reference| <= 1e-3 (fp32)
+P16 = (16000, 512, 160, 64, 25, 7000)
+P32 = (32000, 1024, 320, 64, 50, 14000)
+
+
+def build(mt, preset=P16, feature_type='logmel'):
+    from sedx import models
+    m = getattr(models, mt)(*preset, 25, feature_type)
+    sd = m.state_dict()
+    for k, v in synth.make_state_dict(mt, seed=SEEDS[mt]).items():
+        sd[k] = torch.from_numpy(v)
+    m.load_state_dict(sd, strict=True)
+    return m.to('cuda').eval()
+
+
+def run(m, wave):
+    with torch.no_grad():
+        out = m(torch.as_tensor(np.asarray(wave), dtype=torch.float32).cuda())
+    return {k: v.cpu().numpy() for k, v in out.items()}
+
+
+def err(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    assert a.shape == b.shape, (a.shape, b.shape)
+    return float(np.max(np.abs(a - b)))
+
+
+@pytest.fixture(scope='module', params=[GRU, TRF])
+def model(request):
+    return request.param, build(request.param)
+
+
+def test_short_clip_all_outputs(model, golden_dir):
+    mt, m = model
+    g = np.load(os.path.join(golden_dir, 'stages_%s.npz' % mt))
+    out = run(m, g['wave'])
+    for k in ('framewise_output', 'clipwise_output'):
+        e = err(out[k], g[k])
+        print(mt, k, 'max|d| =', e)
+        assert e <= TOL
+    emb_scale = max(1.0, float(np.abs(g['embedding']).max()))
+    assert err(out['embedding'], g['embedding']) <= TOL * emb_scale
+
+
+@pytest.mark.parametrize('kind', ['ragged', 'clip10s'])
+def test_clip_goldens(model, golden_dir, kind):
+    mt, m = model
+    g = np.load(os.path.join(golden_dir, '%s_%s.npz' % (kind, mt)))
+    if kind == 'ragged':
+        wave = synth.make_waveforms(1, seconds=7777 / 16000., sample_rate=16000, seed=12)
+    else:
+        wave = synth.make_waveforms(2, seconds=10.0, sample_rate=16000, seed=1234)
+    out = run(m, wave)
+    for k in ('framewise_output', 'clipwise_output'):
+        e = err(out[k], g[k])
+        print(mt, kind, k, 'max|d| =', e)
+        assert e <= TOL
+
+
+def test_batch32_vs_oracle(model):
+    """Headline config (B=32, 10 s @ 16 kHz) against the CPU oracle."""
+    mt, m = model
+    wave = synth.make_waveforms(32, seconds=10.0, sample_rate=16000, seed=4321)
+    out = run(m, wave)
+    ref = O.forward(O.full_state(synth.make_state_dict(mt, seed=SEEDS[mt])), mt, wave=wave)
+    for k in ('framewise_output', 'clipwise_output', 'embedding'):
+        scale = max(1.0, float(ref[k].abs().max()))
+        e = err(out[k], ref[k].numpy())
+        print(mt, 'B=32', k, 'max|d| =', e)
+        assert e <= TOL * scale
+
+
+def test_batch_invariance(model):
+    """A clip's output does not depend on the batch it runs in."""
+    mt, m = model
+    wave = synth.make_waveforms(5, seconds=3.0, sample_rate=16000, seed=99)
+    full = run(m, wave)
+    for i in (0, 3):
+        one = run(m, wave[i:i + 1])
+        assert np.array_equal(one['framewise_output'][0], full['framewise_output'][i])
+
+
+def test_windowed_and_events(model, golden_dir):
+    from sedx import inference
+    mt, m = model
+    g = np.load(os.path.join(golden_dir, 'windowed_%s.npz' % mt))
+    ev = json.load(open(os.path.join(golden_dir, 'events.json')))
+    audio = torch.from_numpy(synth.make_waveforms(2, seconds=10.0, sample_rate=16000, seed=1234)[:1]).cuda()
+    merged = inference.predict_windows(m, audio, 5, 1, pad_clip=False).cpu().numpy()
+    e = err(merged, g['merged_5_1'])
+    print(mt, 'windowed 5/1 max|d| =', e)
+    assert e <= TOL
+    merged_ms = inference.predict_windows(m, audio, 6, 0.5, pad_clip=True).cpu().numpy()
+    assert err(merged_ms, g['merged_6_05']) <= TOL
+    for which in ('default', 'synthetic'):
+        params = ev['params_' + which]
+        got = inference.events_from_framewise(merged, params)
+        exp = ev[mt][which]
+        if got != exp:
+            # report the threshold margin that explains a flip
+            hi = np.broadcast_to(np.asarray(params['sed_high_threshold'], np.float64), (25,))
+            margin = np.min(np.abs(g['merged_5_1'][0] - hi[None, :]))
+            pytest.fail('event mismatch (%s), min |x - high| = %g' % (which, margin))
+
+
+def test_windowed_multi_clip_matches_single(model):
+    from sedx import inference
+    mt, m = model
+    audio = torch.from_numpy(synth.make_waveforms(3, seconds=10.0, sample_rate=16000, seed=5)).cuda()
+    allm = inference.predict_windows(m, audio, 5, 1).cpu().numpy()
+    for i in range(3):
+        one = inference.predict_windows(m, audio[i:i + 1], 5, 1).cpu().numpy()
+        assert np.array_equal(one[0], allm[i])
+
+
+def test_gamma(golden_dir):
+    from sedx import inference
+    g = np.load(os.path.join(golden_dir, 'gamma_%s.npz' % GRU))
+    m = build(GRU, P32, 'gamma')
+    audio = torch.from_numpy(synth.make_waveforms(2, seconds=10.0, sample_rate=32000, seed=77)).cuda()
+    feats = inference.gamma_features(m, audio)
+    q = torch.round(feats.double() * 32767).to(torch.int32).cpu().numpy()
+    d = np.abs(q - g['features_int16'].astype(np.int32))
+    print('gamma int16 codes: max |d| =', d.max(), 'frac differing =', (d > 0).mean())
+    assert d.max() <= 2 and (d > 0).mean() < 0.01
+    gold_feats = torch.from_numpy(g['features_int16'].astype(np.float64) / 32767.).float().cuda()
+    with torch.no_grad():
+        out = m(gold_feats)
+    for k in ('framewise_output', 'clipwise_output'):
+        e = err(out[k].cpu().numpy(), g[k])
+        print('gamma', k, 'max|d| =', e)
+        assert e <= TOL
+
+
+def test_errors_are_loud():
+    m = build(GRU)
+    with pytest.raises(RuntimeError):
+        m(torch.zeros(1, 16000))                       # CPU tensor: no fallback
+    with pytest.raises(RuntimeError):
+        m(torch.zeros(1, 200, device='cuda'))          # too short for reflect pad
+    m.train()
+    with pytest.raises(RuntimeError):
+        m(torch.zeros(1, 16000, device='cuda'))        # training mode out of scope

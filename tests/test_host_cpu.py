@@ -1,0 +1,105 @@
+"""CPU-only checks of the product's host side: the C-ABI library loads and
+exports every symbol include/sedx.h declares, the native event extraction
+(host C++) matches the reference's vad known answers, and the model classes
+keep the reference state_dict contract.  No GPU compute is called."""
+import json
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import sed_oracle as O
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _header_symbols():
+    src = open(os.path.join(REPO, 'include', 'sedx.h')).read()
+    return sorted(set(re.findall(r'\b(sedx_[a-z_]+)\s*\(', src)))
+
+
+def test_library_exports_every_declared_symbol():
+    from sedx import _lib
+    L = _lib.lib()
+    syms = _header_symbols()
+    assert len(syms) >= 15
+    for s in syms:
+        assert hasattr(L, s), s
+    assert sorted(_lib.EXPORTS) == syms
+    assert b'gfx950' in L.sedx_version()
+
+
+def test_state_dict_contract():
+    from sedx import models
+    exp = {'Cnn_9layers_Gru_FrameAtt': (73, 6178336), 'Cnn_9layers_Transformer_FrameAtt': (75, 6047264)}
+    for mt, (nk, ne) in exp.items():
+        m = getattr(models, mt)(16000, 512, 160, 64, 25, 7000, 25, 'logmel')
+        sd = m.state_dict()
+        assert len(sd) == nk and sum(v.numel() for v in sd.values()) == ne
+        fr = O.frontend_state('16k')
+        for k, v in fr.items():
+            np.testing.assert_allclose(sd[k].numpy(), v, rtol=2e-6, atol=2e-7)
+
+
+def test_frontend_construction_matches_reference(golden_dir):
+    from sedx import stft
+    g = np.load(os.path.join(golden_dir, 'frontend.npz'))
+    for q, p in O.PRESETS.items():
+        w = stft.mel_weights(p['sample_rate'], p['window_size'], 64, p['fmin'], p['fmax'])
+        np.testing.assert_allclose(w, g['melW_' + q], rtol=2e-6, atol=1e-9)
+
+
+def test_native_events_match_vad_kat(golden_dir):
+    from sedx import inference
+    kat = json.load(open(os.path.join(golden_dir, 'vad_kat.json')))
+    for case in kat:
+        if 'x' not in case:
+            continue
+        x = np.asarray(case['x'], np.float32)[None, :, None]
+        params = {'sed_high_threshold': case['thres'], 'sed_low_threshold': case['low_thres'],
+                  'n_smooth': case['n_smooth'], 'n_salt': case['n_salt']}
+        try:
+            got = inference.event_pairs(x, params)[:, 2:].tolist()
+        except RuntimeError:
+            got = 'raises'
+        # the reference is run on float64 arrays here; float32 compare is identical
+        # unless a value sits within float32 rounding of a threshold
+        assert got == case['pairs'], case
+
+
+def test_native_events_match_golden_events(golden_dir):
+    from sedx import inference
+    ev = json.load(open(os.path.join(golden_dir, 'events.json')))
+    for mt in ('Cnn_9layers_Gru_FrameAtt', 'Cnn_9layers_Transformer_FrameAtt'):
+        merged = np.load(os.path.join(golden_dir, 'windowed_%s.npz' % mt))['merged_5_1']
+        for which in ('default', 'synthetic'):
+            got = inference.events_from_framewise(merged, ev['params_' + which])
+            assert got == ev[mt][which]
+
+
+def test_events_random_vs_oracle():
+    from sedx import inference
+    rng = np.random.default_rng(3)
+    for _ in range(20):
+        fw = rng.uniform(0, 1, (2, 200, 25)).astype(np.float32)
+        fw = np.cumsum(fw - 0.5, axis=1) / 8 + 0.5
+        fw = fw.astype(np.float32)
+        params = {'sed_high_threshold': rng.uniform(0.4, 0.7, 25).tolist(),
+                  'sed_low_threshold': rng.uniform(0.1, 0.4, 25).tolist(),
+                  'n_smooth': int(rng.integers(0, 12)), 'n_salt': int(rng.integers(0, 12))}
+        try:
+            got = inference.events_from_framewise(fw, params)
+        except RuntimeError:
+            with pytest.raises(IndexError):
+                O.events_from_framewise(fw, params)
+            continue
+        assert got == O.events_from_framewise(fw, params)
+
+
+def test_window_geometry_host_rules():
+    # loop control of predict.py:297-338 on the oracle side
+    assert O.window_starts(10.0, 5, 1) == [0, 1, 2, 3, 4, 5]
+    assert len(O.window_starts(10.0, 6, 0.5)) == 9
+    assert O.window_starts(3.0, 5, 1) == [0]
