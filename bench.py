@@ -1,7 +1,8 @@
 """Benchmark of the MI355X-native SED inference path (BASELINE.json metric).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--model gru|transformer]
-                    [--mode clip|window] [--batch 32] [--no-cpu-baseline]
+                    [--mode clip|window] [--batch 32] [--precision x3|exact]
+                    [--no-cpu-baseline] [--no-exact]
 
 One step = one forward of the hot path over one batch of synthetic 10 s @
 16 kHz clips per GPU (clip mode = main_strong inference_prob semantics, B=32
@@ -10,9 +11,11 @@ random-init with the reference architecture.  For N > 1 (launched by
 torch.distributed.run, one process per GPU) every rank runs its own shard of
 clips (weak scaling) and the framewise outputs are gathered to rank 0 over
 RCCL inside each step — the path's only collective.  Rank 0 prints ONE JSON
-line.
+line.  The headline uses the default conv arithmetic (3xbf16-split MFMA, fp32
+accumulate); the exact fp32-MFMA mode is timed beside it (value_exact_fp32).
 """
 import argparse
+import ctypes
 import json
 import os
 import statistics
@@ -24,8 +27,6 @@ for _p in (REPO, os.path.join(REPO, 'sound-event-detection_amd')):
     if _p not in sys.path:
         sys.path.insert(0, _p)
 
-import ctypes  # noqa: E402
-
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
@@ -33,20 +34,21 @@ import torch.distributed as dist  # noqa: E402
 from sedx import _lib, distributed, inference, models, synth  # noqa: E402
 
 METRIC = '10s@16kHz clips/sec (whole node) + ms/clip p50, Cnn_9_Gru_FrameAtt logmel'
-FP32_MFMA_PEAK_TF = 157.3      # MI355X_MICROARCH.md: FP32 matrix peak (spec)
+# MI355X_MICROARCH.md: FP32 matrix peak 157.3 TF; BF16 dense MFMA ~2.5 PF.  The
+# x3 scheme issues 3 bf16 MFMAs per useful MAC, so its arithmetic peak is 2.5/3 PF.
+PEAK_TF = {'exact': 157.3, 'x3': 2500.0 / 3}
 MODEL_NAMES = {'gru': 'Cnn_9layers_Gru_FrameAtt', 'transformer': 'Cnn_9layers_Transformer_FrameAtt'}
-# conv stages 2..8 of sedx_stage_times: (F, Cin, Cout, T divisor)
-CONV_STAGES = {'b1c2': (64, 64, 64, 1), 'b2c1': (32, 64, 128, 2), 'b2c2': (32, 128, 128, 2),
-               'b3c1': (16, 128, 256, 4), 'b3c2': (16, 256, 256, 4), 'b4c1': (8, 256, 512, 8),
-               'b4c2': (8, 512, 512, 8)}
+# conv stages of sedx_stage_times: (F, Cin, Cout, number of 2x poolings before it)
+CONV_STAGES = {'b1c2': (64, 64, 64, 0), 'b2c1': (32, 64, 128, 1), 'b2c2': (32, 128, 128, 1),
+               'b3c1': (16, 128, 256, 2), 'b3c2': (16, 256, 256, 2), 'b4c1': (8, 256, 512, 3),
+               'b4c2': (8, 512, 512, 3)}
 
 
 def conv_flops(stage, B, T):
-    F, cin, cout, div = CONV_STAGES[stage]
-    t = T
-    for _ in range({1: 0, 2: 1, 4: 2, 8: 3}[div]):
-        t //= 2
-    return 2.0 * B * t * F * cout * 9 * cin
+    F, cin, cout, npool = CONV_STAGES[stage]
+    for _ in range(npool):
+        T //= 2
+    return 2.0 * B * T * F * cout * 9 * cin
 
 
 def build_model(name, device):
@@ -77,27 +79,8 @@ def cpu_baseline(name, seconds):
                       'forward on the host CPU' % (n, el)}
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=20)
-    ap.add_argument('--warmup', type=int, default=3)
-    ap.add_argument('--batch', type=int, default=32, help='clips per GPU per step')
-    ap.add_argument('--model', choices=list(MODEL_NAMES), default='gru')
-    ap.add_argument('--mode', choices=['clip', 'window'], default='clip')
-    ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--cpu-seconds', type=float, default=15.0)
-    args = ap.parse_args()
-
-    world, rank, local = distributed.init()
-    if world != args.gpus and rank == 0:
-        print('warning: --gpus %d but WORLD_SIZE %d' % (args.gpus, world), file=sys.stderr)
-    dev = torch.device('cuda', local)
-    torch.cuda.set_device(dev)
-    name = MODEL_NAMES[args.model]
-    model = build_model(name, dev)
-    B = args.batch
-    wave = torch.from_numpy(synth.make_waveforms(B, 10.0, 16000, seed=1234 + rank)).to(dev)
+def measure(model, wave, args, world, rank, dev):
+    B = wave.shape[0]
 
     def step():
         with torch.no_grad():
@@ -127,8 +110,6 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     value = world * B * args.steps / elapsed
-
-    # latency: per-step synchronous wall time (ms per clip), p50 over steps
     lat = []
     for _ in range(max(5, min(args.steps, 20))):
         torch.cuda.synchronize()
@@ -136,38 +117,82 @@ def main():
         step()
         torch.cuda.synchronize()
         lat.append((time.perf_counter() - a) * 1e3 / B)
-    p50 = statistics.median(lat)
+    return value, elapsed, statistics.median(lat)
 
-    # per-stage device time with HIP events on the launch stream (profiled pass)
-    stage_ms, roof = None, None
+
+def stage_times(model, wave, dev, reps):
+    """Per-stage device time: HIP events recorded by libsedx on the stream the
+    kernels are launched on (sedx_set_profiling / sedx_stage_times)."""
+    nat = model.native(dev)
+    L = _lib.lib()
+    _lib.check(L.sedx_set_profiling(nat.h, 1), nat.h, 'set_profiling')
+    acc = np.zeros(len(_lib.STAGES))
+    for _ in range(reps):
+        with torch.no_grad():
+            model(wave)
+        ms = (ctypes.c_float * len(_lib.STAGES))()
+        n = ctypes.c_int32()
+        _lib.check(L.sedx_stage_times(nat.h, ms, len(_lib.STAGES), ctypes.byref(n)), nat.h, 'stage_times')
+        acc += np.array(ms[:])
+    _lib.check(L.sedx_set_profiling(nat.h, 0), nat.h, 'set_profiling')
+    return {s: round(float(v), 4) for s, v in zip(_lib.STAGES, acc / reps)}
+
+
+def roofline(stage_ms, B, precision):
+    T = 160000 // 160 + 1
+    conv = {s: stage_ms[s] for s in CONV_STAGES}
+    dom = max(conv, key=conv.get)
+    flops = conv_flops(dom, B, T)
+    achieved = flops / (conv[dom] * 1e-3) / 1e12
+    peak = PEAK_TF[precision]
+    total = sum(conv_flops(s, B, T) for s in CONV_STAGES)
+    return {'bound': 'mfma',
+            'kernel': 'conv3x3_%s (%s)' % ('x3_kernel' if precision == 'x3' else 'kernel', dom),
+            'arith': '3xbf16-split MFMA 32x32x16, fp32 acc (peak = bf16 dense 2.5 PF / 3)'
+                     if precision == 'x3' else 'fp32 MFMA 32x32x2',
+            'achieved': round(achieved, 2), 'peak': round(peak, 1), 'unit': 'TFLOP/s',
+            'frac': round(achieved / peak, 4), 'traffic': None,
+            'flops_per_launch': flops, 'avg_launch_ms': conv[dom],
+            'conv_stack_tflops': round(total / (sum(conv.values()) * 1e-3) / 1e12, 2)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--batch', type=int, default=32, help='clips per GPU per step')
+    ap.add_argument('--model', choices=list(MODEL_NAMES), default='gru')
+    ap.add_argument('--mode', choices=['clip', 'window'], default='clip')
+    ap.add_argument('--precision', choices=list(PEAK_TF), default='x3')
+    ap.add_argument('--no-exact', action='store_true', help='skip timing the exact fp32 mode')
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--cpu-seconds', type=float, default=15.0)
+    args = ap.parse_args()
+
+    world, rank, local = distributed.init()
+    if world != args.gpus and rank == 0:
+        print('warning: --gpus %d but WORLD_SIZE %d' % (args.gpus, world), file=sys.stderr)
+    dev = torch.device('cuda', local)
+    torch.cuda.set_device(dev)
+    name = MODEL_NAMES[args.model]
+    model = build_model(name, dev).set_precision(args.precision)
+    B = args.batch
+    wave = torch.from_numpy(synth.make_waveforms(B, 10.0, 16000, seed=1234 + rank)).to(dev)
+
+    value, elapsed, p50 = measure(model, wave, args, world, rank, dev)
+    stage_ms = roof = None
     if args.mode == 'clip':
-        nat = model.native(dev)
-        L = _lib.lib()
-        _lib.check(L.sedx_set_profiling(nat.h, 1), nat.h, 'set_profiling')
-        acc = np.zeros(len(_lib.STAGES))
-        reps = max(3, min(args.steps, 10))
-        for _ in range(reps):
-            with torch.no_grad():
-                model(wave)
-            ms = (ctypes.c_float * len(_lib.STAGES))()
-            n = ctypes.c_int32()
-            _lib.check(L.sedx_stage_times(nat.h, ms, len(_lib.STAGES), ctypes.byref(n)), nat.h,
-                       'stage_times')
-            acc += np.array(ms[:])
-        _lib.check(L.sedx_set_profiling(nat.h, 0), nat.h, 'set_profiling')
-        acc /= reps
-        stage_ms = {s: round(float(v), 4) for s, v in zip(_lib.STAGES, acc)}
-        T = 160000 // 160 + 1
-        conv = {s: stage_ms[s] for s in CONV_STAGES}
-        dom = max(conv, key=conv.get)
-        dom_flops = conv_flops(dom, B, T)
-        achieved = dom_flops / (conv[dom] * 1e-3) / 1e12
-        total_conv_flops = sum(conv_flops(s, B, T) for s in CONV_STAGES)
-        roof = {'bound': 'mfma', 'kernel': 'conv3x3_kernel (%s, fp32 MFMA 32x32x2)' % dom,
-                'achieved': round(achieved, 2), 'peak': FP32_MFMA_PEAK_TF, 'unit': 'TFLOP/s',
-                'frac': round(achieved / FP32_MFMA_PEAK_TF, 4), 'traffic': None,
-                'flops_per_launch': dom_flops, 'avg_launch_ms': conv[dom],
-                'conv_stack_tflops': round(total_conv_flops / (sum(conv.values()) * 1e-3) / 1e12, 2)}
+        stage_ms = stage_times(model, wave, dev, max(3, min(args.steps, 10)))
+        roof = roofline(stage_ms, B, args.precision)
+    exact = None
+    if not args.no_exact and args.precision != 'exact':
+        model.set_precision('exact')
+        ev, _, ep50 = measure(model, wave, args, world, rank, dev)
+        exact = {'value': round(ev, 2), 'ms_per_clip_p50': round(ep50, 4)}
+        if args.mode == 'clip':
+            exact['roofline'] = roofline(stage_times(model, wave, dev, 3), B, 'exact')
+        model.set_precision(args.precision)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -178,14 +203,16 @@ def main():
             'metric': METRIC, 'value': round(value, 2), 'unit': 'clips/s', 'n_gpus': world,
             'steps': args.steps, 'warmup': args.warmup,
             'ms_per_step': round(elapsed / args.steps * 1e3, 4), 'ms_per_clip_p50': round(p50, 4),
-            'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32',
+            'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
+            'dtype': 'f32' if args.precision == 'exact' else 'f32 (conv: 3xbf16-split MFMA, f32 accumulate)',
             'data': 'synthetic (seeded 0.1*N(0,1) + gated tones; random-init weights)',
             'config': {'workload': '%s logmel 16k, %d x 10 s clips per GPU per step (%s mode)'
                                    % (name, B, args.mode),
                        'batch_per_gpu': B, 'global_batch': B * world, 'clip_seconds': 10,
-                       'sample_rate': 16000, 'mode': args.mode,
+                       'sample_rate': 16000, 'mode': args.mode, 'precision': args.precision,
                        'parallelism': 'dp%d clip-sharded, RCCL gather of framewise' % world},
             'roofline': roof, 'cpu_baseline': cpu, 'stage_ms': stage_ms,
+            'value_exact_fp32': exact,
         }
         if cpu:
             line['speedup_vs_cpu'] = round(value / cpu['value'], 1)

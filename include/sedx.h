@@ -138,6 +138,16 @@ sedx_status sedx_window_workspace_size(const sedx_handle* h, int64_t n_clips, in
                                        float sample_duration, float overlap_value,
                                        int32_t pad_clip, size_t* bytes);
 
+/* Arithmetic of the 9-layer conv stack (96.8 % of the FLOPs).
+ *  SEDX_PRECISION_X3    (default) bf16 MFMA with a 3-term hi/lo operand split
+ *                       (hi*hi + hi*lo + lo*hi, fp32 accumulate): operands
+ *                       carry 16 significant bits, products err ~2^-16 rel.
+ *  SEDX_PRECISION_EXACT fp32-in / fp32-acc MFMA (v_mfma_f32_32x32x2_f32),
+ *                       bit-for-bit an fma chain, 16/3 x slower.
+ * Everything else (FFT frontend, GRU / MHA, head) is fp32 in both modes. */
+typedef enum { SEDX_PRECISION_EXACT = 0, SEDX_PRECISION_X3 = 1 } sedx_precision;
+sedx_status sedx_set_precision(sedx_handle* h, int32_t mode);
+
 /* Per-stage device timing (the reference only wall-clocks whole loops,
  * pytorch/main_strong.py:565-574).  When on, every forward records HIP events
  * on its stream at the stage boundaries; sedx_stage_times waits for them and

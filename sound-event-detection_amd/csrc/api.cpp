@@ -37,6 +37,7 @@ struct DevWeights {
   float* c1_b = nullptr;
   float* wp[8] = {};    // packed conv weights: block k conv j -> index 2(k-1)+(j-1); [0] unused
   float* cb[8] = {};    // folded biases
+  void* wx3[8] = {};    // split bf16 hi/lo packs for conv3x3_x3 (same indices)
   float* w_ih = nullptr;   // [1536][512]
   float* b_ih = nullptr;   // [1536]
   float* whhT = nullptr;   // [2][256][768]
@@ -70,6 +71,7 @@ struct sedx_handle {
   void* ws = nullptr;        // cached workspace
   size_t ws_bytes = 0;
   // optional per-stage timing (sedx_set_profiling): events at stage boundaries
+  int precision = SEDX_PRECISION_X3;   // conv stack arithmetic (sedx_set_precision)
   bool profiling = false;
   hipEvent_t ev[SEDX_N_STAGES + 1] = {};
   bool ev_recorded[SEDX_N_STAGES + 1] = {};
@@ -236,20 +238,26 @@ sedx_status run_body(sedx_handle* h, int64_t B, const Geometry& g, float* ws, co
   const int iB = (int)B;
   mark(h, 1, s);
   launch_conv_c1(X0, iB, (int)g.T, w.c1_w, w.c1_b, A, s);
-  mark(h, 2, s);
-  launch_conv3x3(A, iB, (int)g.T, 64, 64, 64, w.wp[1], w.cb[1], P, EPI_POOL2, s);
-  mark(h, 3, s);
-  launch_conv3x3(P, iB, (int)g.T1, 32, 64, 128, w.wp[2], w.cb[2], A, EPI_STORE, s);
-  mark(h, 4, s);
-  launch_conv3x3(A, iB, (int)g.T1, 32, 128, 128, w.wp[3], w.cb[3], P, EPI_POOL2, s);
-  mark(h, 5, s);
-  launch_conv3x3(P, iB, (int)g.T2, 16, 128, 256, w.wp[4], w.cb[4], A, EPI_STORE, s);
-  mark(h, 6, s);
-  launch_conv3x3(A, iB, (int)g.T2, 16, 256, 256, w.wp[5], w.cb[5], P, EPI_POOL2, s);
-  mark(h, 7, s);
-  launch_conv3x3(P, iB, (int)g.T3, 8, 256, 512, w.wp[6], w.cb[6], A, EPI_STORE, s);
-  mark(h, 8, s);
-  launch_conv3x3(A, iB, (int)g.T3, 8, 512, 512, w.wp[7], w.cb[7], P, EPI_FMEAN, s);
+  struct L {
+    const float* in;
+    int T, F, cin, cout, idx, epi;
+    float* out;
+  };
+  const L layers[7] = {{A, (int)g.T, 64, 64, 64, 1, EPI_POOL2, P},
+                       {P, (int)g.T1, 32, 64, 128, 2, EPI_STORE, A},
+                       {A, (int)g.T1, 32, 128, 128, 3, EPI_POOL2, P},
+                       {P, (int)g.T2, 16, 128, 256, 4, EPI_STORE, A},
+                       {A, (int)g.T2, 16, 256, 256, 5, EPI_POOL2, P},
+                       {P, (int)g.T3, 8, 256, 512, 6, EPI_STORE, A},
+                       {A, (int)g.T3, 8, 512, 512, 7, EPI_FMEAN, P}};
+  for (int i = 0; i < 7; ++i) {
+    const L& c = layers[i];
+    mark(h, 2 + i, s);
+    if (h->precision == SEDX_PRECISION_X3)
+      launch_conv3x3_x3(c.in, iB, c.T, c.F, c.cin, c.cout, w.wx3[c.idx], w.cb[c.idx], c.out, c.epi, s);
+    else
+      launch_conv3x3(c.in, iB, c.T, c.F, c.cin, c.cout, w.wp[c.idx], w.cb[c.idx], c.out, c.epi, s);
+  }
   mark(h, 9, s);
   float* S = P;                                   // [B][T3][512]
   const int M = (int)(B * g.T3);
@@ -343,7 +351,15 @@ T* carve(char*& p, size_t n) {
 // ============================================================================
 extern "C" {
 
-const char* sedx_version(void) { return "sedx 0.1 (gfx950, fp32 MFMA)"; }
+const char* sedx_version(void) { return "sedx 0.2 (gfx950: fp32 MFMA exact + 3xbf16-split MFMA)"; }
+
+sedx_status sedx_set_precision(sedx_handle* h, int32_t mode) {
+  if (!h) return SEDX_EINVAL;
+  if (mode != SEDX_PRECISION_EXACT && mode != SEDX_PRECISION_X3)
+    return fail(h, SEDX_EINVAL, "unknown precision mode %d", mode);
+  h->precision = mode;
+  return SEDX_OK;
+}
 
 const char* sedx_last_error(const sedx_handle* h) { return h ? h->err.c_str() : "null handle"; }
 
@@ -472,6 +488,7 @@ sedx_status sedx_finalize_weights(sedx_handle* h) {
   // ---- conv weights: fold BN, pack [Cin/8][9][8][Cout] ----
   const int ch[5] = {1, 64, 128, 256, 512};
   std::vector<float> packed[8], cbias[8], c1w(64 * 9), c1b(64);
+  std::vector<uint16_t> packed_x3[8];
   for (int k = 1; k <= 4; ++k)
     for (int j = 1; j <= 2; ++j) {
       const std::string p = "conv_block" + std::to_string(k);
@@ -499,6 +516,32 @@ sedx_status sedx_finalize_weights(sedx_handle* h) {
                 (float)(wt[((size_t)o * cin + i) * 9 + t] * sc[o]);
           }
       cbias[idx] = bias;
+      // 3xbf16 split pack: [Cout/BN][Cin/16][9][BN][4 slots x 8 bf16], slot c at c ^ ((n>>2)&3)
+      {
+        const int BN = (cout == 64) ? 64 : 128;
+        std::vector<uint16_t>& px = packed_x3[idx];
+        px.assign((size_t)cout * cin * 9 * 2, 0);
+        auto rne = [](float x) -> uint32_t {
+          uint32_t u;
+          std::memcpy(&u, &x, 4);
+          return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
+        };
+        for (int o = 0; o < cout; ++o)
+          for (int i = 0; i < cin; ++i)
+            for (int t = 0; t < 9; ++t) {
+              const float x = (float)(wt[((size_t)o * cin + i) * 9 + t] * sc[o]);
+              const uint32_t hb = rne(x);
+              const uint32_t hbits = hb << 16;
+              float hf;
+              std::memcpy(&hf, &hbits, 4);
+              const uint32_t lb = rne(x - hf);
+              const int nt = o / BN, n = o % BN, chunk = i / 16, k = i % 16;
+              const int sw = (n >> 2) & 3;
+              const size_t rec = ((((size_t)nt * (cin / 16) + chunk) * 9 + t) * BN + n) * 32;
+              px[rec + 8 * ((k / 8) ^ sw) + (k % 8)] = (uint16_t)hb;
+              px[rec + 8 * ((2 + k / 8) ^ sw) + (k % 8)] = (uint16_t)lb;
+            }
+      }
     }
 
   // ---- head ----
@@ -638,6 +681,7 @@ sedx_status sedx_finalize_weights(sedx_handle* h) {
   for (int i = 1; i < 8; ++i) {
     add((void**)&W.wp[i], packed[i].data(), packed[i].size() * 4);
     add((void**)&W.cb[i], cbias[i].data(), cbias[i].size() * 4);
+    add((void**)&W.wx3[i], packed_x3[i].data(), packed_x3[i].size() * 2);
   }
   if (is_gru(h)) {
     add((void**)&W.w_ih, w_ih.data(), w_ih.size() * 4);

@@ -131,57 +131,61 @@ __global__ __launch_bounds__(256, 2) void conv3x3_kernel(const float* __restrict
   const float* in_b = in + (int64_t)b * T * F * Cin;
   float4 ra[NA], rw[NW];
 
-  auto load_chunk = [&](int chunk) {
-    const int c0 = chunk * KC;
-#pragma unroll
-    for (int i = 0; i < NA; ++i) {
-      const int idx = tid + i * 256;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (idx < A_ITEMS) {
-        const int pix = idx >> 1, q = idx & 1;
-        const int r = pix / CS, c = pix - r * CS;
-        const int t = t0 - 1 + r, f = c - 1;
-        if (t >= 0 && t < T && f >= 0 && f < F)
-          v = *reinterpret_cast<const float4*>(in_b + ((int64_t)t * F + f) * Cin + c0 + 4 * q);
-      }
-      ra[i] = v;
-    }
-    const float* wsrc = wp + (int64_t)chunk * 9 * KC * Cout + n0;
-#pragma unroll
-    for (int i = 0; i < NW; ++i) {
-      const int idx = tid + i * 256;
-      if (idx < W_ITEMS) {
-        const int row = idx / (BN / 4), c4 = idx - row * (BN / 4);
-        rw[i] = *reinterpret_cast<const float4*>(wsrc + (int64_t)row * Cout + 4 * c4);
-      }
-    }
-  };
-  auto store_chunk = [&]() {
-#pragma unroll
-    for (int i = 0; i < NA; ++i) {
-      const int idx = tid + i * 256;
-      if (idx < A_ITEMS) {
-        const int pix = idx >> 1, q = idx & 1;
-        float* dst = As + (4 * q) * PL + pix;
-        dst[0] = ra[i].x;
-        dst[PL] = ra[i].y;
-        dst[2 * PL] = ra[i].z;
-        dst[3 * PL] = ra[i].w;
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < NW; ++i) {
-      const int idx = tid + i * 256;
-      if (idx < W_ITEMS) *reinterpret_cast<float4*>(Ws + 4 * idx) = rw[i];
-    }
-  };
+#define SEDX_LOAD_CHUNK(chunk_) \
+  { \
+    const int c0 = (chunk_) * KC;                                                                \
+_Pragma("unroll")                                                                                \
+    for (int i = 0; i < NA; ++i) {                                                               \
+      const int idx = tid + i * 256;                                                             \
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);                                                \
+      if (idx < A_ITEMS) {                                                                       \
+        const int pix = idx >> 1, q = idx & 1;                                                   \
+        const int r = pix / CS, c = pix - r * CS;                                                \
+        const int t = t0 - 1 + r, f = c - 1;                                                     \
+        if (t >= 0 && t < T && f >= 0 && f < F)                                                  \
+          v = *reinterpret_cast<const float4*>(in_b + ((int64_t)t * F + f) * Cin + c0 + 4 * q);  \
+      }                                                                                          \
+      ra[i] = v;                                                                                 \
+    }                                                                                            \
+    const float* wsrc = wp + (int64_t)(chunk_) * 9 * KC * Cout + n0;                             \
+_Pragma("unroll")                                                                                \
+    for (int i = 0; i < NW; ++i) {                                                               \
+      const int idx = tid + i * 256;                                                             \
+      if (idx < W_ITEMS) {                                                                       \
+        const int row = idx / (BN / 4), c4 = idx - row * (BN / 4);                               \
+        rw[i] = *reinterpret_cast<const float4*>(wsrc + (int64_t)row * Cout + 4 * c4);          \
+      } else {                                                                                   \
+        rw[i] = make_float4(0.f, 0.f, 0.f, 0.f);           \
+      }                                                                                          \
+    }                                                                                            \
+  }
+#define SEDX_STORE_CHUNK() \
+  { \
+_Pragma("unroll")                                                                                \
+    for (int i = 0; i < NA; ++i) {                                                               \
+      const int idx = tid + i * 256;                                                             \
+      if (idx < A_ITEMS) {                                                                       \
+        const int pix = idx >> 1, q = idx & 1;                                                   \
+        float* dst = As + (4 * q) * PL + pix;                                                    \
+        dst[0] = ra[i].x;                                                                        \
+        dst[PL] = ra[i].y;                                                                       \
+        dst[2 * PL] = ra[i].z;                                                                   \
+        dst[3 * PL] = ra[i].w;                                                                   \
+      }                                                                                          \
+    }                                                                                            \
+_Pragma("unroll")                                                                                \
+    for (int i = 0; i < NW; ++i) {                                                               \
+      const int idx = tid + i * 256;                                                             \
+      if (idx < W_ITEMS) *reinterpret_cast<float4*>(Ws + 4 * idx) = rw[i];                       \
+    }                                                                                            \
+  }
 
   const int nchunks = Cin / KC;
-  load_chunk(0);
-  store_chunk();
+  SEDX_LOAD_CHUNK(0);
+  SEDX_STORE_CHUNK();
   __syncthreads();
   for (int chunk = 0; chunk < nchunks; ++chunk) {
-    if (chunk + 1 < nchunks) load_chunk(chunk + 1);
+    if (chunk + 1 < nchunks) SEDX_LOAD_CHUNK(chunk + 1);
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
       const int toff = (tap / 3) * CS + (tap % 3);
@@ -201,11 +205,13 @@ __global__ __launch_bounds__(256, 2) void conv3x3_kernel(const float* __restrict
     }
     __syncthreads();
     if (chunk + 1 < nchunks) {
-      store_chunk();
+      SEDX_STORE_CHUNK();
       __syncthreads();
     }
   }
 
+#undef SEDX_LOAD_CHUNK
+#undef SEDX_STORE_CHUNK
   // ---- epilogue: bias + ReLU into LDS, then store / pool / freq-mean ----
   float* Cs = smem;
 #pragma unroll

@@ -65,6 +65,12 @@ void launch_conv3x3(const float* in, int B, int T, int F, int Cin, int Cout,
                     const float* wp, const float* bias, float* out, int epi,
                     hipStream_t s);
 
+// Same contract on bf16 MFMA with a 3-term hi/lo split (fp32-class accuracy).
+// wp = host-packed split weights [Cout/BN][Cin/16][9][BN][4 x 16 B] (BN = 64 if
+// Cout == 64 else 128), slots XOR-swizzled by ((n >> 2) & 3).
+void launch_conv3x3_x3(const float* in, int B, int T, int F, int Cin, int Cout, const void* wp,
+                       const float* bias, float* out, int epi, hipStream_t s);
+
 // ---- sequence / head ------------------------------------------------------
 // C[M][N] = act(A[M][K] . W[N][K]^T + bias[N]);  act: 0 none, 1 relu
 void launch_linear(const float* A, int M, int K, const float* W, int N, const float* bias,

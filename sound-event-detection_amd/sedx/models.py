@@ -167,6 +167,7 @@ class _Native(object):
         self.h = h
         self.device_index = device_index
         self.signature = None
+        self.precision = 'x3'   # the library default
 
     def load(self, state_dict):
         L = _lib.lib()
@@ -217,6 +218,7 @@ class _SedModel(nn.Module):
         self.conv_block3 = ConvBlock(128, 256)
         self.conv_block4 = ConvBlock(256, 512)
         self._natives = {}
+        self.precision = 'x3'
 
     def _config(self):
         cfg = _lib.SedxConfig()
@@ -251,7 +253,19 @@ class _SedModel(nn.Module):
         if nat.signature != sig:
             nat.load(self.state_dict())
             nat.signature = sig
+        if nat.precision != self.precision:
+            _lib.check(_lib.lib().sedx_set_precision(nat.h, _lib.PRECISION[self.precision]), nat.h,
+                       'set_precision')
+            nat.precision = self.precision
         return nat
+
+    def set_precision(self, mode):
+        """Conv-stack arithmetic: 'x3' (default; 3xbf16-split MFMA, fp32
+        accumulate, ~1e-6 from fp32) or 'exact' (fp32 MFMA)."""
+        if mode not in _lib.PRECISION:
+            raise ValueError('precision must be one of %s' % sorted(_lib.PRECISION))
+        self.precision = mode
+        return self
 
     def _check_eval(self, mixup_lambda, timeshift):
         if self.training:

@@ -45,9 +45,11 @@ def err(a, b):
     return float(np.max(np.abs(a - b)))
 
 
-@pytest.fixture(scope='module', params=[GRU, TRF])
+@pytest.fixture(scope='module', params=[(GRU, 'x3'), (TRF, 'x3'), (GRU, 'exact'), (TRF, 'exact')],
+                ids=['gru-x3', 'trf-x3', 'gru-exact', 'trf-exact'])
 def model(request):
-    return request.param, build(request.param)
+    mt, prec = request.param
+    return mt, build(mt).set_precision(prec)
 
 
 def test_short_clip_all_outputs(model, golden_dir):

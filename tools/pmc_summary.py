@@ -1,0 +1,60 @@
+"""Summarise a profile_round.sh run into profiles/<tag>_*.{json,md}.
+
+Per kernel: calls and average duration (rocprofv3 --kernel-trace --stats),
+average FETCH_SIZE / WRITE_SIZE per launch from the two separate --pmc passes.
+Units / gfx950 corrections per /opt/skills/guides/MI355X_MICROARCH.md §HBM:
+FETCH_SIZE and WRITE_SIZE are KiB; on gfx950 FETCH_SIZE reports exactly half
+the bytes of a wide (16 B/lane) coalesced read, so hbm_read = 2 * FETCH_SIZE
+* 1024 (both raw and corrected values are kept); WRITE_SIZE is exact for
+16-B stores.
+
+usage: python tools/pmc_summary.py gpurun_out/prof r01
+"""
+import csv
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+def short(name):
+    return name.split('(')[0].replace('void ', '').strip()
+
+
+def main(src, tag):
+    stats = list(csv.DictReader(open(os.path.join(src, 'kt', 'kt_kernel_stats.csv'))))
+    out = {}
+    for r in stats:
+        out[short(r['Name'])] = {'calls': int(r['Calls']), 'avg_ns': float(r['AverageNs']),
+                                 'pct': float(r['Percentage'])}
+    for ctr, sub in (('FETCH_SIZE', 'pmc_fetch'), ('WRITE_SIZE', 'pmc_write')):
+        acc = defaultdict(list)
+        p = os.path.join(src, sub, 'pmc_counter_collection.csv')
+        for r in csv.DictReader(open(p)):
+            if r['Counter_Name'] == ctr:
+                acc[short(r['Kernel_Name'])].append(float(r['Counter_Value']))
+        for k, v in acc.items():
+            out.setdefault(k, {})[ctr.lower() + '_kib_avg'] = sum(v) / len(v)
+    for k, v in out.items():
+        if 'fetch_size_kib_avg' in v and 'write_size_kib_avg' in v:
+            v['hbm_read_bytes_corrected'] = 2 * v['fetch_size_kib_avg'] * 1024
+            v['hbm_write_bytes'] = v['write_size_kib_avg'] * 1024
+            v['hbm_bytes_corrected'] = v['hbm_read_bytes_corrected'] + v['hbm_write_bytes']
+    os.makedirs('profiles', exist_ok=True)
+    with open(os.path.join('profiles', '%s_kernel_summary.json' % tag), 'w') as f:
+        json.dump(out, f, indent=1, sort_keys=True)
+    lines = ['| kernel | calls | avg us | % | FETCH KiB (raw) | WRITE KiB | HBM MB (corrected) |',
+             '|---|---|---|---|---|---|---|']
+    for k, v in sorted(out.items(), key=lambda kv: -kv[1].get('pct', 0)):
+        lines.append('| %s | %s | %.1f | %.2f | %s | %s | %s |' % (
+            k, v.get('calls', ''), v.get('avg_ns', 0) / 1e3, v.get('pct', 0),
+            '%.0f' % v['fetch_size_kib_avg'] if 'fetch_size_kib_avg' in v else '',
+            '%.0f' % v['write_size_kib_avg'] if 'write_size_kib_avg' in v else '',
+            '%.1f' % (v['hbm_bytes_corrected'] / 1e6) if 'hbm_bytes_corrected' in v else ''))
+    with open(os.path.join('profiles', '%s_kernel_summary.md' % tag), 'w') as f:
+        f.write('\n'.join(lines) + '\n')
+    print('\n'.join(lines))
+
+
+if __name__ == '__main__':
+    main(sys.argv[1], sys.argv[2])
