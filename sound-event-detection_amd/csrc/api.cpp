@@ -7,6 +7,7 @@
 #include <complex>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -41,6 +42,7 @@ struct DevWeights {
   float* w_ih = nullptr;   // [1536][512]
   float* b_ih = nullptr;   // [1536]
   float* whhT = nullptr;   // [2][256][768]
+  float* whh = nullptr;    // [2][768][256] (cooperative recurrence)
   float* bhh = nullptr;    // [2][768]
   float* wqkv = nullptr;   // [1536][512]
   float* bqkv = nullptr;
@@ -72,6 +74,7 @@ struct sedx_handle {
   size_t ws_bytes = 0;
   // optional per-stage timing (sedx_set_profiling): events at stage boundaries
   int precision = SEDX_PRECISION_X3;   // conv stack arithmetic (sedx_set_precision)
+  bool gru_simple = getenv("SEDX_GRU_SIMPLE") != nullptr;   // A/B: per-(clip,dir) recurrence
   bool profiling = false;
   hipEvent_t ev[SEDX_N_STAGES + 1] = {};
   bool ev_recorded[SEDX_N_STAGES + 1] = {};
@@ -197,7 +200,8 @@ WsLayout ws_layout(const sedx_handle* h, int64_t B, const Geometry& g) {
   a = std::max(a, (size_t)B * g.T2 * 16 * 256);
   a = std::max(a, (size_t)B * g.T3 * 8 * 512);
   // head scratch (after the conv stack): G/QKV + H + O + logits
-  a = std::max(a, (size_t)B * g.T3 * (1536 + 512 + 512 + h->nac) + 4 * 64);
+  a = std::max(a, (size_t)B * g.T3 * (1536 + 512 + 512 + h->nac) + 4 * 64 +
+                      gru_coop_workspace_bytes((int)B) / sizeof(float) + 64);
   l.bufA = off;
   off += align_up(a);
   size_t b = (size_t)B * g.T1 * 32 * 64;
@@ -267,7 +271,10 @@ sedx_status run_body(sedx_handle* h, int64_t B, const Geometry& g, float* ws, co
   float* LG = O + align_up((size_t)M * 512);      // [M][nac]
   if (is_gru(h)) {
     launch_linear(S, M, 512, w.w_ih, 1536, w.b_ih, G, 0, s);
-    launch_gru(G, iB, (int)g.T3, w.whhT, w.bhh, Hs, s);
+    if (h->gru_simple)
+      launch_gru(G, iB, (int)g.T3, w.whhT, w.bhh, Hs, s);
+    else
+      launch_gru_coop(G, iB, (int)g.T3, w.whh, w.bhh, Hs, LG + align_up((size_t)M * h->nac), s);
   } else {
     launch_linear(S, M, 512, w.wqkv, 1536, w.bqkv, G, 0, s);
     launch_mha(G, iB, (int)g.T3, O, s);
@@ -545,7 +552,7 @@ sedx_status sedx_finalize_weights(sedx_handle* h) {
     }
 
   // ---- head ----
-  std::vector<float> w_ih, b_ih, whhT, bhh, wqkv, bqkv, wfc, bfc;
+  std::vector<float> w_ih, b_ih, whhT, bhh, wqkv, bqkv, wfc, bfc, whh_nat;
   if (is_gru(h)) {
     w_ih.resize(1536 * 512);
     b_ih.resize(1536);
@@ -562,6 +569,7 @@ sedx_status sedx_finalize_weights(sedx_handle* h) {
       std::copy(bh.begin(), bh.end(), bhh.begin() + d * 768);
       for (int r = 0; r < 768; ++r)
         for (int k = 0; k < 256; ++k) whhT[((size_t)d * 256 + k) * 768 + r] = whh[(size_t)r * 256 + k];
+      whh_nat.insert(whh_nat.end(), whh.begin(), whh.end());
     }
   } else {
     wqkv.resize(1536 * 512);
@@ -687,6 +695,7 @@ sedx_status sedx_finalize_weights(sedx_handle* h) {
     add((void**)&W.w_ih, w_ih.data(), w_ih.size() * 4);
     add((void**)&W.b_ih, b_ih.data(), b_ih.size() * 4);
     add((void**)&W.whhT, whhT.data(), whhT.size() * 4);
+    add((void**)&W.whh, whh_nat.data(), whh_nat.size() * 4);
     add((void**)&W.bhh, bhh.data(), bhh.size() * 4);
   } else {
     add((void**)&W.wqkv, wqkv.data(), wqkv.size() * 4);

@@ -81,6 +81,13 @@ void launch_linear(const float* A, int M, int K, const float* W, int N, const fl
 void launch_gru(const float* G, int B, int T, const float* whhT, const float* bhh, float* H,
                 hipStream_t s);
 
+// Cooperative bi-GRU recurrence (8 workgroups per (32-clip group, direction)
+// exchanging h slices each step).  whh = W_hh [2][768][256] (natural layout);
+// ws >= gru_coop_workspace_bytes(B) bytes of device scratch (counters + exchange).
+size_t gru_coop_workspace_bytes(int B);
+void launch_gru_coop(const float* G, int B, int T, const float* whh, const float* bhh, float* H,
+                     void* ws, hipStream_t s);
+
 // MHA core: QKV [B][T][1536] (q|k|v, head h = cols 64h..64h+63) -> O [B][T][512]
 void launch_mha(const float* QKV, int B, int T, float* O, hipStream_t s);
 

@@ -102,6 +102,19 @@ def test_batch_invariance(model):
         assert np.array_equal(one['framewise_output'][0], full['framewise_output'][i])
 
 
+@pytest.mark.parametrize('n_clips,seconds', [(1, 1.0), (40, 1.0), (544, 0.5)])
+def test_gru_clip_groups(n_clips, seconds):
+    """Cooperative GRU: 1 group, 2 groups (ragged last), and more groups than
+    resident slots (544 clips = 17 groups of 32 > 16 slots)."""
+    m = build(GRU)
+    wave = synth.make_waveforms(n_clips, seconds=seconds, sample_rate=16000, seed=n_clips)
+    out = run(m, wave)
+    ref = O.forward(O.full_state(synth.make_state_dict(GRU, seed=0)), GRU, wave=wave)
+    e = err(out['framewise_output'], ref['framewise_output'].numpy())
+    print('GRU groups', n_clips, 'max|d| =', e)
+    assert e <= TOL
+
+
 def test_windowed_and_events(model, golden_dir):
     from sedx import inference
     mt, m = model
