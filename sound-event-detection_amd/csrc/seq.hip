@@ -137,20 +137,18 @@ void launch_gru(const float* G, int B, int T, const float* whhT, const float* bh
 // workgroups ("slices") each own 32 hidden units = 96 gate rows of W_hh,
 // kept for the whole kernel in VGPRs as bf16 hi/lo MFMA B-fragments
 // (12 waves = 3 gates x 4 K-quarters, 32 VGPRs each).  Per step:
-//   sweep h_{s-1} [32 clips x 256] as tagged 8-byte granules {tag, fp32}
-//   with sc1 loads until every tag equals the step epoch (the data IS the
-//   flag: MI355X_MICROARCH.md / cdna_hip_programming.md G16 recipe R2, one
-//   aligned 8-B sc1 store per granule, no fence, no counter) -> split to bf16
-//   hi/lo A image in LDS -> 12 MFMAs per wave (x3 split, fp32 acc) ->
-//   K-quarter partials summed in LDS -> gates (r,z,n, ATen order) -> h_s slice
-//   to H and, as granules tagged gs+1, to the parity-double-buffered exchange.
-// Double buffering is safe because a slice only publishes step gs after it has
-// swept step gs-1 from every slice, i.e. after every slice has finished
-// reading step gs-2's buffer (also at group boundaries, where the sweep still
-// runs although h is reset).  The grid is persistent over clip groups
-// (<= 16 slots x 16 WGs, all resident); the granules are zeroed by
-// hipMemsetAsync before every launch (epoch = gs + 1 is never 0); every sweep
-// is bounded and reports through *err.
+//   wait (all 8 slices published step s-1) -> gather h_{s-1} [32 x 256] with
+//   sc1 loads -> split to bf16 hi/lo A image in LDS -> 12 MFMAs per wave
+//   (x3 split, fp32 acc) -> K-quarter partials summed in LDS -> gates (r,z,n,
+//   ATen order) -> h_s slice to H and, write-through (sc1), to the exchange
+//   buffer -> every wave s_waitcnt vmcnt(0) -> barrier -> one agent-scope
+//   atomic add on the (slot, dir) counter.
+// Visibility follows MI355X_MICROARCH.md "Valid forms" row 1 (sc1 stores +
+// drained vmcnt + one atomic per workgroup; sc1 load poll; every load of the
+// exchanged bytes sc1; a barrier between the poll and the other waves' loads).
+// The grid is persistent over clip groups (<= 16 slots x 16 WGs, all
+// resident); counters are zeroed by hipMemsetAsync before every launch; every
+// spin is bounded and reports through *err.
 // ---------------------------------------------------------------------------
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 __device__ __forceinline__ uint32_t bf16_rne_s(float x) {
@@ -171,8 +169,8 @@ __device__ __forceinline__ void split8_s(const float* v, uint4& hi, uint4& lo) {
 __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__ G, int B, int T,
                                                        const float* __restrict__ whh,
                                                        const float* __restrict__ bhh,
-                                                       float* __restrict__ H,
-                                                       unsigned long long* X, unsigned* err) {
+                                                       float* __restrict__ H, float* X,
+                                                       unsigned* cnt, unsigned* err) {
   __shared__ uint4 Aimg[16 * 32 * 4];          // h_{s-1} hi/lo, [kstep][clip][4 slots]
   __shared__ float part[4][3][32][33];         // K-quarter partial gate pre-activations
   __shared__ float hprev[32][33];              // own-slice h_{s-1}
@@ -201,16 +199,17 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
   const float br = bhh[dir * 768 + 32 * p + u];
   const float bz = bhh[dir * 768 + 256 + 32 * p + u];
   const float bn = bhh[dir * 768 + 512 + 32 * p + u];
-  unsigned long long* Xs = X + (int64_t)(slot * 2 + dir) * 2 * 32 * 256;
+  unsigned* C = cnt + (slot * 2 + dir) * 16;
+  float* Xs = X + (int64_t)(slot * 2 + dir) * 2 * 32 * 256;
 
   int j = 0;
   for (int g = slot; g < ngroups; g += nslots, ++j) {
     const int c0 = g * 32;
     const int nc = min(32, B - c0);
     for (int s = 0; s < T; ++s) {
-      const int gs = j * T + s;                // global step of this slot; granule tag = gs + 1
+      const int gs = j * T + s;                // global step of this slot
       const int t = dir ? T - 1 - s : s;
-      // gate inputs of this step (independent of h): issue before the sweep
+      // gate inputs of this step (independent of h): issue before the wait
       float gi[2][3];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
@@ -225,53 +224,45 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
           gi[i][0] = gi[i][1] = gi[i][2] = 0.f;
         }
       }
-      // sweep step gs-1's granules (tag gs) of all 8 slices: 32 clips x 32 k-octets
-      float hv8[2][8];
       if (gs > 0) {
-        const unsigned long long* src = Xs + ((gs - 1) & 1) * 32 * 256;
-        unsigned spins = 0;
-        for (;;) {
-          bool ok = true;
-#pragma unroll
-          for (int i = 0; i < 2; ++i) {
-            const int it = tid + 768 * i;
-            if (it < 1024) {
-              const int c = it >> 5, oct = it & 31;
-#pragma unroll
-              for (int e = 0; e < 8; ++e) {
-                const unsigned long long w =
-                    __hip_atomic_load(src + c * 256 + 8 * oct + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                ok &= (unsigned)(w >> 32) == (unsigned)gs;
-                hv8[i][e] = __uint_as_float((uint32_t)w);
-              }
+        if (tid == 0) {
+          const unsigned target = 8u * (unsigned)gs;
+          unsigned spins = 0;
+          while (__hip_atomic_load(C, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > (1u << 24)) {
+              atomicOr(err, 1u);
+              break;
             }
           }
-          if (__syncthreads_and(ok)) break;
-          if (++spins > (1u << 22)) {
-            if (tid == 0) atomicOr(err, 1u);
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
         }
+        __syncthreads();
       }
       if (s == 0) {
         for (int i = tid; i < 16 * 32 * 4; i += 768) Aimg[i] = make_uint4(0, 0, 0, 0);
         for (int i = tid; i < 32 * 32; i += 768) hprev[i >> 5][i & 31] = 0.f;
       } else {
+        // gather h_{s-1}: 32 clips x 32 octets of k, sc1 (agent) 8-B loads
+        const float* src = Xs + ((gs - 1) & 1) * 32 * 256;
+        for (int it = tid; it < 32 * 32; it += 768) {
+          const int c = it >> 5, oct = it & 31;
+          const unsigned long long* q =
+              reinterpret_cast<const unsigned long long*>(src + c * 256 + 8 * oct);
+          float v[8];
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          const int it = tid + 768 * i;
-          if (it < 1024) {
-            const int c = it >> 5, oct = it & 31;
-            uint4 hi, lo;
-            split8_s(hv8[i], hi, lo);
-            const int ks = oct >> 1, hh = oct & 1, sw = (c >> 2) & 3;
-            Aimg[(ks * 32 + c) * 4 + (hh ^ sw)] = hi;
-            Aimg[(ks * 32 + c) * 4 + ((2 + hh) ^ sw)] = lo;
-            if ((oct >> 2) == p) {
+          for (int e = 0; e < 4; ++e) {
+            const unsigned long long w = __hip_atomic_load(q + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            v[2 * e] = __uint_as_float((uint32_t)w);
+            v[2 * e + 1] = __uint_as_float((uint32_t)(w >> 32));
+          }
+          uint4 hi, lo;
+          split8_s(v, hi, lo);
+          const int ks = oct >> 1, hh = oct & 1, sw = (c >> 2) & 3;
+          Aimg[(ks * 32 + c) * 4 + (hh ^ sw)] = hi;
+          Aimg[(ks * 32 + c) * 4 + ((2 + hh) ^ sw)] = lo;
+          if ((oct >> 2) == p) {
 #pragma unroll
-              for (int e = 0; e < 8; ++e) hprev[c][8 * (oct & 3) + e] = hv8[i][e];
-            }
+            for (int e = 0; e < 8; ++e) hprev[c][8 * (oct & 3) + e] = v[e];
           }
         }
       }
@@ -296,8 +287,8 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
       for (int r = 0; r < 16; ++r)
         part[kq][nt][(r & 3) + 8 * (r >> 2) + 4 * h][lane & 31] = acc[r];
       __syncthreads();
-      // gates, then publish h_s as tagged granules (data is the flag)
-      unsigned long long* dst = Xs + (gs & 1) * 32 * 256;
+      // gates + publish
+      float* dst = Xs + (gs & 1) * 32 * 256;
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int pr = tid + 768 * i;
@@ -314,11 +305,13 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
             hv = n + z * (hprev[c][u] - n);
             H[((int64_t)(c0 + c) * T + t) * 512 + dir * 256 + 32 * p + u] = hv;
           }
-          __hip_atomic_store(dst + c * 256 + 32 * p + u,
-                             ((unsigned long long)(unsigned)(gs + 1) << 32) | __float_as_uint(hv),
-                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(reinterpret_cast<unsigned*>(dst + c * 256 + 32 * p + u),
+                             __float_as_uint(hv), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
       }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) __hip_atomic_fetch_add(C, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
@@ -326,7 +319,7 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
 size_t gru_coop_workspace_bytes(int B) {
   const int ngroups = (B + 31) / 32;
   const int nslots = ngroups < 16 ? ngroups : 16;
-  return 256 + (size_t)nslots * 2 * 2 * 32 * 256 * 8;
+  return 256 + (size_t)nslots * 2 * 16 * 4 + (size_t)nslots * 2 * 2 * 32 * 256 * 4;
 }
 
 void launch_gru_coop(const float* G, int B, int T, const float* whh, const float* bhh, float* H,
@@ -334,11 +327,11 @@ void launch_gru_coop(const float* G, int B, int T, const float* whh, const float
   const int ngroups = (B + 31) / 32;
   const int nslots = ngroups < 16 ? ngroups : 16;
   unsigned* err = static_cast<unsigned*>(ws);
-  unsigned long long* X = reinterpret_cast<unsigned long long*>(static_cast<char*>(ws) + 256);
-  // zero the error word and every granule (no stale tag may match an epoch)
-  (void)hipMemsetAsync(ws, 0, gru_coop_workspace_bytes(B), s);
+  unsigned* cnt = err + 64;
+  float* X = reinterpret_cast<float*>(cnt + nslots * 2 * 16);
+  (void)hipMemsetAsync(ws, 0, 256 + (size_t)nslots * 2 * 16 * 4, s);
   hipLaunchKernelGGL(gru_coop_kernel, dim3(16 * nslots), dim3(768), 0, s, G, B, T, whh, bhh, H, X,
-                     err);
+                     cnt, err);
 }
 
 // ---------------------------------------------------------------------------
