@@ -77,7 +77,7 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
   constexpr int A_ITEMS = NPOS * 2;
   constexpr int NA = (A_ITEMS + 511) / 512;
 
-  __shared__ uint4 lds[2 * A_U4 + 2 * W_U4];
+  __shared__ uint4 lds[A_U4 + 9 * W_U4];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -118,7 +118,6 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
   const uint4* wbase = wsp + (int64_t)blockIdx.y * nunits * W_U4;
 
   float4 ra[NA][2];
-  uint4 rwn = make_uint4(0, 0, 0, 0);
 
 #define SEDX_LOAD_A(chunk)                                                              \
   {                                                                                     \
@@ -156,59 +155,78 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
     }                                                                                   \
   }
 
-  uint4* Abuf0 = lds;
-  uint4* Abuf1 = lds + A_U4;
-  uint4* Wslot0 = lds + 2 * A_U4;
-  uint4* Wslot1 = Wslot0 + W_U4;
-
-  // prologue
-  SEDX_LOAD_A(0);
-  SEDX_STORE_A(Abuf0);
-  if (tid < W_U4) {
-    Wslot0[tid] = wbase[tid];
-    if (nunits > 1) rwn = wbase[W_U4 + tid];
+  // LDS: one A halo image + the whole chunk's weights (9 taps); the next
+  // chunk is prefetched into registers while this one's 9 x 12 MFMAs run.
+  constexpr int WC_U4 = 9 * W_U4;
+  constexpr int NW = (WC_U4 + 511) / 512;
+  uint4* Abuf = lds;
+  uint4* Wbuf = lds + A_U4;
+  uint4 rw[NW];
+#define SEDX_LOAD_W(chunk)                                                              \
+  {                                                                                     \
+    const uint4* src_ = wbase + (int64_t)(chunk) * WC_U4;                               \
+    _Pragma("unroll") for (int i = 0; i < NW; ++i) {                                    \
+      const int idx = tid + i * 512;                                                    \
+      rw[i] = (idx < WC_U4) ? src_[idx] : make_uint4(0, 0, 0, 0);                       \
+    }                                                                                   \
   }
-  if (nchunks > 1) SEDX_LOAD_A(1);
-  __syncthreads();
+#define SEDX_STORE_W()                                                                  \
+  {                                                                                     \
+    _Pragma("unroll") for (int i = 0; i < NW; ++i) {                                    \
+      const int idx = tid + i * 512;                                                    \
+      if (idx < WC_U4) Wbuf[idx] = rw[i];                                               \
+    }                                                                                   \
+  }
 
-  for (int u = 0; u < nunits; ++u) {
-    const int chunk = u / 9;
-    const int tap = u - chunk * 9;
-    if (tid < W_U4) {
-      if (u + 1 < nunits) ((u & 1) ? Wslot0 : Wslot1)[tid] = rwn;
-      if (u + 2 < nunits) rwn = wbase[(int64_t)(u + 2) * W_U4 + tid];
-    }
-    if (tap == 0 && chunk + 1 < nchunks) {
-      uint4* An = (chunk & 1) ? Abuf0 : Abuf1;
-      SEDX_STORE_A(An);
-      if (chunk + 2 < nchunks) SEDX_LOAD_A(chunk + 2);
-    }
-    const uint4* A = (chunk & 1) ? Abuf1 : Abuf0;
-    const uint4* W = (u & 1) ? Wslot1 : Wslot0;
-    const int toff = (tap / 3) * CS + (tap % 3);
-    bf16x8 ahi[MT], alo[MT], bh[NT], bl[NT];
+  SEDX_LOAD_A(0);
+  SEDX_LOAD_W(0);
+  SEDX_STORE_A(Abuf);
+  SEDX_STORE_W();
+  __syncthreads();
+  if (nchunks > 1) {
+    SEDX_LOAD_A(1);
+    SEDX_LOAD_W(1);
+  }
+  for (int chunk = 0; chunk < nchunks; ++chunk) {
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      const int P = pbase[mt] + toff;
-      const int s = (P >> SWS) & 3;
-      ahi[mt] = as_bf16x8(A[P * 4 + (h ^ s)]);
-      alo[mt] = as_bf16x8(A[P * 4 + ((2 + h) ^ s)]);
-    }
+    for (int tap = 0; tap < 9; ++tap) {
+      const int toff = (tap / 3) * CS + (tap % 3);
+      const uint4* W = Wbuf + tap * W_U4;
+      bf16x8 ahi[MT], alo[MT], bh[NT], bl[NT];
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-      bh[nt] = as_bf16x8(W[bhi[nt]]);
-      bl[nt] = as_bf16x8(W[blo[nt]]);
-    }
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
+      for (int mt = 0; mt < MT; ++mt) {
+        const int P = pbase[mt] + toff;
+        const int s = (P >> SWS) & 3;
+        ahi[mt] = as_bf16x8(Abuf[P * 4 + (h ^ s)]);
+        alo[mt] = as_bf16x8(Abuf[P * 4 + ((2 + h) ^ s)]);
+      }
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
-        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi[mt], bh[nt], acc[mt][nt], 0, 0, 0);
-        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi[mt], bl[nt], acc[mt][nt], 0, 0, 0);
-        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(alo[mt], bh[nt], acc[mt][nt], 0, 0, 0);
+        bh[nt] = as_bf16x8(W[bhi[nt]]);
+        bl[nt] = as_bf16x8(W[blo[nt]]);
       }
-    __syncthreads();
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi[mt], bh[nt], acc[mt][nt], 0, 0, 0);
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi[mt], bl[nt], acc[mt][nt], 0, 0, 0);
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(alo[mt], bh[nt], acc[mt][nt], 0, 0, 0);
+        }
+    }
+    if (chunk + 1 < nchunks) {
+      __syncthreads();
+      SEDX_STORE_A(Abuf);
+      SEDX_STORE_W();
+      __syncthreads();
+      if (chunk + 2 < nchunks) {
+        SEDX_LOAD_A(chunk + 2);
+        SEDX_LOAD_W(chunk + 2);
+      }
+    }
   }
+#undef SEDX_LOAD_W
+#undef SEDX_STORE_W
 #undef SEDX_LOAD_A
 #undef SEDX_STORE_A
 
