@@ -68,13 +68,19 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
                                                          const uint4* __restrict__ wsp,
                                                          const float* __restrict__ bias,
                                                          float* __restrict__ out) {
-  constexpr int BM = 256, TT = BM / F, RT = TT + 2, CS = F + 2, NPOS = RT * CS;
-  constexpr int SWS = (F == 8) ? 3 : 2;
+  constexpr int BM = 256, TT = BM / F, RT = TT + 2, CS = F + 2;
+  // LDS halo image: 80-B pixel records (5 x 16 B) on rows of CSP positions;
+  // CSP per (F, epilogue) from the bank-conflict search: every
+  // ds_read_b128 of an A fragment is conflict-free and every tap offset is a
+  // compile-time immediate.
+  constexpr int CSP = (EPI == EPI_POOL2) ? (F == 64 ? 72 : F == 32 ? 40 : 24)
+                                         : (F == 64 ? 66 : F == 32 ? 34 : F == 16 ? 32 : 24);
+  constexpr int NPOS = RT * CSP;
   constexpr int WAVES_N = BN / 64, WAVES_M = 8 / WAVES_N, WM = BM / WAVES_M;
   constexpr int MT = WM / 32, NT = 2;
-  constexpr int A_U4 = NPOS * 4;
+  constexpr int A_U4 = NPOS * 5;
   constexpr int W_U4 = BN * 4;
-  constexpr int A_ITEMS = NPOS * 2;
+  constexpr int A_ITEMS = RT * CS * 2;
   constexpr int NA = (A_ITEMS + 511) / 512;
 
   __shared__ uint4 lds[A_U4 + 9 * W_U4];
@@ -93,7 +99,7 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
   for (int mt = 0; mt < MT; ++mt) {
     int tl, f;
     rowmap<F, EPI>(wm * WM + mt * 32 + (lane & 31), tl, f);
-    pbase[mt] = tl * CS + f;
+    pbase[mt] = (tl * CSP + f) * 5;
   }
   int bhi[NT], blo[NT];
 #pragma unroll
@@ -146,11 +152,12 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
       const int idx = tid + i * 512;                                                    \
       if (idx < A_ITEMS) {                                                              \
         const int pos = idx >> 1, hh = idx & 1;                                         \
-        const int s = (pos >> SWS) & 3;                                                 \
+        const int r = pos / CS, c = pos - r * CS;                                       \
+        const int rec = (r * CSP + c) * 5;                                              \
         uint4 hi, lo;                                                                   \
         split8(ra[i][0], ra[i][1], hi, lo);                                             \
-        (buf)[pos * 4 + (hh ^ s)] = hi;                                                 \
-        (buf)[pos * 4 + ((2 + hh) ^ s)] = lo;                                           \
+        (buf)[rec + hh] = hi;                                                           \
+        (buf)[rec + 2 + hh] = lo;                                                       \
       }                                                                                 \
     }                                                                                   \
   }
@@ -190,15 +197,14 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
   for (int chunk = 0; chunk < nchunks; ++chunk) {
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
-      const int toff = (tap / 3) * CS + (tap % 3);
+      const int toff = (tap / 3) * CSP + (tap % 3);
       const uint4* W = Wbuf + tap * W_U4;
       bf16x8 ahi[MT], alo[MT], bh[NT], bl[NT];
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
-        const int P = pbase[mt] + toff;
-        const int s = (P >> SWS) & 3;
-        ahi[mt] = as_bf16x8(Abuf[P * 4 + (h ^ s)]);
-        alo[mt] = as_bf16x8(Abuf[P * 4 + ((2 + h) ^ s)]);
+        const uint4* Ap = Abuf + pbase[mt] + toff * 5;
+        ahi[mt] = as_bf16x8(Ap[h]);
+        alo[mt] = as_bf16x8(Ap[2 + h]);
       }
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
