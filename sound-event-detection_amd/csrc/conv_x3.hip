@@ -195,31 +195,53 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
     SEDX_LOAD_W(1);
   }
   for (int chunk = 0; chunk < nchunks; ++chunk) {
-#pragma unroll
-    for (int tap = 0; tap < 9; ++tap) {
-      const int toff = (tap / 3) * CSP + (tap % 3);
-      const uint4* W = Wbuf + tap * W_U4;
-      bf16x8 ahi[MT], alo[MT], bh[NT], bl[NT];
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        const uint4* Ap = Abuf + pbase[mt] + toff * 5;
-        ahi[mt] = as_bf16x8(Ap[h]);
-        alo[mt] = as_bf16x8(Ap[2 + h]);
-      }
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        bh[nt] = as_bf16x8(W[bhi[nt]]);
-        bl[nt] = as_bf16x8(W[blo[nt]]);
-      }
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) {
-          acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi[mt], bh[nt], acc[mt][nt], 0, 0, 0);
-          acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi[mt], bl[nt], acc[mt][nt], 0, 0, 0);
-          acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(alo[mt], bh[nt], acc[mt][nt], 0, 0, 0);
-        }
+    // software pipeline over the 9 taps: fragments of tap t+1 are read from
+    // LDS (two register sets, static indices) while tap t's 12 MFMAs issue.
+    bf16x8 fa[2][2 * MT], fb[2][2 * NT];
+#define SEDX_READ_FRAGS(set, tap_)                                                      \
+    {                                                                                   \
+      const int toff_ = ((tap_) / 3) * CSP + ((tap_) % 3);                              \
+      const uint4* W_ = Wbuf + (tap_) * W_U4;                                           \
+      _Pragma("unroll") for (int mt = 0; mt < MT; ++mt) {                               \
+        const uint4* Ap = Abuf + pbase[mt] + toff_ * 5;                                 \
+        fa[set][2 * mt] = as_bf16x8(Ap[h]);                                             \
+        fa[set][2 * mt + 1] = as_bf16x8(Ap[2 + h]);                                     \
+      }                                                                                 \
+      _Pragma("unroll") for (int nt = 0; nt < NT; ++nt) {                               \
+        fb[set][2 * nt] = as_bf16x8(W_[bhi[nt]]);                                       \
+        fb[set][2 * nt + 1] = as_bf16x8(W_[blo[nt]]);                                   \
+      }                                                                                 \
+      __builtin_amdgcn_sched_barrier(0);                                                \
     }
+#define SEDX_MFMAS(set)                                                                 \
+    {                                                                                   \
+      _Pragma("unroll") for (int mt = 0; mt < MT; ++mt)                                 \
+      _Pragma("unroll") for (int nt = 0; nt < NT; ++nt) {                               \
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[set][2 * mt], fb[set][2 * nt], acc[mt][nt], 0, 0, 0);     \
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[set][2 * mt], fb[set][2 * nt + 1], acc[mt][nt], 0, 0, 0); \
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[set][2 * mt + 1], fb[set][2 * nt], acc[mt][nt], 0, 0, 0); \
+      }                                                                                 \
+    }
+    SEDX_READ_FRAGS(0, 0);
+    SEDX_READ_FRAGS(1, 1);
+    SEDX_MFMAS(0);
+    SEDX_READ_FRAGS(0, 2);
+    SEDX_MFMAS(1);
+    SEDX_READ_FRAGS(1, 3);
+    SEDX_MFMAS(0);
+    SEDX_READ_FRAGS(0, 4);
+    SEDX_MFMAS(1);
+    SEDX_READ_FRAGS(1, 5);
+    SEDX_MFMAS(0);
+    SEDX_READ_FRAGS(0, 6);
+    SEDX_MFMAS(1);
+    SEDX_READ_FRAGS(1, 7);
+    SEDX_MFMAS(0);
+    SEDX_READ_FRAGS(0, 8);
+    SEDX_MFMAS(1);
+    SEDX_MFMAS(0);
+#undef SEDX_READ_FRAGS
+#undef SEDX_MFMAS
     if (chunk + 1 < nchunks) {
       __syncthreads();
       SEDX_STORE_A(Abuf);
