@@ -404,39 +404,90 @@ void launch_mha(const float* QKV, int B, int T, float* O, hipStream_t s) {
 // ---------------------------------------------------------------------------
 // AttBlock finish.  grid B, block 64 (thread = class).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void att_head_kernel(const float* __restrict__ logits, int T,
-                                                      int C, int ldl, int out_frames,
-                                                      float* __restrict__ fw,
-                                                      float* __restrict__ clip,
-                                                      float* __restrict__ emb) {
-  const int b = blockIdx.x;
+__global__ __launch_bounds__(256) void att_head_kernel(const float* __restrict__ logits, int T,
+                                                       int C, int ldl, int out_frames,
+                                                       float* __restrict__ fw,
+                                                       float* __restrict__ clip,
+                                                       float* __restrict__ emb) {
+  // one clip per block; T-chunks of 128 frames staged in LDS.  Pass 1: per
+  // class sum over T of exp(clamp(att)) + 1e-6 (t order).  Pass 2: norm * cla
+  // accumulated in t order; cla kept in LDS for the framewise / embedding
+  // writes, which all 256 threads perform coalesced.
+  constexpr int TC = 128;
+  __shared__ float s_att[TC][33];
+  __shared__ float s_cla[TC][33];
+  __shared__ float s_sum[32];
+  const int b = blockIdx.x, tid = threadIdx.x;
   const float* lg = logits + (int64_t)b * T * ldl;
-  for (int c = threadIdx.x; c < C; c += 64) {
-    float sum = 0.f;
-    for (int t = 0; t < T; ++t) {
-      const float a = fminf(fmaxf(lg[(int64_t)t * ldl + c], -10.0f), 10.0f);
-      sum += expf(a) + 1e-6f;
+  // classes are processed 32 at a time (C = 25 on the reference path)
+  for (int c0 = 0; c0 < C; c0 += 32) {
+    const int nc = min(32, C - c0);
+    float sum = 0.f, acc = 0.f, last = 0.f;
+    for (int pass = 0; pass < 2; ++pass) {
+      for (int t0 = 0; t0 < T; t0 += TC) {
+        const int nt = min(TC, T - t0);
+        __syncthreads();
+        for (int i = tid; i < nt * 32; i += 256) {
+          const int t = i >> 5, c = i & 31;
+          if (c < nc) {
+            s_att[t][c] = lg[(int64_t)(t0 + t) * ldl + c0 + c];
+            s_cla[t][c] = lg[(int64_t)(t0 + t) * ldl + C + c0 + c];
+          }
+        }
+        __syncthreads();
+        if (tid < nc) {
+          const int c = tid;
+          if (pass == 0) {
+            for (int t = 0; t < nt; ++t) sum += expf(fminf(fmaxf(s_att[t][c], -10.0f), 10.0f)) + 1e-6f;
+          } else {
+            const float tot = s_sum[c];
+            for (int t = 0; t < nt; ++t) {
+              const float na = (expf(fminf(fmaxf(s_att[t][c], -10.0f), 10.0f)) + 1e-6f) / tot;
+              const float cl = sigmoidf_(s_cla[t][c]);
+              acc += na * cl;
+              s_cla[t][c] = cl;
+              last = cl;
+            }
+          }
+        }
+        if (pass == 1) {
+          __syncthreads();
+          // framewise: frames 8(t0+t) .. +7, classes c0..c0+nc
+          for (int i = tid; i < nt * 8 * nc; i += 256) {
+            const int c = i % nc, fr = i / nc;
+            const int t = fr >> 3;
+            fw[((int64_t)b * out_frames + 8 * t0 + fr) * C + c0 + c] = s_cla[t][c];
+          }
+          if (emb)
+            for (int i = tid; i < nt * nc; i += 256) {
+              const int t = i % nt, c = i / nt;
+              emb[((int64_t)b * C + c0 + c) * T + t0 + t] = s_cla[t][c];
+            }
+        }
+      }
+      if (pass == 0) {
+        if (tid < nc) s_sum[tid] = sum;
+        __syncthreads();
+      }
     }
-    float acc = 0.f, last = 0.f;
-    for (int t = 0; t < T; ++t) {
-      const float a = fminf(fmaxf(lg[(int64_t)t * ldl + c], -10.0f), 10.0f);
-      const float na = (expf(a) + 1e-6f) / sum;
-      const float cla = sigmoidf_(lg[(int64_t)t * ldl + C + c]);
-      acc += na * cla;
-      last = cla;
-      if (emb) emb[((int64_t)b * C + c) * T + t] = cla;
-      float* dst = fw + ((int64_t)b * out_frames + 8 * t) * C + c;
-#pragma unroll
-      for (int r = 0; r < 8; ++r) dst[(int64_t)r * C] = cla;
+    __syncthreads();
+    if (tid < nc) {
+      clip[(int64_t)b * C + c0 + tid] = acc;
+      s_sum[tid] = last;            // value repeated into the GRU padding frames
     }
-    for (int f = 8 * T; f < out_frames; ++f) fw[((int64_t)b * out_frames + f) * C + c] = last;
-    clip[(int64_t)b * C + c] = acc;
+    __syncthreads();
+    const int npad = out_frames - 8 * T;
+    for (int i = tid; i < npad * nc; i += 256) {
+      const int c = i % nc, f = 8 * T + i / nc;
+      fw[((int64_t)b * out_frames + f) * C + c0 + c] = s_sum[c];
+    }
+    __syncthreads();
   }
 }
 
 void launch_att_head(const float* logits, int B, int T, int C, int ldl, int out_frames,
                      float* framewise, float* clipwise, float* emb_cla, hipStream_t s) {
-  hipLaunchKernelGGL(att_head_kernel, dim3(B), dim3(64), 0, s, logits, T, C, ldl, out_frames,
+  hipLaunchKernelGGL(att_head_kernel, dim3(B), dim3(256), 0, s, logits, T, C, ldl, out_frames,
                      framewise, clipwise, emb_cla);
 }
 
