@@ -1,0 +1,285 @@
+// Cooperative bi-GRU recurrence for gfx950 (nn.GRU(512, 256, bidirectional,
+// batch_first) of Cnn_9layers_Gru_FrameAtt, pytorch/models.py:614-615, :670;
+// ATen gate order r, z, n and h' = n + z (h - n)).
+//
+// Per (clip group of 32, direction) eight workgroups ("slices") each own 32
+// hidden units = 96 gate rows of W_hh, kept for the whole kernel in VGPRs as
+// bf16 hi/lo MFMA B-fragments (12 waves = 3 gates x 4 K-quarters, 32 VGPRs
+// each).  Per step: wait until all 8 slices published h_{s-1} -> gather
+// h_{s-1} [32 x 256] with sc1 loads -> split to a bf16 hi/lo A image in LDS ->
+// 12 MFMAs per wave (x3 split, fp32 acc) -> K-quarter partials summed in LDS
+// -> gates -> publish the h_s slice.
+//
+// Two hand-off protocols, chosen once per launch:
+//  * XCD-local (fast): the grid puts the 8 slices of a (slot, dir) pair on
+//    blocks b = r + 8k (one residue r), which the dispatcher deals to one XCD.
+//    At start every slice reads HW_REG_XCC_ID and the 8 ids are exchanged
+//    with the global protocol; only if all 8 agree does the pair use plain
+//    stores (they stay in the XCD's shared L2) + s_waitcnt vmcnt(0) + a plain
+//    per-slice flag, with sc1 (L1-bypassing, L2-served) polls and loads.
+//  * global (fallback, any placement): MI355X_MICROARCH.md "Valid forms"
+//    row 1: sc1 (write-through) payload stores, s_waitcnt vmcnt(0) in every
+//    storing wave, barrier, one agent-scope atomic add per slice; sc1 poll of
+//    the counter, barrier, sc1 loads of the payload.
+// Results are identical in both modes (same arithmetic; only the transport
+// differs).  The exchange buffer is double-buffered by step parity (a slice
+// publishes step gs only after it has gathered step gs-1 from every slice,
+// i.e. after all slices finished reading step gs-2's buffer; at group
+// boundaries the wait still runs although h is reset).  Flags, counters and
+// the id table are zeroed by hipMemsetAsync before every launch; every spin is
+// bounded and reports through *err.
+#include "sedx_internal.h"
+
+namespace sedx {
+
+typedef float f32x16_g __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8_g __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ uint32_t g_bf16_rne(float x) {
+  const uint32_t u = __float_as_uint(x);
+  return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
+}
+__device__ __forceinline__ void g_split8(const float* v, uint4& hi, uint4& lo) {
+  uint32_t hh[8], ll[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    hh[i] = g_bf16_rne(v[i]);
+    ll[i] = g_bf16_rne(v[i] - __uint_as_float(hh[i] << 16));
+  }
+  hi = make_uint4(hh[0] | (hh[1] << 16), hh[2] | (hh[3] << 16), hh[4] | (hh[5] << 16), hh[6] | (hh[7] << 16));
+  lo = make_uint4(ll[0] | (ll[1] << 16), ll[2] | (ll[3] << 16), ll[4] | (ll[5] << 16), ll[6] | (ll[7] << 16));
+}
+__device__ __forceinline__ float g_sigmoid(float x) { return 1.0f / (1.0f + expf(-x)); }
+__device__ __forceinline__ unsigned g_ld(const unsigned* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // sc1
+}
+
+constexpr int GRU_MAX_SLOTS = 4;      // 2 * slots (slot, dir) pairs on 8 XCD residues
+constexpr unsigned GRU_SPIN = 1u << 24;
+
+struct GruSync {                      // zeroed every launch
+  unsigned err;
+  unsigned pad0[63];
+  unsigned ready[8][16];              // per pair: id-exchange arrivals
+  unsigned xcc[8][16];                // per pair: slice XCC ids (+1)
+  unsigned cnt[8][16];                // per pair: global-protocol step counter
+  unsigned flag[8][8][16];            // per pair, per slice: fast-protocol step flag
+};
+
+__global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__ G, int B, int T,
+                                                       const float* __restrict__ whh,
+                                                       const float* __restrict__ bhh,
+                                                       float* __restrict__ H, float* X,
+                                                       GruSync* sync, int nslots, int allow_fast) {
+  __shared__ uint4 Aimg[16 * 32 * 4];          // h_{s-1} hi/lo, [kstep][clip][4 slots]
+  __shared__ float part[4][3][32][33];         // K-quarter partial gate pre-activations
+  __shared__ float hprev[32][33];              // own-slice h_{s-1}
+  __shared__ int s_fast;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int pair = blockIdx.x & 7;             // dispatch residue -> one XCD (observed)
+  const int p = blockIdx.x >> 3;               // slice 0..7
+  const int slot = pair >> 1, dir = pair & 1;
+  if (slot >= nslots) return;                  // whole workgroup exits (uniform)
+  const int nt = wave % 3, kq = wave / 3, h = lane >> 5;
+  const int ngroups = (B + 31) / 32;
+
+  // ---- placement check (global protocol) ----
+  if (tid == 0) {
+    unsigned xid;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xid));
+    __hip_atomic_store(&sync->xcc[pair][p], (xid & 0xffu) + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_fetch_add(&sync->ready[pair][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned spins = 0;
+    while (g_ld(&sync->ready[pair][0]) < 8u) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > GRU_SPIN) {
+        atomicOr(&sync->err, 1u);
+        break;
+      }
+    }
+    int fast = allow_fast;
+    const unsigned x0 = g_ld(&sync->xcc[pair][0]);
+    for (int i = 1; i < 8; ++i) fast &= (g_ld(&sync->xcc[pair][i]) == x0);
+    s_fast = fast;
+  }
+  __syncthreads();
+  const bool fast = s_fast != 0;
+
+  // W_hh slice -> B fragments: B[k][n] = W_hh[gate row n][k]
+  bf16x8_g Bhi[4], Blo[4];
+  {
+    const float* wrow = whh + ((int64_t)dir * 768 + nt * 256 + 32 * p + (lane & 31)) * 256;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const float4* q = reinterpret_cast<const float4*>(wrow + 16 * (4 * kq + ks) + 8 * h);
+      const float4 a = q[0], b = q[1];
+      const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+      uint4 hi, lo;
+      g_split8(v, hi, lo);
+      Bhi[ks] = __builtin_bit_cast(bf16x8_g, hi);
+      Blo[ks] = __builtin_bit_cast(bf16x8_g, lo);
+    }
+  }
+  const int u = tid & 31;                      // gate-phase unit (768 % 32 == 0)
+  const float br = bhh[dir * 768 + 32 * p + u];
+  const float bz = bhh[dir * 768 + 256 + 32 * p + u];
+  const float bn = bhh[dir * 768 + 512 + 32 * p + u];
+  float* Xs = X + (int64_t)pair * 2 * 32 * 256;
+  unsigned* C = &sync->cnt[pair][0];
+  unsigned* Fl = &sync->flag[pair][0][0];
+
+  int j = 0;
+  for (int g = slot; g < ngroups; g += nslots, ++j) {
+    const int c0 = g * 32;
+    const int nc = min(32, B - c0);
+    for (int s = 0; s < T; ++s) {
+      const int gs = j * T + s;                // step of this pair; flags/counts are gs-based
+      const int t = dir ? T - 1 - s : s;
+      float gi[2][3];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int pr = tid + 768 * i;
+        const int c = pr >> 5;
+        if (pr < 1024 && c < nc) {
+          const float* gp = G + ((int64_t)(c0 + c) * T + t) * 1536 + dir * 768 + 32 * p + u;
+          gi[i][0] = gp[0];
+          gi[i][1] = gp[256];
+          gi[i][2] = gp[512];
+        } else {
+          gi[i][0] = gi[i][1] = gi[i][2] = 0.f;
+        }
+      }
+      if (gs > 0) {
+        if (fast) {
+          if (tid < 8) {
+            unsigned spins = 0;
+            while (g_ld(Fl + tid * 16) < (unsigned)gs) {
+              if (++spins > GRU_SPIN) {
+                atomicOr(&sync->err, 2u);
+                break;
+              }
+            }
+          }
+        } else if (tid == 0) {
+          const unsigned target = 8u * (unsigned)gs;
+          unsigned spins = 0;
+          while (g_ld(C) < target) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > GRU_SPIN) {
+              atomicOr(&sync->err, 1u);
+              break;
+            }
+          }
+        }
+        __syncthreads();
+      }
+      if (s == 0) {
+        for (int i = tid; i < 16 * 32 * 4; i += 768) Aimg[i] = make_uint4(0, 0, 0, 0);
+        for (int i = tid; i < 32 * 32; i += 768) hprev[i >> 5][i & 31] = 0.f;
+      } else {
+        const float* src = Xs + ((gs - 1) & 1) * 32 * 256;
+        for (int it = tid; it < 32 * 32; it += 768) {
+          const int c = it >> 5, oct = it & 31;
+          const unsigned long long* q =
+              reinterpret_cast<const unsigned long long*>(src + c * 256 + 8 * oct);
+          float v[8];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const unsigned long long w = __hip_atomic_load(q + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            v[2 * e] = __uint_as_float((uint32_t)w);
+            v[2 * e + 1] = __uint_as_float((uint32_t)(w >> 32));
+          }
+          uint4 hi, lo;
+          g_split8(v, hi, lo);
+          const int ks = oct >> 1, hh = oct & 1, sw = (c >> 2) & 3;
+          Aimg[(ks * 32 + c) * 4 + (hh ^ sw)] = hi;
+          Aimg[(ks * 32 + c) * 4 + ((2 + hh) ^ sw)] = lo;
+          if ((oct >> 2) == p) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) hprev[c][8 * (oct & 3) + e] = v[e];
+          }
+        }
+      }
+      __syncthreads();
+      f32x16_g acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+      {
+        const int c = lane & 31, sw = (c >> 2) & 3;
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+          const int kk = 4 * kq + ks;
+          const bf16x8_g ahi = __builtin_bit_cast(bf16x8_g, Aimg[(kk * 32 + c) * 4 + (h ^ sw)]);
+          const bf16x8_g alo = __builtin_bit_cast(bf16x8_g, Aimg[(kk * 32 + c) * 4 + ((2 + h) ^ sw)]);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi, Bhi[ks], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi, Blo[ks], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(alo, Bhi[ks], acc, 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        part[kq][nt][(r & 3) + 8 * (r >> 2) + 4 * h][lane & 31] = acc[r];
+      __syncthreads();
+      float* dst = Xs + (gs & 1) * 32 * 256;
+      float hvs[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int pr = tid + 768 * i;
+        hvs[i] = 0.f;
+        if (pr < 1024) {
+          const int c = pr >> 5;
+          if (c < nc) {
+            const float ghr = (((part[0][0][c][u] + part[1][0][c][u]) + part[2][0][c][u]) + part[3][0][c][u]) + br;
+            const float ghz = (((part[0][1][c][u] + part[1][1][c][u]) + part[2][1][c][u]) + part[3][1][c][u]) + bz;
+            const float ghn = (((part[0][2][c][u] + part[1][2][c][u]) + part[2][2][c][u]) + part[3][2][c][u]) + bn;
+            const float r = g_sigmoid(gi[i][0] + ghr);
+            const float z = g_sigmoid(gi[i][1] + ghz);
+            const float n = tanhf(gi[i][2] + r * ghn);
+            hvs[i] = n + z * (hprev[c][u] - n);
+          }
+          float* xp = dst + c * 256 + 32 * p + u;
+          if (fast)
+            *xp = hvs[i];
+          else
+            __hip_atomic_store(reinterpret_cast<unsigned*>(xp), __float_as_uint(hvs[i]),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        if (fast)
+          *reinterpret_cast<volatile unsigned*>(Fl + p * 16) = (unsigned)(gs + 1);
+        else
+          __hip_atomic_fetch_add(C, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      // the H output is not part of the hand-off: store it after the publish
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int pr = tid + 768 * i;
+        const int c = pr >> 5;
+        if (pr < 1024 && c < nc) H[((int64_t)(c0 + c) * T + t) * 512 + dir * 256 + 32 * p + u] = hvs[i];
+      }
+    }
+  }
+}
+
+size_t gru_coop_workspace_bytes(int B) {
+  (void)B;
+  return ((sizeof(GruSync) + 255) & ~size_t(255)) + (size_t)8 * 2 * 32 * 256 * 4;
+}
+
+void launch_gru_coop(const float* G, int B, int T, const float* whh, const float* bhh, float* H,
+                     void* ws, hipStream_t s) {
+  const int ngroups = (B + 31) / 32;
+  const int nslots = ngroups < GRU_MAX_SLOTS ? ngroups : GRU_MAX_SLOTS;
+  GruSync* sync = static_cast<GruSync*>(ws);
+  float* X = reinterpret_cast<float*>(static_cast<char*>(ws) + ((sizeof(GruSync) + 255) & ~size_t(255)));
+  const int allow_fast = getenv("SEDX_GRU_GLOBAL_ONLY") ? 0 : 1;   // A/B switch
+  (void)hipMemsetAsync(sync, 0, sizeof(GruSync), s);
+  hipLaunchKernelGGL(gru_coop_kernel, dim3(64), dim3(768), 0, s, G, B, T, whh, bhh, H, X, sync,
+                     nslots, allow_fast);
+}
+
+}  // namespace sedx

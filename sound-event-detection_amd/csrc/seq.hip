@@ -132,207 +132,7 @@ void launch_gru(const float* G, int B, int T, const float* whhT, const float* bh
   hipLaunchKernelGGL(gru_kernel, dim3(B, 2), dim3(256), 0, s, G, T, whhT, bhh, H);
 }
 
-// ---------------------------------------------------------------------------
-// Cooperative bi-GRU recurrence.  Per (clip group of 32, direction) eight
-// workgroups ("slices") each own 32 hidden units = 96 gate rows of W_hh,
-// kept for the whole kernel in VGPRs as bf16 hi/lo MFMA B-fragments
-// (12 waves = 3 gates x 4 K-quarters, 32 VGPRs each).  Per step:
-//   wait (all 8 slices published step s-1) -> gather h_{s-1} [32 x 256] with
-//   sc1 loads -> split to bf16 hi/lo A image in LDS -> 12 MFMAs per wave
-//   (x3 split, fp32 acc) -> K-quarter partials summed in LDS -> gates (r,z,n,
-//   ATen order) -> h_s slice to H and, write-through (sc1), to the exchange
-//   buffer -> every wave s_waitcnt vmcnt(0) -> barrier -> one agent-scope
-//   atomic add on the (slot, dir) counter.
-// Visibility follows MI355X_MICROARCH.md "Valid forms" row 1 (sc1 stores +
-// drained vmcnt + one atomic per workgroup; sc1 load poll; every load of the
-// exchanged bytes sc1; a barrier between the poll and the other waves' loads).
-// The grid is persistent over clip groups (<= 16 slots x 16 WGs, all
-// resident); counters are zeroed by hipMemsetAsync before every launch; every
-// spin is bounded and reports through *err.
-// ---------------------------------------------------------------------------
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-__device__ __forceinline__ uint32_t bf16_rne_s(float x) {
-  const uint32_t u = __float_as_uint(x);
-  return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
-}
-__device__ __forceinline__ void split8_s(const float* v, uint4& hi, uint4& lo) {
-  uint32_t hh[8], ll[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    hh[i] = bf16_rne_s(v[i]);
-    ll[i] = bf16_rne_s(v[i] - __uint_as_float(hh[i] << 16));
-  }
-  hi = make_uint4(hh[0] | (hh[1] << 16), hh[2] | (hh[3] << 16), hh[4] | (hh[5] << 16), hh[6] | (hh[7] << 16));
-  lo = make_uint4(ll[0] | (ll[1] << 16), ll[2] | (ll[3] << 16), ll[4] | (ll[5] << 16), ll[6] | (ll[7] << 16));
-}
-
-__global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__ G, int B, int T,
-                                                       const float* __restrict__ whh,
-                                                       const float* __restrict__ bhh,
-                                                       float* __restrict__ H, float* X,
-                                                       unsigned* cnt, unsigned* err) {
-  __shared__ uint4 Aimg[16 * 32 * 4];          // h_{s-1} hi/lo, [kstep][clip][4 slots]
-  __shared__ float part[4][3][32][33];         // K-quarter partial gate pre-activations
-  __shared__ float hprev[32][33];              // own-slice h_{s-1}
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int p = blockIdx.x & 7, dir = (blockIdx.x >> 3) & 1, slot = blockIdx.x >> 4;
-  const int nslots = gridDim.x >> 4;
-  const int nt = wave % 3, kq = wave / 3, h = lane >> 5;
-  const int ngroups = (B + 31) / 32;
-
-  // W_hh slice -> B fragments: B[k][n] = W_hh[gate row n][k]
-  bf16x8 Bhi[4], Blo[4];
-  {
-    const float* wrow = whh + ((int64_t)dir * 768 + nt * 256 + 32 * p + (lane & 31)) * 256;
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      const float4* q = reinterpret_cast<const float4*>(wrow + 16 * (4 * kq + ks) + 8 * h);
-      const float4 a = q[0], b = q[1];
-      const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-      uint4 hi, lo;
-      split8_s(v, hi, lo);
-      Bhi[ks] = __builtin_bit_cast(bf16x8, hi);
-      Blo[ks] = __builtin_bit_cast(bf16x8, lo);
-    }
-  }
-  const int u = tid & 31;                      // gate-phase unit (768 % 32 == 0)
-  const float br = bhh[dir * 768 + 32 * p + u];
-  const float bz = bhh[dir * 768 + 256 + 32 * p + u];
-  const float bn = bhh[dir * 768 + 512 + 32 * p + u];
-  unsigned* C = cnt + (slot * 2 + dir) * 16;
-  float* Xs = X + (int64_t)(slot * 2 + dir) * 2 * 32 * 256;
-
-  int j = 0;
-  for (int g = slot; g < ngroups; g += nslots, ++j) {
-    const int c0 = g * 32;
-    const int nc = min(32, B - c0);
-    for (int s = 0; s < T; ++s) {
-      const int gs = j * T + s;                // global step of this slot
-      const int t = dir ? T - 1 - s : s;
-      // gate inputs of this step (independent of h): issue before the wait
-      float gi[2][3];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int pr = tid + 768 * i;
-        const int c = pr >> 5;
-        if (pr < 1024 && c < nc) {
-          const float* gp = G + ((int64_t)(c0 + c) * T + t) * 1536 + dir * 768 + 32 * p + u;
-          gi[i][0] = gp[0];
-          gi[i][1] = gp[256];
-          gi[i][2] = gp[512];
-        } else {
-          gi[i][0] = gi[i][1] = gi[i][2] = 0.f;
-        }
-      }
-      if (gs > 0) {
-        if (tid == 0) {
-          const unsigned target = 8u * (unsigned)gs;
-          unsigned spins = 0;
-          while (__hip_atomic_load(C, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-            __builtin_amdgcn_s_sleep(1);
-            if (++spins > (1u << 24)) {
-              atomicOr(err, 1u);
-              break;
-            }
-          }
-        }
-        __syncthreads();
-      }
-      if (s == 0) {
-        for (int i = tid; i < 16 * 32 * 4; i += 768) Aimg[i] = make_uint4(0, 0, 0, 0);
-        for (int i = tid; i < 32 * 32; i += 768) hprev[i >> 5][i & 31] = 0.f;
-      } else {
-        // gather h_{s-1}: 32 clips x 32 octets of k, sc1 (agent) 8-B loads
-        const float* src = Xs + ((gs - 1) & 1) * 32 * 256;
-        for (int it = tid; it < 32 * 32; it += 768) {
-          const int c = it >> 5, oct = it & 31;
-          const unsigned long long* q =
-              reinterpret_cast<const unsigned long long*>(src + c * 256 + 8 * oct);
-          float v[8];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const unsigned long long w = __hip_atomic_load(q + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            v[2 * e] = __uint_as_float((uint32_t)w);
-            v[2 * e + 1] = __uint_as_float((uint32_t)(w >> 32));
-          }
-          uint4 hi, lo;
-          split8_s(v, hi, lo);
-          const int ks = oct >> 1, hh = oct & 1, sw = (c >> 2) & 3;
-          Aimg[(ks * 32 + c) * 4 + (hh ^ sw)] = hi;
-          Aimg[(ks * 32 + c) * 4 + ((2 + hh) ^ sw)] = lo;
-          if ((oct >> 2) == p) {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) hprev[c][8 * (oct & 3) + e] = v[e];
-          }
-        }
-      }
-      __syncthreads();
-      // recurrent GEMM partial: 32 clips x 32 rows (gate nt) over K quarter kq
-      f32x16 acc;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-      {
-        const int c = lane & 31, sw = (c >> 2) & 3;
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) {
-          const int kk = 4 * kq + ks;
-          const bf16x8 ahi = __builtin_bit_cast(bf16x8, Aimg[(kk * 32 + c) * 4 + (h ^ sw)]);
-          const bf16x8 alo = __builtin_bit_cast(bf16x8, Aimg[(kk * 32 + c) * 4 + ((2 + h) ^ sw)]);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi, Bhi[ks], acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi, Blo[ks], acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(alo, Bhi[ks], acc, 0, 0, 0);
-        }
-      }
-#pragma unroll
-      for (int r = 0; r < 16; ++r)
-        part[kq][nt][(r & 3) + 8 * (r >> 2) + 4 * h][lane & 31] = acc[r];
-      __syncthreads();
-      // gates + publish
-      float* dst = Xs + (gs & 1) * 32 * 256;
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int pr = tid + 768 * i;
-        if (pr < 1024) {
-          const int c = pr >> 5;
-          float hv = 0.f;
-          if (c < nc) {
-            const float ghr = (((part[0][0][c][u] + part[1][0][c][u]) + part[2][0][c][u]) + part[3][0][c][u]) + br;
-            const float ghz = (((part[0][1][c][u] + part[1][1][c][u]) + part[2][1][c][u]) + part[3][1][c][u]) + bz;
-            const float ghn = (((part[0][2][c][u] + part[1][2][c][u]) + part[2][2][c][u]) + part[3][2][c][u]) + bn;
-            const float r = sigmoidf_(gi[i][0] + ghr);
-            const float z = sigmoidf_(gi[i][1] + ghz);
-            const float n = tanhf(gi[i][2] + r * ghn);
-            hv = n + z * (hprev[c][u] - n);
-            H[((int64_t)(c0 + c) * T + t) * 512 + dir * 256 + 32 * p + u] = hv;
-          }
-          __hip_atomic_store(reinterpret_cast<unsigned*>(dst + c * 256 + 32 * p + u),
-                             __float_as_uint(hv), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0) __hip_atomic_fetch_add(C, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
-
-size_t gru_coop_workspace_bytes(int B) {
-  const int ngroups = (B + 31) / 32;
-  const int nslots = ngroups < 16 ? ngroups : 16;
-  return 256 + (size_t)nslots * 2 * 16 * 4 + (size_t)nslots * 2 * 2 * 32 * 256 * 4;
-}
-
-void launch_gru_coop(const float* G, int B, int T, const float* whh, const float* bhh, float* H,
-                     void* ws, hipStream_t s) {
-  const int ngroups = (B + 31) / 32;
-  const int nslots = ngroups < 16 ? ngroups : 16;
-  unsigned* err = static_cast<unsigned*>(ws);
-  unsigned* cnt = err + 64;
-  float* X = reinterpret_cast<float*>(cnt + nslots * 2 * 16);
-  (void)hipMemsetAsync(ws, 0, 256 + (size_t)nslots * 2 * 16 * 4, s);
-  hipLaunchKernelGGL(gru_coop_kernel, dim3(16 * nslots), dim3(768), 0, s, G, B, T, whh, bhh, H, X,
-                     cnt, err);
-}
+// (the cooperative multi-CU recurrence lives in gru.hip)
 
 // ---------------------------------------------------------------------------
 // MHA core.  grid (ceil(T/128), B*8); thread = query row.

@@ -115,6 +115,28 @@ def test_gru_clip_groups(n_clips, seconds):
     assert e <= TOL
 
 
+def test_gru_handoff_modes_bit_identical():
+    """XCD-local and global GRU hand-off protocols move the same bytes: the
+    outputs must be bit-identical (and the faster one is used by default)."""
+    import time
+    m = build(GRU)
+    wave = synth.make_waveforms(32, seconds=10.0, sample_rate=16000, seed=8)
+    outs, times = {}, {}
+    for mode in ('global', 'auto'):
+        if mode == 'global':
+            os.environ['SEDX_GRU_GLOBAL_ONLY'] = '1'
+        else:
+            os.environ.pop('SEDX_GRU_GLOBAL_ONLY', None)
+        run(m, wave)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        outs[mode] = run(m, wave)['framewise_output']
+        times[mode] = time.perf_counter() - t0
+    print('GRU hand-off: global %.3f ms, auto %.3f ms (whole forward)' %
+          (times['global'] * 1e3, times['auto'] * 1e3))
+    assert np.array_equal(outs['global'], outs['auto'])
+
+
 def test_windowed_and_events(model, golden_dir):
     from sedx import inference
     mt, m = model
