@@ -64,7 +64,19 @@ struct GruSync {                      // zeroed every launch
   unsigned xcc[8][16];                // per pair: slice XCC ids (+1)
   unsigned cnt[8][16];                // per pair: global-protocol step counter
   unsigned flag[8][8][16];            // per pair, per slice: fast-protocol step flag
+  unsigned long long stamps[8];       // SEDX_GRU_STAMPS diagnostic builds only
+  unsigned mode;                      // 1 = XCD-local protocol was used by pair 0
 };
+#ifdef SEDX_GRU_STAMPS
+#define GRU_STAMP(i)                                                                    \
+  if (tid == 0 && pair == 0 && p == 0) {                                                \
+    const unsigned long long now_ = __builtin_amdgcn_s_memtime();                       \
+    st_acc[i] += now_ - st_last;                                                        \
+    st_last = now_;                                                                     \
+  }
+#else
+#define GRU_STAMP(i)
+#endif
 
 __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__ G, int B, int T,
                                                        const float* __restrict__ whh,
@@ -105,6 +117,11 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
   }
   __syncthreads();
   const bool fast = s_fast != 0;
+  if (tid == 0 && pair == 0 && p == 0) sync->mode = fast ? 1u : 0u;
+#ifdef SEDX_GRU_STAMPS
+  unsigned long long st_acc[4] = {0, 0, 0, 0};
+  unsigned long long st_last = __builtin_amdgcn_s_memtime();
+#endif
 
   // W_hh slice -> B fragments: B[k][n] = W_hh[gate row n][k]
   bf16x8_g Bhi[4], Blo[4];
@@ -174,6 +191,7 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
         }
         __syncthreads();
       }
+      GRU_STAMP(0);
       if (s == 0) {
         for (int i = tid; i < 16 * 32 * 4; i += 768) Aimg[i] = make_uint4(0, 0, 0, 0);
         for (int i = tid; i < 32 * 32; i += 768) hprev[i >> 5][i & 31] = 0.f;
@@ -202,6 +220,7 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
         }
       }
       __syncthreads();
+      GRU_STAMP(1);
       f32x16_g acc;
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[r] = 0.f;
@@ -221,6 +240,7 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
       for (int r = 0; r < 16; ++r)
         part[kq][nt][(r & 3) + 8 * (r >> 2) + 4 * h][lane & 31] = acc[r];
       __syncthreads();
+      GRU_STAMP(2);
       float* dst = Xs + (gs & 1) * 32 * 256;
       float hvs[2];
 #pragma unroll
@@ -254,6 +274,7 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
         else
           __hip_atomic_fetch_add(C, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
+      GRU_STAMP(3);
       // the H output is not part of the hand-off: store it after the publish
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
@@ -263,6 +284,10 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
       }
     }
   }
+#ifdef SEDX_GRU_STAMPS
+  if (tid == 0 && pair == 0 && p == 0)
+    for (int i = 0; i < 4; ++i) sync->stamps[i] = st_acc[i];
+#endif
 }
 
 size_t gru_coop_workspace_bytes(int B) {

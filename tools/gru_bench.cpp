@@ -1,0 +1,59 @@
+// Stand-alone micro-benchmark of the cooperative GRU recurrence
+// (diagnostic build with -DSEDX_GRU_STAMPS: per-phase s_memtime sums of
+// workgroup (pair 0, slice 0)).  Build: see tools/gpu_gru_bench.sh
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#include "../sound-event-detection_amd/csrc/sedx_internal.h"
+
+struct Sync {                         // must mirror GruSync in gru.hip
+  unsigned err;
+  unsigned pad0[63];
+  unsigned ready[8][16];
+  unsigned xcc[8][16];
+  unsigned cnt[8][16];
+  unsigned flag[8][8][16];
+  unsigned long long stamps[8];
+  unsigned mode;
+};
+
+int main(int argc, char** argv) {
+  const int B = argc > 1 ? atoi(argv[1]) : 32, T = argc > 2 ? atoi(argv[2]) : 125;
+  const int reps = 20;
+  std::vector<float> hG((size_t)B * T * 1536), hw(2 * 768 * 256), hb(2 * 768);
+  srand(1);
+  for (auto& v : hG) v = (rand() / (float)RAND_MAX - 0.5f);
+  for (auto& v : hw) v = (rand() / (float)RAND_MAX - 0.5f) * 0.1f;
+  for (auto& v : hb) v = (rand() / (float)RAND_MAX - 0.5f) * 0.1f;
+  float *G, *W, *Bb, *H;
+  void* ws;
+  hipMalloc(&G, hG.size() * 4); hipMalloc(&W, hw.size() * 4); hipMalloc(&Bb, hb.size() * 4);
+  hipMalloc(&H, (size_t)B * T * 512 * 4);
+  const size_t wsb = sedx::gru_coop_workspace_bytes(B);
+  hipMalloc(&ws, wsb);
+  hipMemcpy(G, hG.data(), hG.size() * 4, hipMemcpyHostToDevice);
+  hipMemcpy(W, hw.data(), hw.size() * 4, hipMemcpyHostToDevice);
+  hipMemcpy(Bb, hb.data(), hb.size() * 4, hipMemcpyHostToDevice);
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0); hipEventCreate(&e1);
+  for (int mode = 0; mode < 2; ++mode) {
+    if (mode == 0) setenv("SEDX_GRU_GLOBAL_ONLY", "1", 1); else unsetenv("SEDX_GRU_GLOBAL_ONLY");
+    sedx::launch_gru_coop(G, B, T, W, Bb, H, ws, 0);
+    hipDeviceSynchronize();
+    hipEventRecord(e0, 0);
+    for (int r = 0; r < reps; ++r) sedx::launch_gru_coop(G, B, T, W, Bb, H, ws, 0);
+    hipEventRecord(e1, 0);
+    hipEventSynchronize(e1);
+    float ms = 0;
+    hipEventElapsedTime(&ms, e0, e1);
+    Sync sy;
+    hipMemcpy(&sy, ws, sizeof(Sync), hipMemcpyDeviceToHost);
+    const double tot = (double)(sy.stamps[0] + sy.stamps[1] + sy.stamps[2] + sy.stamps[3]);
+    printf("%s: mode=%u err=%u  %.3f ms/launch  %.2f us/step | wait %.0f%% gather %.0f%% mfma %.0f%% gates+publish %.0f%% (s_memtime ticks/step %.0f)\n",
+           mode ? "auto" : "global", sy.mode, sy.err, ms / reps, ms / reps * 1e3 / T,
+           100 * sy.stamps[0] / tot, 100 * sy.stamps[1] / tot, 100 * sy.stamps[2] / tot,
+           100 * sy.stamps[3] / tot, tot / T);
+  }
+  return 0;
+}
