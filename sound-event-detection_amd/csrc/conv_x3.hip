@@ -6,17 +6,28 @@
 // 16/3 the fp32-MFMA rate.  Same data layout and epilogues as conv.hip
 // (ConvBlock, pytorch/models.py:98-141).
 //
-// Block = 512 threads (8 waves), output tile 256 pixels x BN channels,
-// wave tile 64x64 (BN=128) or 32x64 (BN=64).  K loop = (16-channel chunk,
-// tap) units.  Per chunk the (TT+2) x (F+2) halo of the fp32 input is loaded
-// to registers, split to bf16 hi/lo and written once to LDS as 64-B pixel
-// records [hi k0-7 | hi k8-15 | lo k0-7 | lo k8-15] with the 16-B slots
-// XOR-swizzled by position (conflict analysis: DESIGN.md); all 9 taps read it
-// with shifted positions.  Weights are pre-split + pre-swizzled on the host
-// in the exact LDS image, [ntile][chunk][tap][BN][64 B], and streamed one
-// (chunk, tap) unit at a time through a 2-slot LDS ring, prefetched two units
-// ahead in registers.  The MFMA row -> pixel map is chosen per epilogue so
-// that 2x2 pooling (and the 8-bin freq mean) is an in-lane register sum.
+// Block = 512 threads (8 waves, wave tile 64 x 64), output tile BM pixels x
+// BN channels (256 x 128, or 512 x 64 for the 64-channel layer).  K loop =
+// 16-channel chunks x 9 taps.  Per chunk the (TT+2) x (F+2) halo of the fp32
+// input is split to bf16 hi/lo and written once to LDS as 80-B pixel records
+// [hi k0-7 | hi k8-15 | lo k0-7 | lo k8-15 | pad]; all 9 taps read it with
+// shifted positions (row stride CSP chosen per shape so every A-fragment
+// ds_read_b128 is bank-conflict-free and every tap offset is an immediate).
+// Weights are pre-split + pre-swizzled on the host in the exact LDS image,
+// [ntile][chunk][tap][BN][64 B].
+//
+// Pipeline (persistent workgroups, one per resident slot):
+//   * A halo images are double-buffered per chunk;
+//   * weights stream in stages of one kernel row (3 taps) through a 2-slot
+//     LDS ring;
+//   * one barrier per stage; after it each thread writes the stage-after-next
+//     weights and (once per chunk) the next chunk's halo from registers, then
+//     issues the global loads that refill those registers, while the MFMAs of
+//     the current stage keep the matrix pipes busy;
+//   * A/B fragments of tap t+1 are read from LDS (two register sets) while
+//     tap t's 12 MFMAs issue, across stage, chunk and tile boundaries.
+// The MFMA row -> pixel map is chosen per epilogue so that 2x2 pooling (and
+// the 8-bin freq mean) is an in-lane register sum.
 #include "sedx_internal.h"
 
 namespace sedx {
@@ -24,26 +35,28 @@ namespace sedx {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
-__device__ __forceinline__ uint32_t bf16_rne(float x) {
-  const uint32_t u = __float_as_uint(x);
-  return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+// hi = bf16_rne(x), lo = bf16_rne(x - hi): v_cvt_pk_bf16_f32 (RNE) per pair
+__device__ __forceinline__ void split2(float x0, float x1, uint32_t& hi, uint32_t& lo) {
+  const bf16x2 h = {(__bf16)x0, (__bf16)x1};
+  hi = __builtin_bit_cast(uint32_t, h);
+  const float r0 = x0 - __uint_as_float(hi << 16);
+  const float r1 = x1 - __uint_as_float(hi & 0xFFFF0000u);
+  const bf16x2 l = {(__bf16)r0, (__bf16)r1};
+  lo = __builtin_bit_cast(uint32_t, l);
 }
 
 __device__ __forceinline__ void split8(const float4 a, const float4 b, uint4& hi, uint4& lo) {
-  const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-  uint32_t hh[8], ll[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    hh[i] = bf16_rne(v[i]);
-    ll[i] = bf16_rne(v[i] - __uint_as_float(hh[i] << 16));
-  }
-  hi = make_uint4(hh[0] | (hh[1] << 16), hh[2] | (hh[3] << 16), hh[4] | (hh[5] << 16), hh[6] | (hh[7] << 16));
-  lo = make_uint4(ll[0] | (ll[1] << 16), ll[2] | (ll[3] << 16), ll[4] | (ll[5] << 16), ll[6] | (ll[7] << 16));
+  split2(a.x, a.y, hi.x, lo.x);
+  split2(a.z, a.w, hi.y, lo.y);
+  split2(b.x, b.y, hi.z, lo.z);
+  split2(b.z, b.w, hi.w, lo.w);
 }
 
 __device__ __forceinline__ bf16x8 as_bf16x8(uint4 v) { return __builtin_bit_cast(bf16x8, v); }
 
-// MFMA row R (0..255 of the block tile) -> (t_local, f)
+// MFMA row R (0..BM-1 of the block tile) -> (t_local, f)
 template <int F, int EPI>
 __device__ __forceinline__ void rowmap(int R, int& tl, int& f) {
   if (EPI == EPI_POOL2) {            // R = 4q + e: a 2x2 pool group in one lane's regs 4g..4g+3
@@ -51,63 +64,148 @@ __device__ __forceinline__ void rowmap(int R, int& tl, int& f) {
     const int tp = q / (F / 2), fp = q % (F / 2);
     tl = 2 * tp + (e >> 1);
     f = 2 * fp + (e & 1);
-  } else if (EPI == EPI_FMEAN) {     // F == 8: the 8 bins of a t in regs {4g + 2j + (0,1)}
-    const int tile = R >> 5, r = R & 31;
-    const int hh = (r >> 2) & 1, i = r & 3, g = r >> 3;
-    tl = 4 * tile + 2 * hh + (i >> 1);
-    f = 2 * g + (i & 1);
+  } else if (F == 8) {
+    // 32 rows = 4 t x 8 f.  ds_read_b128 lane groups {0-3,12-15,20-27} and
+    // {4-11,16-19,28-31} each get two whole t rows ({t0,t2} / {t1,t3}), so at
+    // row stride 12 their 16 positions are distinct mod 16 (conflict-free);
+    // in the C layout a lane's regs {0-3,12-15} and {4-11} are each one t
+    // (t0/t1 for lanes 0-31, t3/t2 for lanes 32-63): the freq mean stays
+    // in-lane.
+    const int r = R & 31, half = r >> 4, q = (r >> 2) & 3;
+    const int tq = half ? ((0x3021 >> (4 * q)) & 0xF) : ((0x2130 >> (4 * q)) & 0xF);
+    tl = 4 * (R >> 5) + tq;
+    f = (r & 3) + 4 * half;
   } else {
     tl = R / F;
     f = R % F;
   }
 }
 
+// Tiles (b, t-tile, n-tile), n-tile fastest so tiles sharing an input halo
+// run side by side, are dealt in 8 contiguous ranges, one per XCD (workgroup
+// i runs on XCD i % 8), so neighbouring t-tiles share one L2.  A workgroup's
+// units (tile, chunk) form one stream: the pipeline runs straight through
+// tile boundaries, where only the epilogue (stores from the accumulators)
+// is inserted.
+#ifdef SEDX_CONV_STAMPS
+// diagnostic build (tools/conv_bench.cpp): per-wave s_memtime sums
+__device__ unsigned long long g_conv_stamps[8];
+#define SEDX_ST_DECL                                                                    \
+  unsigned long long st_bar = 0, st_vm = 0, st_epi = 0, st_x = 0;                       \
+  const unsigned long long st_t0 = __builtin_amdgcn_s_memtime();                        \
+  const unsigned long long st_r0 = __builtin_amdgcn_s_memrealtime();
+#define SEDX_ST_BEGIN() st_x = __builtin_amdgcn_s_memtime()
+#define SEDX_ST_END(a) a += __builtin_amdgcn_s_memtime() - st_x
+#define SEDX_ST_VMWAIT()                                                                \
+  {                                                                                     \
+    SEDX_ST_BEGIN();                                                                    \
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                    \
+    SEDX_ST_END(st_vm);                                                                 \
+  }
+#define SEDX_ST_FLUSH()                                                                 \
+  if (lane == 0) {                                                                      \
+    atomicAdd(&g_conv_stamps[0], __builtin_amdgcn_s_memtime() - st_t0);                 \
+    atomicAdd(&g_conv_stamps[1], st_bar);                                               \
+    atomicAdd(&g_conv_stamps[2], st_vm);                                                \
+    atomicAdd(&g_conv_stamps[3], st_epi);                                               \
+    atomicAdd(&g_conv_stamps[4], 1ull);                                                 \
+    atomicAdd(&g_conv_stamps[5], __builtin_amdgcn_s_memrealtime() - st_r0);             \
+  }
+#else
+#define SEDX_ST_DECL
+#define SEDX_ST_BEGIN()
+#define SEDX_ST_END(a)
+#define SEDX_ST_VMWAIT()
+#define SEDX_ST_FLUSH()
+#endif
+
+struct ConvCursor {
+  int k, chunk, b, t0, nb;
+  bool valid;
+};
+
+template <int F, int BN>
+struct ConvGeom {
+  static constexpr int BM = (BN == 64) ? 512 : 256;
+  static constexpr int TT = BM / F;
+};
+
 template <int F, int BN, int EPI>
-__global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict__ in, int T,
+__global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict__ in, int B, int T,
                                                          int Cin, int Cout,
                                                          const uint4* __restrict__ wsp,
                                                          const float* __restrict__ bias,
                                                          float* __restrict__ out) {
-  constexpr int BM = 256, TT = BM / F, RT = TT + 2, CS = F + 2;
-  // LDS halo image: 80-B pixel records (5 x 16 B) on rows of CSP positions;
-  // CSP per (F, epilogue) from the bank-conflict search: every
-  // ds_read_b128 of an A fragment is conflict-free and every tap offset is a
-  // compile-time immediate.
+  constexpr int BM = ConvGeom<F, BN>::BM, TT = ConvGeom<F, BN>::TT;
+  constexpr int RT = TT + 2, CS = F + 2;
   constexpr int CSP = (EPI == EPI_POOL2) ? (F == 64 ? 72 : F == 32 ? 40 : 24)
-                                         : (F == 64 ? 66 : F == 32 ? 34 : F == 16 ? 32 : 24);
+                                         : (F == 64 ? 66 : F == 32 ? 34 : F == 16 ? 32 : 12);
   constexpr int NPOS = RT * CSP;
   constexpr int WAVES_N = BN / 64, WAVES_M = 8 / WAVES_N, WM = BM / WAVES_M;
   constexpr int MT = WM / 32, NT = 2;
-  constexpr int A_U4 = NPOS * 5;
-  constexpr int W_U4 = BN * 4;
+  static_assert(MT == 2, "64 x 64 wave tiles");
+  constexpr int A_U4 = NPOS * 5;          // one halo image
+  constexpr int W_U4 = BN * 4;            // one tap
+  constexpr int WS_U4 = 3 * W_U4;         // one stage (kernel row)
   constexpr int A_ITEMS = RT * CS * 2;
   constexpr int NA = (A_ITEMS + 511) / 512;
+  constexpr int NW = (WS_U4 + 511) / 512;
 
-  __shared__ uint4 lds[A_U4 + 9 * W_U4];
+  // W ring first so every fragment read is (lane base VGPR) + immediate
+  __shared__ uint4 lds[2 * WS_U4 + 2 * A_U4];
+  uint4* const Wbuf = lds;
+  uint4* const Abuf = lds + 2 * WS_U4;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WAVES_N, wn = wave % WAVES_N;
   const int h = lane >> 5;
   const int tiles_t = (T + TT - 1) / TT;
-  const int b = blockIdx.x / tiles_t;
-  const int t0 = (blockIdx.x - b * tiles_t) * TT;
-  const int n0 = blockIdx.y * BN;
+  const int nN = Cout / BN;
+  const int ntiles = B * tiles_t * nN;
+  const int per_xcd = (ntiles + 7) >> 3;
+  const int xcd = blockIdx.x & 7, slot0 = blockIdx.x >> 3, slots = gridDim.x >> 3;
+  const int nchunks = Cin >> 4;           // even for every layer (host checks)
 
-  int pbase[MT];
+  auto decode = [&](ConvCursor& c) {
+    const int within = slot0 + c.k * slots;
+    const int tile = xcd * per_xcd + within;
+    c.valid = within < per_xcd && tile < ntiles;
+    const int m = tile / nN;
+    c.nb = tile - m * nN;
+    c.b = m / tiles_t;
+    c.t0 = (m - c.b * tiles_t) * TT;
+  };
+  auto advance = [&](ConvCursor& c) {
+    if (++c.chunk == nchunks) {
+      c.chunk = 0;
+      ++c.k;
+      decode(c);
+    }
+  };
+
+  // per-lane LDS bases (uint4 units), kept opaque so the compiler folds only
+  // the tap / buffer / slot constants into the ds_read immediates
+  int abase[2][MT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     int tl, f;
     rowmap<F, EPI>(wm * WM + mt * 32 + (lane & 31), tl, f);
-    pbase[mt] = (tl * CSP + f) * 5;
+    const int p = 2 * WS_U4 + (tl * CSP + f) * 5 + h;
+    abase[0][mt] = p;
+    abase[1][mt] = p + A_U4;
+    asm volatile("" : "+v"(abase[0][mt]));
+    asm volatile("" : "+v"(abase[1][mt]));
   }
-  int bhi[NT], blo[NT];
+  int wbase[NT][2];
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) {
     const int n = wn * 64 + nt * 32 + (lane & 31);
     const int s = (n >> 2) & 3;
-    bhi[nt] = n * 4 + (h ^ s);
-    blo[nt] = n * 4 + ((2 + h) ^ s);
+    wbase[nt][0] = n * 4 + (h ^ s);
+    wbase[nt][1] = n * 4 + ((2 + h) ^ s);
+    asm volatile("" : "+v"(wbase[nt][0]));
+    asm volatile("" : "+v"(wbase[nt][1]));
   }
 
   f32x16 acc[MT][NT];
@@ -118,26 +216,22 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[mt][nt][r] = 0.0f;
 
-  const float* in_b = in + (int64_t)b * T * F * Cin;
-  const int nchunks = Cin >> 4;
-  const int nunits = nchunks * 9;
-  const uint4* wbase = wsp + (int64_t)blockIdx.y * nunits * W_U4;
-
   float4 ra[NA][2];
+  uint4 rw[2][NW];                        // W stage x lives in rw[x & 1]
 
-#define SEDX_LOAD_A(chunk)                                                              \
+#define SEDX_LOAD_A(c_)                                                                 \
   {                                                                                     \
-    const int c0_ = (chunk) * 16;                                                       \
+    const float* in_b_ = in + (int64_t)(c_).b * T * F * Cin + (c_).chunk * 16;          \
     _Pragma("unroll") for (int i = 0; i < NA; ++i) {                                    \
       const int idx = tid + i * 512;                                                    \
       float4 v0 = make_float4(0.f, 0.f, 0.f, 0.f), v1 = v0;                             \
       if (idx < A_ITEMS) {                                                              \
         const int pos = idx >> 1, hh = idx & 1;                                         \
         const int r = pos / CS, c = pos - r * CS;                                       \
-        const int t = t0 - 1 + r, f = c - 1;                                            \
+        const int t = (c_).t0 - 1 + r, f = c - 1;                                       \
         if (t >= 0 && t < T && f >= 0 && f < F) {                                       \
           const float4* src = reinterpret_cast<const float4*>(                          \
-              in_b + ((int64_t)t * F + f) * Cin + c0_ + 8 * hh);                        \
+              in_b_ + ((int64_t)t * F + f) * Cin + 8 * hh);                             \
           v0 = src[0];                                                                  \
           v1 = src[1];                                                                  \
         }                                                                               \
@@ -148,6 +242,7 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
   }
 #define SEDX_STORE_A(buf)                                                               \
   {                                                                                     \
+    uint4* dst_ = Abuf + (buf) * A_U4;                                                  \
     _Pragma("unroll") for (int i = 0; i < NA; ++i) {                                    \
       const int idx = tid + i * 512;                                                    \
       if (idx < A_ITEMS) {                                                              \
@@ -156,186 +251,286 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
         const int rec = (r * CSP + c) * 5;                                              \
         uint4 hi, lo;                                                                   \
         split8(ra[i][0], ra[i][1], hi, lo);                                             \
-        (buf)[rec + hh] = hi;                                                           \
-        (buf)[rec + 2 + hh] = lo;                                                       \
+        dst_[rec + hh] = hi;                                                            \
+        dst_[rec + 2 + hh] = lo;                                                        \
       }                                                                                 \
+    }                                                                                   \
+  }
+#define SEDX_LOAD_W(rs, c_, ky_)                                                        \
+  {                                                                                     \
+    const uint4* src_ = wsp + (((int64_t)(c_).nb * nchunks + (c_).chunk) * 3 + (ky_)) * WS_U4; \
+    _Pragma("unroll") for (int i = 0; i < NW; ++i) {                                    \
+      const int idx = tid + i * 512;                                                    \
+      rw[rs][i] = (idx < WS_U4) ? src_[idx] : make_uint4(0, 0, 0, 0);                   \
+    }                                                                                   \
+  }
+#define SEDX_STORE_W(rs, slot)                                                          \
+  {                                                                                     \
+    uint4* dst_ = Wbuf + (slot) * WS_U4;                                                \
+    _Pragma("unroll") for (int i = 0; i < NW; ++i) {                                    \
+      const int idx = tid + i * 512;                                                    \
+      if (idx < WS_U4) dst_[idx] = rw[rs][i];                                           \
     }                                                                                   \
   }
 
-  // LDS: one A halo image + the whole chunk's weights (9 taps); the next
-  // chunk is prefetched into registers while this one's 9 x 12 MFMAs run.
-  constexpr int WC_U4 = 9 * W_U4;
-  constexpr int NW = (WC_U4 + 511) / 512;
-  uint4* Abuf = lds;
-  uint4* Wbuf = lds + A_U4;
-  uint4 rw[NW];
-#define SEDX_LOAD_W(chunk)                                                              \
+  bf16x8 fa[2][2 * MT], fb[2][2 * NT];
+  // fragments of tap a (0..8) of a unit whose halo is in A buffer `abuf`
+  // and whose stage a/3 sits in W slot `wslot`
+#define SEDX_READ_FRAGS(set, abuf, wslot, tap_)                                         \
   {                                                                                     \
-    const uint4* src_ = wbase + (int64_t)(chunk) * WC_U4;                               \
-    _Pragma("unroll") for (int i = 0; i < NW; ++i) {                                    \
-      const int idx = tid + i * 512;                                                    \
-      rw[i] = (idx < WC_U4) ? src_[idx] : make_uint4(0, 0, 0, 0);                       \
+    constexpr int aoff_ = (((tap_) / 3) * CSP + ((tap_) % 3)) * 5;                      \
+    constexpr int woff_ = (wslot) * WS_U4 + ((tap_) % 3) * W_U4;                        \
+    _Pragma("unroll") for (int mt = 0; mt < MT; ++mt) {                                 \
+      fa[set][2 * mt] = as_bf16x8(lds[abase[abuf][mt] + aoff_]);                        \
+      fa[set][2 * mt + 1] = as_bf16x8(lds[abase[abuf][mt] + aoff_ + 2]);                \
     }                                                                                   \
-  }
-#define SEDX_STORE_W()                                                                  \
-  {                                                                                     \
-    _Pragma("unroll") for (int i = 0; i < NW; ++i) {                                    \
-      const int idx = tid + i * 512;                                                    \
-      if (idx < WC_U4) Wbuf[idx] = rw[i];                                               \
+    _Pragma("unroll") for (int nt = 0; nt < NT; ++nt) {                                 \
+      fb[set][2 * nt] = as_bf16x8(lds[wbase[nt][0] + woff_]);                           \
+      fb[set][2 * nt + 1] = as_bf16x8(lds[wbase[nt][1] + woff_]);                       \
     }                                                                                   \
+    __builtin_amdgcn_sched_barrier(0);                                                  \
   }
-
-  SEDX_LOAD_A(0);
-  SEDX_LOAD_W(0);
-  SEDX_STORE_A(Abuf);
-  SEDX_STORE_W();
-  __syncthreads();
-  if (nchunks > 1) {
-    SEDX_LOAD_A(1);
-    SEDX_LOAD_W(1);
-  }
-  for (int chunk = 0; chunk < nchunks; ++chunk) {
-    // software pipeline over the 9 taps: fragments of tap t+1 are read from
-    // LDS (two register sets, static indices) while tap t's 12 MFMAs issue.
-    bf16x8 fa[2][2 * MT], fb[2][2 * NT];
-#define SEDX_READ_FRAGS(set, tap_)                                                      \
-    {                                                                                   \
-      const int toff_ = ((tap_) / 3) * CSP + ((tap_) % 3);                              \
-      const uint4* W_ = Wbuf + (tap_) * W_U4;                                           \
-      _Pragma("unroll") for (int mt = 0; mt < MT; ++mt) {                               \
-        const uint4* Ap = Abuf + pbase[mt] + toff_ * 5;                                 \
-        fa[set][2 * mt] = as_bf16x8(Ap[h]);                                             \
-        fa[set][2 * mt + 1] = as_bf16x8(Ap[2 + h]);                                     \
-      }                                                                                 \
-      _Pragma("unroll") for (int nt = 0; nt < NT; ++nt) {                               \
-        fb[set][2 * nt] = as_bf16x8(W_[bhi[nt]]);                                       \
-        fb[set][2 * nt + 1] = as_bf16x8(W_[blo[nt]]);                                   \
-      }                                                                                 \
-      __builtin_amdgcn_sched_barrier(0);                                                \
-    }
 #define SEDX_MFMAS(set)                                                                 \
-    {                                                                                   \
-      _Pragma("unroll") for (int mt = 0; mt < MT; ++mt)                                 \
-      _Pragma("unroll") for (int nt = 0; nt < NT; ++nt) {                               \
-        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[set][2 * mt], fb[set][2 * nt], acc[mt][nt], 0, 0, 0);     \
-        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[set][2 * mt], fb[set][2 * nt + 1], acc[mt][nt], 0, 0, 0); \
-        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[set][2 * mt + 1], fb[set][2 * nt], acc[mt][nt], 0, 0, 0); \
-      }                                                                                 \
-    }
-    SEDX_READ_FRAGS(0, 0);
-    SEDX_READ_FRAGS(1, 1);
-    SEDX_MFMAS(0);
-    SEDX_READ_FRAGS(0, 2);
-    SEDX_MFMAS(1);
-    SEDX_READ_FRAGS(1, 3);
-    SEDX_MFMAS(0);
-    SEDX_READ_FRAGS(0, 4);
-    SEDX_MFMAS(1);
-    SEDX_READ_FRAGS(1, 5);
-    SEDX_MFMAS(0);
-    SEDX_READ_FRAGS(0, 6);
-    SEDX_MFMAS(1);
-    SEDX_READ_FRAGS(1, 7);
-    SEDX_MFMAS(0);
-    SEDX_READ_FRAGS(0, 8);
-    SEDX_MFMAS(1);
-    SEDX_MFMAS(0);
-#undef SEDX_READ_FRAGS
-#undef SEDX_MFMAS
-    if (chunk + 1 < nchunks) {
-      __syncthreads();
-      SEDX_STORE_A(Abuf);
-      SEDX_STORE_W();
-      __syncthreads();
-      if (chunk + 2 < nchunks) {
-        SEDX_LOAD_A(chunk + 2);
-        SEDX_LOAD_W(chunk + 2);
+  {                                                                                     \
+    _Pragma("unroll") for (int mt = 0; mt < MT; ++mt)                                   \
+    _Pragma("unroll") for (int nt = 0; nt < NT; ++nt) {                                 \
+      acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[set][2 * mt], fb[set][2 * nt], acc[mt][nt], 0, 0, 0);     \
+      acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[set][2 * mt], fb[set][2 * nt + 1], acc[mt][nt], 0, 0, 0); \
+      acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[set][2 * mt + 1], fb[set][2 * nt], acc[mt][nt], 0, 0, 0); \
+    }                                                                                   \
+  }
+
+  auto epilogue = [&](const ConvCursor& c) {
+    int lane_ = lane;                    // opaque: keep the address math here
+    asm volatile("" : "+v"(lane_));
+    const int h = lane_ >> 5;
+    const int n0 = c.nb * BN;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int n = n0 + wn * 64 + nt * 32 + (lane_ & 31);
+      const float bv = bias[n];
+#ifdef SEDX_CONV_ABL_NOSTORE
+      const bool live = bv == -1e30f;   // diagnostic: stores never taken, MFMAs kept
+#else
+      constexpr bool live = true;
+#endif
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int Rbase = wm * WM + mt * 32;
+        float r[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) r[i] = fmaxf(acc[mt][nt][i] + bv, 0.0f);
+        if (EPI == EPI_STORE) {
+          float* ob = out + ((int64_t)c.b * T + c.t0) * F * Cout + n;
+          const int tlim = T - c.t0;
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            int tl, f;
+            rowmap<F, EPI>(Rbase + (i & 3) + 8 * (i >> 2) + 4 * h, tl, f);
+            if (live && tl < tlim) ob[(tl * F + f) * Cout] = r[i];
+            if ((i & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+          }
+        } else if (EPI == EPI_POOL2) {
+          constexpr int FO = F / 2;
+          const int To = T / 2;
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int q = (Rbase + 8 * g + 4 * h) >> 2;
+            const int tp = q / FO, fp = q % FO;
+            const int to = c.t0 / 2 + tp;
+            const float v = (((r[4 * g] + r[4 * g + 1]) + r[4 * g + 2]) + r[4 * g + 3]) * 0.25f;
+            if (live && to < To) out[(((int64_t)c.b * To + to) * FO + fp) * Cout + n] = v;
+          }
+        } else {  // EPI_FMEAN, F == 8: regs {0-3,12-15} and {4-11} are one t each (rowmap)
+          const float sa = (((r[0] + r[1]) + (r[2] + r[3])) + ((r[12] + r[13]) + (r[14] + r[15])));
+          const float sb = (((r[4] + r[5]) + (r[6] + r[7])) + ((r[8] + r[9]) + (r[10] + r[11])));
+          const int tb = c.t0 + 4 * (Rbase >> 5);
+          const int ta = tb + (h ? 3 : 0), tb2 = tb + (h ? 2 : 1);
+          if (live && ta < T) out[((int64_t)c.b * T + ta) * Cout + n] = sa * 0.125f;
+          if (live && tb2 < T) out[((int64_t)c.b * T + tb2) * Cout + n] = sb * 0.125f;
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[mt][nt][i] = 0.0f;
       }
     }
+  };
+
+  SEDX_ST_DECL
+  // cur = unit being computed, n1 / n2 = the next two units of the stream
+  ConvCursor cur{0, 0, 0, 0, 0, false};
+  decode(cur);
+  if (!cur.valid) return;
+  ConvCursor n1 = cur;
+  advance(n1);
+  ConvCursor n2 = n1;
+  if (n2.valid) advance(n2);
+
+  // prologue: halo(cur) -> A0, W(cur, row 0/1) -> slots 0/1; registers hold
+  // W(cur, row 2), W(n1, row 0) and halo(n1)
+  SEDX_LOAD_A(cur);
+  SEDX_LOAD_W(0, cur, 0);
+  SEDX_LOAD_W(1, cur, 1);
+  SEDX_STORE_A(0);
+  SEDX_STORE_W(0, 0);
+  SEDX_STORE_W(1, 1);
+  SEDX_LOAD_W(0, cur, 2);
+  if (n1.valid) {
+    SEDX_LOAD_W(1, n1, 0);
+    SEDX_LOAD_A(n1);
   }
+  __syncthreads();
+  SEDX_READ_FRAGS(0, 0, 0, 0);
+
+  // One stage = taps 3KY..3KY+2 of the current unit (parity U: halo in A
+  // buffer U, stage KY in W slot (U + KY) & 1, fragment set of tap a =
+  // (U + a) & 1).  After the barrier the slot of stage KY is free:
+  //   KY 0: W(cur, 2) -> slot U;      halo(n1) -> A buffer U^1; load halo(n2)
+  //   KY 1: W(n1, 0)  -> slot U^1
+  //   KY 2: W(n1, 1)  -> slot U
+  // each followed by the load of the weights two stages further on into the
+  // register set just drained (W(n1, 1), W(n1, 2), W(n2, 0)).
+#define SEDX_STAGE_STORES(U, KY)                                                        \
+  {                                                                                     \
+    if ((KY) == 0) {                                                                    \
+      SEDX_STORE_W((U) & 1, U);                                                         \
+      if (n1.valid) {                                                                   \
+        SEDX_LOAD_W((U) & 1, n1, 1);                                                    \
+        SEDX_STORE_A((U) ^ 1);                                                          \
+        if (n2.valid) SEDX_LOAD_A(n2);                                                  \
+      }                                                                                 \
+    } else if ((KY) == 1) {                                                             \
+      if (n1.valid) {                                                                   \
+        SEDX_STORE_W(((U) + 1) & 1, ((U) + 1) & 1);                                     \
+        SEDX_LOAD_W(((U) + 1) & 1, n1, 2);                                              \
+      }                                                                                 \
+    } else {                                                                            \
+      if (n1.valid) SEDX_STORE_W((U) & 1, (U) & 1);                                     \
+      if (n2.valid) SEDX_LOAD_W((U) & 1, n2, 0);                                        \
+    }                                                                                   \
+  }
+#define SEDX_STAGE(U, KY)                                                               \
+  {                                                                                     \
+    SEDX_READ_FRAGS(((U) + 3 * (KY) + 1) & 1, U, ((U) + (KY)) & 1, 3 * (KY) + 1);       \
+    SEDX_MFMAS(((U) + 3 * (KY)) & 1);                                                   \
+    SEDX_READ_FRAGS(((U) + 3 * (KY) + 2) & 1, U, ((U) + (KY)) & 1, 3 * (KY) + 2);       \
+    SEDX_MFMAS(((U) + 3 * (KY) + 1) & 1);                                               \
+    SEDX_ST_BEGIN();                                                                    \
+    __syncthreads();                                                                    \
+    SEDX_ST_END(st_bar);                                                                \
+    SEDX_ST_VMWAIT();                                                                   \
+    SEDX_STAGE_STORES(U, KY);                                                           \
+    if ((KY) < 2) {                                                                     \
+      SEDX_READ_FRAGS(((U) + 3 * (KY) + 3) & 1, U, ((U) + (KY) + 1) & 1, 3 * (KY) + 3); \
+    } else {                                                                            \
+      SEDX_READ_FRAGS(((U) + 1) & 1, (U) ^ 1, ((U) + 1) & 1, 0);                        \
+    }                                                                                   \
+    SEDX_MFMAS(((U) + 3 * (KY) + 2) & 1);                                               \
+  }
+
+#define SEDX_UNIT(U)                                                                    \
+  {                                                                                     \
+    SEDX_STAGE(U, 0);                                                                   \
+    SEDX_STAGE(U, 1);                                                                   \
+    SEDX_STAGE(U, 2);                                                                   \
+    if (cur.chunk == nchunks - 1) {                                                     \
+      SEDX_ST_BEGIN();                                                                  \
+      epilogue(cur);                                                                    \
+      SEDX_ST_END(st_epi);                                                              \
+    }                                                                                   \
+    cur = n1;                                                                           \
+    n1 = n2;                                                                            \
+    if (n2.valid) advance(n2);                                                          \
+    if (!cur.valid) break;                                                              \
+  }
+
+  while (true) {
+    SEDX_UNIT(0);
+    SEDX_UNIT(1);
+  }
+  SEDX_ST_FLUSH();
+#undef SEDX_UNIT
+#undef SEDX_STAGE
+#undef SEDX_STAGE_STORES
+#undef SEDX_READ_FRAGS
+#undef SEDX_MFMAS
 #undef SEDX_LOAD_W
 #undef SEDX_STORE_W
 #undef SEDX_LOAD_A
 #undef SEDX_STORE_A
+}
 
-  // ---- epilogue straight from the accumulators ----
-#pragma unroll
-  for (int nt = 0; nt < NT; ++nt) {
-    const int n = n0 + wn * 64 + nt * 32 + (lane & 31);
-    const float bv = bias[n];
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      const int Rbase = wm * WM + mt * 32;
-      float r[16];
-#pragma unroll
-      for (int i = 0; i < 16; ++i) r[i] = fmaxf(acc[mt][nt][i] + bv, 0.0f);
-      if (EPI == EPI_STORE) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          int tl, f;
-          rowmap<F, EPI>(Rbase + (i & 3) + 8 * (i >> 2) + 4 * h, tl, f);
-          const int t = t0 + tl;
-          if (t < T) out[(((int64_t)b * T + t) * F + f) * Cout + n] = r[i];
-        }
-      } else if (EPI == EPI_POOL2) {
-        constexpr int FO = F / 2;
-        const int To = T / 2;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int q = (Rbase + 8 * g + 4 * h) >> 2;
-          const int tp = q / FO, fp = q % FO;
-          const int to = t0 / 2 + tp;
-          const float v = (((r[4 * g] + r[4 * g + 1]) + r[4 * g + 2]) + r[4 * g + 3]) * 0.25f;
-          if (to < To) out[(((int64_t)b * To + to) * FO + fp) * Cout + n] = v;
-        }
-      } else {  // EPI_FMEAN, F == 8
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          float s = 0.f;
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            s += r[4 * g + 2 * j];
-            s += r[4 * g + 2 * j + 1];
-          }
-          const int t = t0 + 4 * (Rbase >> 5) + 2 * h + j;
-          if (t < T) out[((int64_t)b * T + t) * Cout + n] = s * 0.125f;
-        }
-      }
-    }
+template <int F, int BN, int EPI>
+static void launch_x3_epi(const float* in, int B, int T, int Cin, int Cout, const uint4* wp,
+                          const float* bias, float* out, hipStream_t s) {
+  constexpr int TT = ConvGeom<F, BN>::TT;
+  static int resident = 0;           // workgroups resident on the whole device
+  if (!resident) {
+    int dev = 0, ncu = 0, per_cu = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, conv3x3_x3_kernel<F, BN, EPI>, 512, 0);
+    resident = (ncu > 0 ? ncu : 256) * (per_cu > 0 ? per_cu : 1);
   }
+  const int ntiles = B * ((T + TT - 1) / TT) * (Cout / BN);
+  const int per_xcd = (ntiles + 7) / 8;
+  int grid = resident & ~7;
+  if (grid < 8) grid = 8;
+  if (grid > 8 * per_xcd) grid = 8 * per_xcd;
+  hipLaunchKernelGGL((conv3x3_x3_kernel<F, BN, EPI>), dim3(grid), dim3(512), 0, s, in, B, T, Cin, Cout,
+                     wp, bias, out);
 }
 
 template <int F, int BN>
 static void launch_x3(const float* in, int B, int T, int Cin, int Cout, const uint4* wp,
                       const float* bias, float* out, int epi, hipStream_t s) {
-  constexpr int TT = 256 / F;
-  dim3 grid(B * ((T + TT - 1) / TT), Cout / BN);
-  if (epi == EPI_STORE)
-    hipLaunchKernelGGL((conv3x3_x3_kernel<F, BN, EPI_STORE>), grid, dim3(512), 0, s, in, T, Cin, Cout, wp, bias, out);
-  else if (epi == EPI_POOL2)
-    hipLaunchKernelGGL((conv3x3_x3_kernel<F, BN, EPI_POOL2>), grid, dim3(512), 0, s, in, T, Cin, Cout, wp, bias, out);
-  else
-    hipLaunchKernelGGL((conv3x3_x3_kernel<8, BN, EPI_FMEAN>), grid, dim3(512), 0, s, in, T, Cin, Cout, wp, bias, out);
+  // only the (F, epilogue) pairs of the model are instantiated
+  if constexpr (F == 8) {
+    if (epi == EPI_STORE)
+      launch_x3_epi<8, BN, EPI_STORE>(in, B, T, Cin, Cout, wp, bias, out, s);
+    else if (epi == EPI_FMEAN)
+      launch_x3_epi<8, BN, EPI_FMEAN>(in, B, T, Cin, Cout, wp, bias, out, s);
+  } else if constexpr (F == 64) {
+    if (epi == EPI_POOL2)
+      launch_x3_epi<F, BN, EPI_POOL2>(in, B, T, Cin, Cout, wp, bias, out, s);
+  } else {
+    if (epi == EPI_STORE)
+      launch_x3_epi<F, BN, EPI_STORE>(in, B, T, Cin, Cout, wp, bias, out, s);
+    else if (epi == EPI_POOL2)
+      launch_x3_epi<F, BN, EPI_POOL2>(in, B, T, Cin, Cout, wp, bias, out, s);
+  }
 }
 
+// Shapes: Cin a multiple of 32 (the unit stream pairs chunks), Cout a
+// multiple of the n-tile; api.cpp routes only such layers here.
 void launch_conv3x3_x3(const float* in, int B, int T, int F, int Cin, int Cout, const void* wp,
                        const float* bias, float* out, int epi, hipStream_t s) {
   const uint4* w = static_cast<const uint4*>(wp);
+  if (Cin % 32 != 0) return;
   switch (F) {
     case 64:   // block 1 conv2 (Cout 64)
-      launch_x3<64, 64>(in, B, T, Cin, Cout, w, bias, out, epi, s);
+      if (Cout % 64 == 0) launch_x3<64, 64>(in, B, T, Cin, Cout, w, bias, out, epi, s);
       break;
     case 32:
-      launch_x3<32, 128>(in, B, T, Cin, Cout, w, bias, out, epi, s);
+      if (Cout % 128 == 0) launch_x3<32, 128>(in, B, T, Cin, Cout, w, bias, out, epi, s);
       break;
     case 16:
-      launch_x3<16, 128>(in, B, T, Cin, Cout, w, bias, out, epi, s);
+      if (Cout % 128 == 0) launch_x3<16, 128>(in, B, T, Cin, Cout, w, bias, out, epi, s);
       break;
     case 8:
-      launch_x3<8, 128>(in, B, T, Cin, Cout, w, bias, out, epi, s);
+      if (Cout % 128 == 0) launch_x3<8, 128>(in, B, T, Cin, Cout, w, bias, out, epi, s);
       break;
     default: break;
   }
 }
+
+#ifdef SEDX_CONV_STAMPS
+void conv_stamps_rw(unsigned long long* out8, bool reset) {
+  (void)hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_conv_stamps), 8 * sizeof(unsigned long long));
+  if (reset) {
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_conv_stamps), z, sizeof(z));
+  }
+}
+#endif
 
 }  // namespace sedx
