@@ -171,8 +171,8 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
     const int within = slot0 + c.k * slots;
     const int tile = xcd * per_xcd + within;
     c.valid = within < per_xcd && tile < ntiles;
-    const int m = tile / nN;
-    c.nb = tile - m * nN;
+    const int m = c.valid ? tile / nN : 0;   // past the end: loads stay in bounds
+    c.nb = c.valid ? tile - m * nN : 0;
     c.b = m / tiles_t;
     c.t0 = (m - c.b * tiles_t) * TT;
   };
@@ -216,61 +216,67 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[mt][nt][r] = 0.0f;
 
-  float4 ra[NA][2];
-  uint4 rw[2][NW];                        // W stage x lives in rw[x & 1]
+  float4 ra0[NA], ra1[NA];                // staged halo items (2 x 16 B each)
+  bool rok[NA];                           // ... inside the image (else zero)
+  uint4 rw0[NW], rw1[NW];                 // W stage x lives in rw(x & 1)
 
+  // Staging loads and stores are branch-free (indices clamped, halo zeroes by
+  // select) so the compiler's vmcnt bookkeeping stays exact and each wait
+  // covers only the loads it needs.  Per-item halo geometry is loop-invariant.
+  int a_r[NA], a_f[NA], a_off[NA], a_rec[NA];
+  bool a_fok[NA];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) {
+    const int idx = min(tid + i * 512, A_ITEMS - 1);
+    const int pos = idx >> 1, hh = idx & 1;
+    const int r = pos / CS, c = pos - r * CS;
+    a_r[i] = r;
+    a_f[i] = c - 1;
+    a_fok[i] = c >= 1 && c <= F;
+    a_off[i] = min(max(c - 1, 0), F - 1) * Cin + 8 * hh;
+    a_rec[i] = (r * CSP + c) * 5 + hh;
+  }
 #define SEDX_LOAD_A(c_)                                                                 \
   {                                                                                     \
     const float* in_b_ = in + (int64_t)(c_).b * T * F * Cin + (c_).chunk * 16;          \
     _Pragma("unroll") for (int i = 0; i < NA; ++i) {                                    \
-      const int idx = tid + i * 512;                                                    \
-      float4 v0 = make_float4(0.f, 0.f, 0.f, 0.f), v1 = v0;                             \
-      if (idx < A_ITEMS) {                                                              \
-        const int pos = idx >> 1, hh = idx & 1;                                         \
-        const int r = pos / CS, c = pos - r * CS;                                       \
-        const int t = (c_).t0 - 1 + r, f = c - 1;                                       \
-        if (t >= 0 && t < T && f >= 0 && f < F) {                                       \
-          const float4* src = reinterpret_cast<const float4*>(                          \
-              in_b_ + ((int64_t)t * F + f) * Cin + 8 * hh);                             \
-          v0 = src[0];                                                                  \
-          v1 = src[1];                                                                  \
-        }                                                                               \
-      }                                                                                 \
-      ra[i][0] = v0;                                                                    \
-      ra[i][1] = v1;                                                                    \
+      const int t = (c_).t0 - 1 + a_r[i];                                               \
+      const bool ok = a_fok[i] && t >= 0 && t < T;                                      \
+      const int tc = min(max(t, 0), T - 1);                                             \
+      const float4* src = reinterpret_cast<const float4*>(in_b_ + (tc * F * Cin + a_off[i])); \
+      ra0[i] = src[0];                                                                  \
+      ra1[i] = src[1];                                                                  \
+      rok[i] = ok;     /* halo zeroes applied at the LDS write, not here */             \
     }                                                                                   \
+    asm volatile("" ::: "memory"); /* issue here: not sunk to the use */                \
   }
 #define SEDX_STORE_A(buf)                                                               \
   {                                                                                     \
     uint4* dst_ = Abuf + (buf) * A_U4;                                                  \
     _Pragma("unroll") for (int i = 0; i < NA; ++i) {                                    \
-      const int idx = tid + i * 512;                                                    \
-      if (idx < A_ITEMS) {                                                              \
-        const int pos = idx >> 1, hh = idx & 1;                                         \
-        const int r = pos / CS, c = pos - r * CS;                                       \
-        const int rec = (r * CSP + c) * 5;                                              \
-        uint4 hi, lo;                                                                   \
-        split8(ra[i][0], ra[i][1], hi, lo);                                             \
-        dst_[rec + hh] = hi;                                                            \
-        dst_[rec + 2 + hh] = lo;                                                        \
-      }                                                                                 \
+      uint4 hi, lo;                                                                     \
+      const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);                                 \
+      split8(rok[i] ? ra0[i] : z, rok[i] ? ra1[i] : z, hi, lo);                         \
+      dst_[a_rec[i]] = hi;                                                              \
+      dst_[a_rec[i] + 2] = lo;                                                          \
     }                                                                                   \
+    asm volatile("" ::: "memory");                                                      \
   }
 #define SEDX_LOAD_W(rs, c_, ky_)                                                        \
   {                                                                                     \
     const uint4* src_ = wsp + (((int64_t)(c_).nb * nchunks + (c_).chunk) * 3 + (ky_)) * WS_U4; \
     _Pragma("unroll") for (int i = 0; i < NW; ++i) {                                    \
-      const int idx = tid + i * 512;                                                    \
-      rw[rs][i] = (idx < WS_U4) ? src_[idx] : make_uint4(0, 0, 0, 0);                   \
+      const uint4 v_ = src_[min(tid + i * 512, WS_U4 - 1)];                             \
+      if ((rs) == 0) rw0[i] = v_; else rw1[i] = v_;                                     \
     }                                                                                   \
+    asm volatile("" ::: "memory");                                                      \
   }
 #define SEDX_STORE_W(rs, slot)                                                          \
   {                                                                                     \
     uint4* dst_ = Wbuf + (slot) * WS_U4;                                                \
-    _Pragma("unroll") for (int i = 0; i < NW; ++i) {                                    \
-      const int idx = tid + i * 512;                                                    \
-      if (idx < WS_U4) dst_[idx] = rw[rs][i];                                           \
-    }                                                                                   \
+    _Pragma("unroll") for (int i = 0; i < NW; ++i)                                      \
+      dst_[min(tid + i * 512, WS_U4 - 1)] = ((rs) == 0) ? rw0[i] : rw1[i];              \
+    asm volatile("" ::: "memory"); /* before the refill loads are issued */             \
   }
 
   bf16x8 fa[2][2 * MT], fb[2][2 * NT];
@@ -300,6 +306,15 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
     }                                                                                   \
   }
 
+  // bias of the current tile's columns, loaded when the tile starts (a load
+  // issued in the epilogue would make its wait drain every prefetch in flight)
+  float bcur[NT];
+  auto load_bias = [&](const ConvCursor& c) {
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) bcur[nt] = bias[c.nb * BN + wn * 64 + nt * 32 + (lane & 31)];
+    asm volatile("" ::: "memory");
+  };
+
   auto epilogue = [&](const ConvCursor& c) {
     int lane_ = lane;                    // opaque: keep the address math here
     asm volatile("" : "+v"(lane_));
@@ -308,7 +323,7 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
       const int n = n0 + wn * 64 + nt * 32 + (lane_ & 31);
-      const float bv = bias[n];
+      const float bv = bcur[nt];
 #ifdef SEDX_CONV_ABL_NOSTORE
       const bool live = bv == -1e30f;   // diagnostic: stores never taken, MFMAs kept
 #else
@@ -363,10 +378,11 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
   ConvCursor n1 = cur;
   advance(n1);
   ConvCursor n2 = n1;
-  if (n2.valid) advance(n2);
+  advance(n2);
 
   // prologue: halo(cur) -> A0, W(cur, row 0/1) -> slots 0/1; registers hold
   // W(cur, row 2), W(n1, row 0) and halo(n1)
+  load_bias(cur);
   SEDX_LOAD_A(cur);
   SEDX_LOAD_W(0, cur, 0);
   SEDX_LOAD_W(1, cur, 1);
@@ -374,10 +390,8 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
   SEDX_STORE_W(0, 0);
   SEDX_STORE_W(1, 1);
   SEDX_LOAD_W(0, cur, 2);
-  if (n1.valid) {
-    SEDX_LOAD_W(1, n1, 0);
-    SEDX_LOAD_A(n1);
-  }
+  SEDX_LOAD_W(1, n1, 0);
+  SEDX_LOAD_A(n1);
   __syncthreads();
   SEDX_READ_FRAGS(0, 0, 0, 0);
 
@@ -389,23 +403,41 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
   //   KY 2: W(n1, 1)  -> slot U
   // each followed by the load of the weights two stages further on into the
   // register set just drained (W(n1, 1), W(n1, 2), W(n2, 0)).
+#ifdef SEDX_ABL_NOLDS     // diagnostics (tools/gpu_conv_bench.sh): drop the stage's LDS writes
+#define SEDX_ABL_STORE_W(rs, slot)
+#define SEDX_ABL_STORE_A(buf)
+#else
+#define SEDX_ABL_STORE_W(rs, slot) SEDX_STORE_W(rs, slot)
+#define SEDX_ABL_STORE_A(buf) SEDX_STORE_A(buf)
+#endif
+#if defined(SEDX_ABL_NOLOAD) || defined(SEDX_ABL_NOLOADW)   // ... or its global loads
+#define SEDX_ABL_LOAD_W(rs, c_, ky_)
+#else
+#define SEDX_ABL_LOAD_W(rs, c_, ky_) SEDX_LOAD_W(rs, c_, ky_)
+#endif
+#if defined(SEDX_ABL_NOLOAD) || defined(SEDX_ABL_NOLOADA)
+#define SEDX_ABL_LOAD_A(c_)
+#else
+#define SEDX_ABL_LOAD_A(c_) SEDX_LOAD_A(c_)
+#endif
+#ifdef SEDX_ABL_NOBAR     // ... or its barrier
+#define SEDX_ABL_SYNC()
+#else
+#define SEDX_ABL_SYNC() __syncthreads()
+#endif
 #define SEDX_STAGE_STORES(U, KY)                                                        \
   {                                                                                     \
     if ((KY) == 0) {                                                                    \
-      SEDX_STORE_W((U) & 1, U);                                                         \
-      if (n1.valid) {                                                                   \
-        SEDX_LOAD_W((U) & 1, n1, 1);                                                    \
-        SEDX_STORE_A((U) ^ 1);                                                          \
-        if (n2.valid) SEDX_LOAD_A(n2);                                                  \
-      }                                                                                 \
+      SEDX_ABL_STORE_W((U) & 1, U);                                                     \
+      SEDX_ABL_LOAD_W((U) & 1, n1, 1);                                                  \
+      SEDX_ABL_STORE_A((U) ^ 1);                                                        \
+      SEDX_ABL_LOAD_A(n2);                                                              \
     } else if ((KY) == 1) {                                                             \
-      if (n1.valid) {                                                                   \
-        SEDX_STORE_W(((U) + 1) & 1, ((U) + 1) & 1);                                     \
-        SEDX_LOAD_W(((U) + 1) & 1, n1, 2);                                              \
-      }                                                                                 \
+      SEDX_ABL_STORE_W(((U) + 1) & 1, ((U) + 1) & 1);                                   \
+      SEDX_ABL_LOAD_W(((U) + 1) & 1, n1, 2);                                            \
     } else {                                                                            \
-      if (n1.valid) SEDX_STORE_W((U) & 1, (U) & 1);                                     \
-      if (n2.valid) SEDX_LOAD_W((U) & 1, n2, 0);                                        \
+      SEDX_ABL_STORE_W((U) & 1, (U) & 1);                                               \
+      SEDX_ABL_LOAD_W((U) & 1, n2, 0);                                                  \
     }                                                                                   \
   }
 #define SEDX_STAGE(U, KY)                                                               \
@@ -415,7 +447,7 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
     SEDX_READ_FRAGS(((U) + 3 * (KY) + 2) & 1, U, ((U) + (KY)) & 1, 3 * (KY) + 2);       \
     SEDX_MFMAS(((U) + 3 * (KY) + 1) & 1);                                               \
     SEDX_ST_BEGIN();                                                                    \
-    __syncthreads();                                                                    \
+    SEDX_ABL_SYNC();                                                                    \
     SEDX_ST_END(st_bar);                                                                \
     SEDX_ST_VMWAIT();                                                                   \
     SEDX_STAGE_STORES(U, KY);                                                           \
@@ -439,8 +471,9 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
     }                                                                                   \
     cur = n1;                                                                           \
     n1 = n2;                                                                            \
-    if (n2.valid) advance(n2);                                                          \
+    advance(n2);                                                                        \
     if (!cur.valid) break;                                                              \
+    if (cur.chunk == 0) load_bias(cur);                                                 \
   }
 
   while (true) {
