@@ -138,6 +138,25 @@ def stage_times(model, wave, dev, reps):
     return {s: round(float(v), 4) for s, v in zip(_lib.STAGES, acc / reps)}
 
 
+# HBM traffic per launch comes from the rocprofv3 PMC passes of this bench
+# command (tools/profile_round.sh -> tools/pmc_summary.py; FETCH_SIZE x2 per
+# the gfx950 correction + WRITE_SIZE), committed under profiles/.
+PROFILE_SUMMARY = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles',
+                               'r01b_kernel_summary.json')
+STAGE_KERNEL = {'b1c2': '<64, 64, 1>', 'b2c1': '<32, 128, 0>', 'b2c2': '<32, 128, 1>',
+                'b3c1': '<16, 128, 0>', 'b3c2': '<16, 128, 1>', 'b4c1': '<8, 128, 0>',
+                'b4c2': '<8, 128, 2>'}
+
+
+def profiled_traffic(kernel):
+    try:
+        with open(PROFILE_SUMMARY) as f:
+            v = json.load(f).get(kernel, {})
+        return v.get('hbm_bytes_corrected')
+    except (OSError, ValueError):
+        return None
+
+
 def roofline(stage_ms, B, precision):
     T = 160000 // 160 + 1
     conv = {s: stage_ms[s] for s in CONV_STAGES}
@@ -146,12 +165,17 @@ def roofline(stage_ms, B, precision):
     achieved = flops / (conv[dom] * 1e-3) / 1e12
     peak = PEAK_TF[precision]
     total = sum(conv_flops(s, B, T) for s in CONV_STAGES)
+    kname = 'sedx::conv3x3_%s%s' % ('x3_kernel' if precision == 'x3' else 'kernel', STAGE_KERNEL[dom])
+    traffic = profiled_traffic(kname) if B == 32 else None
     return {'bound': 'mfma',
             'kernel': 'conv3x3_%s (%s)' % ('x3_kernel' if precision == 'x3' else 'kernel', dom),
             'arith': '3xbf16-split MFMA 32x32x16, fp32 acc (peak = bf16 dense 2.5 PF / 3)'
                      if precision == 'x3' else 'fp32 MFMA 32x32x2',
             'achieved': round(achieved, 2), 'peak': round(peak, 1), 'unit': 'TFLOP/s',
-            'frac': round(achieved / peak, 4), 'traffic': None,
+            'frac': round(achieved / peak, 4),
+            'traffic': traffic, 'traffic_unit': 'bytes/launch (HBM, rocprofv3 PMC)',
+            'traffic_source': os.path.relpath(PROFILE_SUMMARY, os.path.dirname(os.path.abspath(__file__)))
+            if traffic is not None else None,
             'flops_per_launch': flops, 'avg_launch_ms': conv[dom],
             'conv_stack_tflops': round(total / (sum(conv.values()) * 1e-3) / 1e12, 2)}
 

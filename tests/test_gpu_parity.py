@@ -21,6 +21,8 @@ SEEDS = {GRU: 0, TRF: 1}
 TOL = 1e-3          # north_star: |framewise - reference| <= 1e-3 (fp32)
 P16 = (16000, 512, 160, 64, 25, 7000)
 P32 = (32000, 1024, 320, 64, 50, 14000)
+P8 = (8000, 256, 80, 64, 12, 3500)
+PRESET_ARGS = {'8k': P8, '16k': P16, '32k': P32}
 
 
 def build(mt, preset=P16, feature_type='logmel'):
@@ -186,6 +188,22 @@ def test_gamma(golden_dir):
     for k in ('framewise_output', 'clipwise_output'):
         e = err(out[k].cpu().numpy(), g[k])
         print('gamma', k, 'max|d| =', e)
+        assert e <= TOL
+
+
+@pytest.mark.parametrize('mt', [GRU, TRF])
+@pytest.mark.parametrize('preset', ['8k', '32k'])
+def test_logmel_presets_vs_oracle(mt, preset):
+    """8 k / 32 k logmel presets (pytorch/predict.py:186-205): other FFT sizes
+    through the same kernels, checked against the oracle on 3 ragged clips."""
+    args = PRESET_ARGS[preset]
+    m = build(mt, args)
+    wave = synth.make_waveforms(3, seconds=2.7, sample_rate=args[0], seed=31)
+    out = run(m, wave)
+    ref = O.forward(O.full_state(synth.make_state_dict(mt, seed=SEEDS[mt]), preset), mt, wave=wave)
+    for k in ('framewise_output', 'clipwise_output'):
+        e = err(out[k], ref[k].numpy())
+        print(mt, preset, k, 'max|d| =', e)
         assert e <= TOL
 
 
