@@ -143,9 +143,11 @@ def stage_times(model, wave, dev, reps):
 # the gfx950 correction + WRITE_SIZE), committed under profiles/.
 PROFILE_SUMMARY = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles',
                                'r01b_kernel_summary.json')
-STAGE_KERNEL = {'b1c2': '<64, 64, 1>', 'b2c1': '<32, 128, 0>', 'b2c2': '<32, 128, 1>',
-                'b3c1': '<16, 128, 0>', 'b3c2': '<16, 128, 1>', 'b4c1': '<8, 128, 0>',
-                'b4c2': '<8, 128, 2>'}
+STAGE_KERNEL = {'b1c2': '<64, 64, 1', 'b2c1': '<32, 128, 0', 'b2c2': '<32, 128, 1',
+                'b3c1': '<16, 128, 0', 'b3c2': '<16, 128, 1', 'b4c1': '<8, 128, 0',
+                'b4c2': '<8, 128, 2'}
+# x3 kernels carry a 4th template argument (FUSE: block 1's conv1 fused into b1c2)
+STAGE_FUSE = {'b1c2': 'true'}
 
 
 def profiled_traffic(kernel):
@@ -165,7 +167,10 @@ def roofline(stage_ms, B, precision):
     achieved = flops / (conv[dom] * 1e-3) / 1e12
     peak = PEAK_TF[precision]
     total = sum(conv_flops(s, B, T) for s in CONV_STAGES)
-    kname = 'sedx::conv3x3_%s%s' % ('x3_kernel' if precision == 'x3' else 'kernel', STAGE_KERNEL[dom])
+    if precision == 'x3':
+        kname = 'sedx::conv3x3_x3_kernel%s, %s>' % (STAGE_KERNEL[dom], STAGE_FUSE.get(dom, 'false'))
+    else:
+        kname = 'sedx::conv3x3_kernel%s>' % STAGE_KERNEL[dom]
     traffic = profiled_traffic(kname) if B == 32 else None
     return {'bound': 'mfma',
             'kernel': 'conv3x3_%s (%s)' % ('x3_kernel' if precision == 'x3' else 'kernel', dom),

@@ -35,6 +35,7 @@ struct DevWeights {
   float* bn0_mean = nullptr;
   float* bn0_bias = nullptr;
   float* c1_w = nullptr;
+  float* c1_wt = nullptr;
   float* c1_b = nullptr;
   float* wp[8] = {};    // packed conv weights: block k conv j -> index 2(k-1)+(j-1); [0] unused
   float* cb[8] = {};    // folded biases
@@ -241,7 +242,14 @@ sedx_status run_body(sedx_handle* h, int64_t B, const Geometry& g, float* ws, co
   float* P = ws + l.bufB;
   const int iB = (int)B;
   mark(h, 1, s);
-  launch_conv_c1(X0, iB, (int)g.T, w.c1_w, w.c1_b, A, s);
+  const bool x3 = h->precision == SEDX_PRECISION_X3;
+  if (x3) {
+    // block 1 as one launch: conv1 computed inside conv2's halo staging (the
+    // b1c1 stage is then just the zero-bordered copy of the bn0 output)
+    launch_block1_fused_x3(X0, iB, (int)g.T, A, w.c1_wt, w.c1_b, w.wx3[1], w.cb[1], nullptr, s);
+  } else {
+    launch_conv_c1(X0, iB, (int)g.T, w.c1_w, w.c1_b, A, s);
+  }
   struct L {
     const float* in;
     int T, F, cin, cout, idx, epi;
@@ -257,7 +265,9 @@ sedx_status run_body(sedx_handle* h, int64_t B, const Geometry& g, float* ws, co
   for (int i = 0; i < 7; ++i) {
     const L& c = layers[i];
     mark(h, 2 + i, s);
-    if (h->precision == SEDX_PRECISION_X3)
+    if (x3 && i == 0)
+      launch_block1_fused_x3(nullptr, iB, c.T, A, w.c1_wt, w.c1_b, w.wx3[c.idx], w.cb[c.idx], c.out, s);
+    else if (x3)
       launch_conv3x3_x3(c.in, iB, c.T, c.F, c.cin, c.cout, w.wx3[c.idx], w.cb[c.idx], c.out, c.epi, s);
     else
       launch_conv3x3(c.in, iB, c.T, c.F, c.cin, c.cout, w.wp[c.idx], w.cb[c.idx], c.out, c.epi, s);
@@ -685,6 +695,10 @@ sedx_status sedx_finalize_weights(sedx_handle* h) {
   add((void**)&W.bn0_mean, mu0.data(), 64 * 4);
   add((void**)&W.bn0_bias, bi0.data(), 64 * 4);
   add((void**)&W.c1_w, c1w.data(), c1w.size() * 4);
+  std::vector<float> c1wt(9 * 64);               // [tap][64]: channel pairs adjacent
+  for (int o = 0; o < 64; ++o)
+    for (int t = 0; t < 9; ++t) c1wt[t * 64 + o] = c1w[o * 9 + t];
+  add((void**)&W.c1_wt, c1wt.data(), c1wt.size() * 4);
   add((void**)&W.c1_b, c1b.data(), c1b.size() * 4);
   for (int i = 1; i < 8; ++i) {
     add((void**)&W.wp[i], packed[i].data(), packed[i].size() * 4);

@@ -28,12 +28,15 @@
 //     tap t's 12 MFMAs issue, across stage, chunk and tile boundaries.
 // The MFMA row -> pixel map is chosen per epilogue so that 2x2 pooling (and
 // the 8-bin freq mean) is an in-lane register sum.
+#include <algorithm>
+
 #include "sedx_internal.h"
 
 namespace sedx {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 
@@ -130,12 +133,19 @@ struct ConvGeom {
   static constexpr int TT = BM / F;
 };
 
-template <int F, int BN, int EPI>
+// FUSE (block 1 only): `in` is the bn0 output padded by one zero row/column
+// on each side, [B][T+2][F+2], and the kernel's input channels (Cin = 64) are
+// block 1's conv1 (Cin 1 -> 64, BN folded into w1/b1, ReLU) computed while
+// the halo is staged: the 525 MB conv1 activation never touches HBM.  The
+// conv1 arithmetic is the fma chain of conv_c1_kernel (same order, same bits).
+template <int F, int BN, int EPI, bool FUSE>
 __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict__ in, int B, int T,
                                                          int Cin, int Cout,
                                                          const uint4* __restrict__ wsp,
                                                          const float* __restrict__ bias,
-                                                         float* __restrict__ out) {
+                                                         float* __restrict__ out,
+                                                         const float* __restrict__ w1,
+                                                         const float* __restrict__ b1) {
   constexpr int BM = ConvGeom<F, BN>::BM, TT = ConvGeom<F, BN>::TT;
   constexpr int RT = TT + 2, CS = F + 2;
   constexpr int CSP = (EPI == EPI_POOL2) ? (F == 64 ? 72 : F == 32 ? 40 : 24)
@@ -147,7 +157,9 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
   constexpr int A_U4 = NPOS * 5;          // one halo image
   constexpr int W_U4 = BN * 4;            // one tap
   constexpr int WS_U4 = 3 * W_U4;         // one stage (kernel row)
-  constexpr int A_ITEMS = RT * CS * 2;
+  // staging items: (halo position, 8-channel half); FUSE: one item per halo
+  // position (all 16 channels: the chunk's conv1 weights are wave-uniform)
+  constexpr int A_ITEMS = FUSE ? RT * CS : 2 * RT * CS;
   constexpr int NA = (A_ITEMS + 511) / 512;
   constexpr int NW = (WS_U4 + 511) / 512;
 
@@ -218,6 +230,7 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
 
   float4 ra0[NA], ra1[NA];                // staged halo items (2 x 16 B each)
   bool rok[NA];                           // ... inside the image (else zero)
+  float xr[FUSE ? NA : 1][9];             // FUSE: conv1 input neighbourhoods
   uint4 rw0[NW], rw1[NW];                 // W stage x lives in rw(x & 1)
 
   // Staging loads and stores are branch-free (indices clamped, halo zeroes by
@@ -228,16 +241,26 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
 #pragma unroll
   for (int i = 0; i < NA; ++i) {
     const int idx = min(tid + i * 512, A_ITEMS - 1);
-    const int pos = idx >> 1, hh = idx & 1;
+    const int pos = FUSE ? idx : idx >> 1, hh = FUSE ? 0 : idx & 1;
     const int r = pos / CS, c = pos - r * CS;
     a_r[i] = r;
     a_f[i] = c - 1;
     a_fok[i] = c >= 1 && c <= F;
-    a_off[i] = min(max(c - 1, 0), F - 1) * Cin + 8 * hh;
+    a_off[i] = FUSE ? min(max(c - 1, 0), F - 1) : min(max(c - 1, 0), F - 1) * Cin + 8 * hh;
     a_rec[i] = (r * CSP + c) * 5 + hh;
   }
 #define SEDX_LOAD_A(c_)                                                                 \
-  {                                                                                     \
+  if constexpr (FUSE) {                                                                 \
+    /* 3x3 neighbourhood of every staged pixel in the padded bn0 output */              \
+    const float* in_b_ = in + (int64_t)(c_).b * (T + 2) * (F + 2);                      \
+    _Pragma("unroll") for (int i = 0; i < NA; ++i) {                                    \
+      const int t = (c_).t0 - 1 + a_r[i];                                               \
+      rok[i] = a_fok[i] && t >= 0 && t < T;                                             \
+      const float* x_ = in_b_ + (min(max(t, 0), T - 1) * (F + 2) + a_off[i]);           \
+      _Pragma("unroll") for (int k = 0; k < 9; ++k) xr[i][k] = x_[(k / 3) * (F + 2) + k % 3]; \
+    }                                                                                   \
+    asm volatile("" ::: "memory");                                                      \
+  } else {                                                                              \
     const float* in_b_ = in + (int64_t)(c_).b * T * F * Cin + (c_).chunk * 16;          \
     _Pragma("unroll") for (int i = 0; i < NA; ++i) {                                    \
       const int t = (c_).t0 - 1 + a_r[i];                                               \
@@ -250,15 +273,40 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
     }                                                                                   \
     asm volatile("" ::: "memory"); /* issue here: not sunk to the use */                \
   }
-#define SEDX_STORE_A(buf)                                                               \
+#define SEDX_STORE_A(buf, c_) SEDX_STORE_A_ITEMS(buf, c_, 0, NA)
+#define SEDX_STORE_A_ITEMS(buf, c_, i0, i1)                                             \
   {                                                                                     \
     uint4* dst_ = Abuf + (buf) * A_U4;                                                  \
-    _Pragma("unroll") for (int i = 0; i < NA; ++i) {                                    \
+    _Pragma("unroll") for (int i = (i0); i < (i1); ++i) {                               \
       uint4 hi, lo;                                                                     \
       const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);                                 \
-      split8(rok[i] ? ra0[i] : z, rok[i] ? ra1[i] : z, hi, lo);                         \
-      dst_[a_rec[i]] = hi;                                                              \
-      dst_[a_rec[i] + 2] = lo;                                                          \
+      if constexpr (FUSE) {                                                             \
+        /* the chunk's 16 conv1 channels, two per packed fma (w1 is [tap][64]:  */      \
+        /* wave-uniform scalar pairs); per channel the fma chain of conv_c1      */      \
+        const int ch0 = (c_).chunk * 16;                                                \
+        _Pragma("unroll") for (int hh = 0; hh < 2; ++hh) {                              \
+          f32x2 a2[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};               \
+          _Pragma("unroll") for (int k = 0; k < 9; ++k) {                               \
+            const f32x2 xx = {xr[i][k], xr[i][k]};                                      \
+            _Pragma("unroll") for (int j = 0; j < 4; ++j)                               \
+              a2[j] = __builtin_elementwise_fma(                                        \
+                  *reinterpret_cast<const f32x2*>(w1 + k * 64 + ch0 + 8 * hh + 2 * j), xx, a2[j]); \
+          }                                                                             \
+          float o[8];                                                                   \
+          _Pragma("unroll") for (int j = 0; j < 4; ++j) {                               \
+            const f32x2 bb = *reinterpret_cast<const f32x2*>(b1 + ch0 + 8 * hh + 2 * j); \
+            o[2 * j] = rok[i] ? fmaxf(a2[j].x + bb.x, 0.0f) : 0.0f;                     \
+            o[2 * j + 1] = rok[i] ? fmaxf(a2[j].y + bb.y, 0.0f) : 0.0f;                 \
+          }                                                                             \
+          split8(make_float4(o[0], o[1], o[2], o[3]), make_float4(o[4], o[5], o[6], o[7]), hi, lo); \
+          dst_[a_rec[i] + hh] = hi;                                                     \
+          dst_[a_rec[i] + 2 + hh] = lo;                                                 \
+        }                                                                               \
+      } else {                                                                          \
+        split8(rok[i] ? ra0[i] : z, rok[i] ? ra1[i] : z, hi, lo);                       \
+        dst_[a_rec[i]] = hi;                                                            \
+        dst_[a_rec[i] + 2] = lo;                                                        \
+      }                                                                                 \
     }                                                                                   \
     asm volatile("" ::: "memory");                                                      \
   }
@@ -386,7 +434,7 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
   SEDX_LOAD_A(cur);
   SEDX_LOAD_W(0, cur, 0);
   SEDX_LOAD_W(1, cur, 1);
-  SEDX_STORE_A(0);
+  SEDX_STORE_A(0, cur);
   SEDX_STORE_W(0, 0);
   SEDX_STORE_W(1, 1);
   SEDX_LOAD_W(0, cur, 2);
@@ -405,10 +453,10 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
   // register set just drained (W(n1, 1), W(n1, 2), W(n2, 0)).
 #ifdef SEDX_ABL_NOLDS     // diagnostics (tools/gpu_conv_bench.sh): drop the stage's LDS writes
 #define SEDX_ABL_STORE_W(rs, slot)
-#define SEDX_ABL_STORE_A(buf)
+#define SEDX_ABL_STORE_A(buf, c_)
 #else
 #define SEDX_ABL_STORE_W(rs, slot) SEDX_STORE_W(rs, slot)
-#define SEDX_ABL_STORE_A(buf) SEDX_STORE_A(buf)
+#define SEDX_ABL_STORE_A(buf, c_) SEDX_STORE_A(buf, c_)
 #endif
 #if defined(SEDX_ABL_NOLOAD) || defined(SEDX_ABL_NOLOADW)   // ... or its global loads
 #define SEDX_ABL_LOAD_W(rs, c_, ky_)
@@ -430,11 +478,19 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
     if ((KY) == 0) {                                                                    \
       SEDX_ABL_STORE_W((U) & 1, U);                                                     \
       SEDX_ABL_LOAD_W((U) & 1, n1, 1);                                                  \
-      SEDX_ABL_STORE_A((U) ^ 1);                                                        \
-      SEDX_ABL_LOAD_A(n2);                                                              \
+      if constexpr (FUSE) {  /* conv1 work spread over two stages */                    \
+        SEDX_STORE_A_ITEMS((U) ^ 1, n1, 0, 1);                                          \
+      } else {                                                                          \
+        SEDX_ABL_STORE_A((U) ^ 1, n1);                                                  \
+        SEDX_ABL_LOAD_A(n2);                                                            \
+      }                                                                                 \
     } else if ((KY) == 1) {                                                             \
       SEDX_ABL_STORE_W(((U) + 1) & 1, ((U) + 1) & 1);                                   \
       SEDX_ABL_LOAD_W(((U) + 1) & 1, n1, 2);                                            \
+      if constexpr (FUSE) {                                                             \
+        SEDX_STORE_A_ITEMS((U) ^ 1, n1, 1, NA);                                         \
+        SEDX_LOAD_A(n2);                                                                \
+      }                                                                                 \
     } else {                                                                            \
       SEDX_ABL_STORE_W((U) & 1, (U) & 1);                                               \
       SEDX_ABL_LOAD_W((U) & 1, n2, 0);                                                  \
@@ -490,18 +546,20 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
 #undef SEDX_STORE_W
 #undef SEDX_LOAD_A
 #undef SEDX_STORE_A
+#undef SEDX_STORE_A_ITEMS
 }
 
-template <int F, int BN, int EPI>
+template <int F, int BN, int EPI, bool FUSE = false>
 static void launch_x3_epi(const float* in, int B, int T, int Cin, int Cout, const uint4* wp,
-                          const float* bias, float* out, hipStream_t s) {
+                          const float* bias, float* out, hipStream_t s,
+                          const float* w1 = nullptr, const float* b1 = nullptr) {
   constexpr int TT = ConvGeom<F, BN>::TT;
   static int resident = 0;           // workgroups resident on the whole device
   if (!resident) {
     int dev = 0, ncu = 0, per_cu = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, conv3x3_x3_kernel<F, BN, EPI>, 512, 0);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, conv3x3_x3_kernel<F, BN, EPI, FUSE>, 512, 0);
     resident = (ncu > 0 ? ncu : 256) * (per_cu > 0 ? per_cu : 1);
   }
   const int ntiles = B * ((T + TT - 1) / TT) * (Cout / BN);
@@ -509,8 +567,8 @@ static void launch_x3_epi(const float* in, int B, int T, int Cin, int Cout, cons
   int grid = resident & ~7;
   if (grid < 8) grid = 8;
   if (grid > 8 * per_xcd) grid = 8 * per_xcd;
-  hipLaunchKernelGGL((conv3x3_x3_kernel<F, BN, EPI>), dim3(grid), dim3(512), 0, s, in, B, T, Cin, Cout,
-                     wp, bias, out);
+  hipLaunchKernelGGL((conv3x3_x3_kernel<F, BN, EPI, FUSE>), dim3(grid), dim3(512), 0, s, in, B, T, Cin,
+                     Cout, wp, bias, out, w1, b1);
 }
 
 template <int F, int BN>
@@ -555,6 +613,34 @@ void launch_conv3x3_x3(const float* in, int B, int T, int F, int Cin, int Cout, 
     default: break;
   }
 }
+
+// bn0 output [B][T][64] -> [B][T+2][66] with a zero border (the fused block-1
+// kernel's conv1 then needs no bounds tests)
+__global__ __launch_bounds__(256) void pad_x0_kernel(const float* __restrict__ x0, int B, int T,
+                                                     float* __restrict__ xp) {
+  const int64_t n = (int64_t)B * (T + 2) * 66;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int f = (int)(i % 66) - 1;
+    const int64_t bt = i / 66;
+    const int t = (int)(bt % (T + 2)) - 1;
+    const int64_t b = bt / (T + 2);
+    xp[i] = (t >= 0 && t < T && f >= 0 && f < 64) ? x0[(b * T + t) * 64 + f] : 0.0f;
+  }
+}
+
+void launch_block1_fused_x3(const float* x0, int B, int T, float* xpad, const float* w1, const float* b1,
+                            const void* wp, const float* bias, float* out, hipStream_t s) {
+  if (x0) {
+    const int64_t n = (int64_t)B * (T + 2) * 66;
+    const int blocks = (int)std::min<int64_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(pad_x0_kernel, dim3(blocks), dim3(256), 0, s, x0, B, T, xpad);
+  }
+  if (out)
+    launch_x3_epi<64, 64, EPI_POOL2, true>(xpad, B, T, 64, 64, static_cast<const uint4*>(wp), bias, out, s,
+                                           w1, b1);
+}
+
+size_t block1_pad_floats(int B, int T) { return (size_t)B * (T + 2) * 66; }
 
 #ifdef SEDX_CONV_STAMPS
 void conv_stamps_rw(unsigned long long* out8, bool reset) {

@@ -70,6 +70,12 @@ void launch_conv3x3(const float* in, int B, int T, int F, int Cin, int Cout,
 // Cout == 64 else 128), slots XOR-swizzled by ((n >> 2) & 3).
 void launch_conv3x3_x3(const float* in, int B, int T, int F, int Cin, int Cout, const void* wp,
                        const float* bias, float* out, int epi, hipStream_t s);
+// block 1 of the CNN in one conv launch (x3): with x0, pads the bn0 output
+// into xpad (block1_pad_floats(B, T) floats); with out, runs conv2 with conv1
+// computed while its halo is staged (conv_x3.hip)
+void launch_block1_fused_x3(const float* x0, int B, int T, float* xpad, const float* w1, const float* b1,
+                            const void* wp, const float* bias, float* out, hipStream_t s);
+size_t block1_pad_floats(int B, int T);
 
 // ---- sequence / head ------------------------------------------------------
 // C[M][N] = act(A[M][K] . W[N][K]^T + bias[N]);  act: 0 none, 1 relu
