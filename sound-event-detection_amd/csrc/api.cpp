@@ -51,6 +51,11 @@ struct DevWeights {
   float* bfc = nullptr;
   float* wac = nullptr;    // [nac][512]
   float* bac = nullptr;
+  // x3 (split bf16) packs of the linear weights for linear_x3.hip
+  void* w_ih_x3 = nullptr;
+  void* wqkv_x3 = nullptr;
+  void* wfc_x3 = nullptr;
+  void* wac_x3 = nullptr;
   // gamma
   float2* g_twiddle = nullptr;
   float* g_window = nullptr;
@@ -279,19 +284,27 @@ sedx_status run_body(sedx_handle* h, int64_t B, const Geometry& g, float* ws, co
   float* Hs = A + align_up((size_t)M * 1536);     // [M][512]
   float* O = Hs + align_up((size_t)M * 512);      // [M][512]
   float* LG = O + align_up((size_t)M * 512);      // [M][nac]
+  // GEMMs: x3 split-bf16 MFMA in x3 mode, fp32 MFMA in exact mode
+  auto linear = [&](const float* a, const float* wf, void* wx, int n, int bn, const float* bias, float* c,
+                    int act) {
+    if (x3)
+      launch_linear_x3(a, M, 512, wx, n, bn, bias, c, act, s);
+    else
+      launch_linear(a, M, 512, wf, n, bias, c, act, s);
+  };
   if (is_gru(h)) {
-    launch_linear(S, M, 512, w.w_ih, 1536, w.b_ih, G, 0, s);
+    linear(S, w.w_ih, w.w_ih_x3, 1536, 128, w.b_ih, G, 0);
     if (h->gru_simple)
       launch_gru(G, iB, (int)g.T3, w.whhT, w.bhh, Hs, s);
     else
       launch_gru_coop(G, iB, (int)g.T3, w.whh, w.bhh, Hs, LG + align_up((size_t)M * h->nac), s);
   } else {
-    launch_linear(S, M, 512, w.wqkv, 1536, w.bqkv, G, 0, s);
+    linear(S, w.wqkv, w.wqkv_x3, 1536, 128, w.bqkv, G, 0);
     launch_mha(G, iB, (int)g.T3, O, s);
-    launch_linear(O, M, 512, w.wfc, 512, w.bfc, Hs, 1, s);
+    linear(O, w.wfc, w.wfc_x3, 512, 128, w.bfc, Hs, 1);
   }
   mark(h, 10, s);
-  launch_linear(Hs, M, 512, w.wac, h->nac, w.bac, LG, 0, s);
+  linear(Hs, w.wac, w.wac_x3, h->nac, 64, w.bac, LG, 0);
   launch_att_head(LG, iB, (int)g.T3, h->cfg.classes_num, h->nac, (int)g.out_frames, d_fw, d_clip,
                   is_gru(h) ? d_emb : nullptr, s);
   if (!is_gru(h) && d_emb) launch_transpose_btd(Hs, iB, (int)g.T3, 512, d_emb, s);
@@ -563,6 +576,30 @@ sedx_status sedx_finalize_weights(sedx_handle* h) {
 
   // ---- head ----
   std::vector<float> w_ih, b_ih, whhT, bhh, wqkv, bqkv, wfc, bfc, whh_nat;
+  // W [N][K] -> [N/BN][K/16][BN][4 slots x 8 bf16], slot c at c ^ ((n>>2)&3)
+  // (the conv x3 layout with a single tap; linear_x3.hip)
+  auto pack_linear_x3 = [](const std::vector<float>& W, int N, int K, int BN) {
+    std::vector<uint16_t> px((size_t)N * K * 2, 0);
+    auto rne = [](float x) -> uint32_t {
+      uint32_t u;
+      std::memcpy(&u, &x, 4);
+      return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
+    };
+    for (int o = 0; o < N; ++o)
+      for (int i = 0; i < K; ++i) {
+        const float x = W[(size_t)o * K + i];
+        const uint32_t hb = rne(x);
+        const uint32_t hbits = hb << 16;
+        float hf;
+        std::memcpy(&hf, &hbits, 4);
+        const uint32_t lb = rne(x - hf);
+        const int nt = o / BN, n = o % BN, ks = i / 16, k = i % 16, sw = (n >> 2) & 3;
+        const size_t rec = (((size_t)nt * (K / 16) + ks) * BN + n) * 32;
+        px[rec + 8 * ((k / 8) ^ sw) + (k % 8)] = (uint16_t)hb;
+        px[rec + 8 * ((2 + k / 8) ^ sw) + (k % 8)] = (uint16_t)lb;
+      }
+    return px;
+  };
   if (is_gru(h)) {
     w_ih.resize(1536 * 512);
     b_ih.resize(1536);
@@ -719,6 +756,18 @@ sedx_status sedx_finalize_weights(sedx_handle* h) {
   }
   add((void**)&W.wac, wac.data(), wac.size() * 4);
   add((void**)&W.bac, bac.data(), bac.size() * 4);
+  std::vector<uint16_t> w_ih_x3, wqkv_x3, wfc_x3, wac_x3;
+  if (is_gru(h)) {
+    w_ih_x3 = pack_linear_x3(w_ih, 1536, 512, 128);
+    add(&W.w_ih_x3, w_ih_x3.data(), w_ih_x3.size() * 2);
+  } else {
+    wqkv_x3 = pack_linear_x3(wqkv, 1536, 512, 128);
+    wfc_x3 = pack_linear_x3(wfc, 512, 512, 128);
+    add(&W.wqkv_x3, wqkv_x3.data(), wqkv_x3.size() * 2);
+    add(&W.wfc_x3, wfc_x3.data(), wfc_x3.size() * 2);
+  }
+  wac_x3 = pack_linear_x3(wac, h->nac, 512, 64);
+  add(&W.wac_x3, wac_x3.data(), wac_x3.size() * 2);
   if (!g_wT.empty()) {
     add((void**)&W.g_twiddle, g_tw.data(), g_tw.size() * 4);
     add((void**)&W.g_window, g_win.data(), g_win.size() * 4);

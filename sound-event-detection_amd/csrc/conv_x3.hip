@@ -437,9 +437,17 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
   SEDX_STORE_A(0, cur);
   SEDX_STORE_W(0, 0);
   SEDX_STORE_W(1, 1);
-  SEDX_LOAD_W(0, cur, 2);
-  SEDX_LOAD_W(1, n1, 0);
-  SEDX_LOAD_A(n1);
+  // pending loads enter the loop in the order the loop's back edge leaves
+  // them, so the waitcnt bookkeeping at the loop header stays exact
+  if constexpr (FUSE) {
+    SEDX_LOAD_W(0, cur, 2);
+    SEDX_LOAD_A(n1);
+    SEDX_LOAD_W(1, n1, 0);
+  } else {
+    SEDX_LOAD_A(n1);
+    SEDX_LOAD_W(0, cur, 2);
+    SEDX_LOAD_W(1, n1, 0);
+  }
   __syncthreads();
   SEDX_READ_FRAGS(0, 0, 0, 0);
 

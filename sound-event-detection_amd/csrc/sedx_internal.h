@@ -81,6 +81,10 @@ size_t block1_pad_floats(int B, int T);
 // C[M][N] = act(A[M][K] . W[N][K]^T + bias[N]);  act: 0 none, 1 relu
 void launch_linear(const float* A, int M, int K, const float* W, int N, const float* bias,
                    float* C, int act, hipStream_t s);
+// x3 (split-bf16 MFMA) GEMM, W pre-packed by the host (linear_x3.hip);
+// K % 32 == 0, N % BN == 0, BN in {64, 128}
+void launch_linear_x3(const float* A, int M, int K, const void* Wp, int N, int BN, const float* bias,
+                      float* C, int act, hipStream_t s);
 
 // bi-GRU recurrence.  G [B][T][1536] = x W_ih^T + b_ih (both dirs);
 // whhT [2][256][768]; bhh [2][768]; H [B][T][512]

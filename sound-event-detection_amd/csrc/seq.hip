@@ -202,86 +202,76 @@ void launch_mha(const float* QKV, int B, int T, float* O, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------------------
-// AttBlock finish.  grid B, block 64 (thread = class).
+// AttBlock finish (pytorch/models.py:161-175, :84-95, :65-81).  One clip per
+// block; thread = (class slot c = tid / 8, t-lane l = tid % 8): each thread
+// walks t = l, l+8, ... and the 8 lanes of a class reduce with shuffles, so
+// the T-long sums are 8-way parallel instead of one serial loop per class.
+// cla is staged per 128-frame chunk in LDS for the coalesced framewise
+// (x8 repeat) and embedding writes.
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ float att_exp_(float a) {
+  return expf(fminf(fmaxf(a, -10.0f), 10.0f)) + 1e-6f;
+}
+__device__ __forceinline__ float sum8_(float v) {      // over the 8 lanes of a class
+  v += __shfl_xor(v, 1);
+  v += __shfl_xor(v, 2);
+  v += __shfl_xor(v, 4);
+  return v;
+}
+
 __global__ __launch_bounds__(256) void att_head_kernel(const float* __restrict__ logits, int T,
                                                        int C, int ldl, int out_frames,
                                                        float* __restrict__ fw,
                                                        float* __restrict__ clip,
                                                        float* __restrict__ emb) {
-  // one clip per block; T-chunks of 128 frames staged in LDS.  Pass 1: per
-  // class sum over T of exp(clamp(att)) + 1e-6 (t order).  Pass 2: norm * cla
-  // accumulated in t order; cla kept in LDS for the framewise / embedding
-  // writes, which all 256 threads perform coalesced.
   constexpr int TC = 128;
-  __shared__ float s_att[TC][33];
   __shared__ float s_cla[TC][33];
-  __shared__ float s_sum[32];
+  __shared__ float s_last[32];
   const int b = blockIdx.x, tid = threadIdx.x;
+  const int cs = tid >> 3, l = tid & 7;
   const float* lg = logits + (int64_t)b * T * ldl;
-  // classes are processed 32 at a time (C = 25 on the reference path)
   for (int c0 = 0; c0 < C; c0 += 32) {
     const int nc = min(32, C - c0);
-    float sum = 0.f, acc = 0.f, last = 0.f;
-    for (int pass = 0; pass < 2; ++pass) {
-      for (int t0 = 0; t0 < T; t0 += TC) {
-        const int nt = min(TC, T - t0);
-        __syncthreads();
-        for (int i = tid; i < nt * 32; i += 256) {
-          const int t = i >> 5, c = i & 31;
-          if (c < nc) {
-            s_att[t][c] = lg[(int64_t)(t0 + t) * ldl + c0 + c];
-            s_cla[t][c] = lg[(int64_t)(t0 + t) * ldl + C + c0 + c];
-          }
+    const bool act = cs < nc;
+    const int c = c0 + cs;
+    // pass 1: sum over t of exp(clamp(att)) + 1e-6
+    float sum = 0.f;
+    if (act)
+      for (int t = l; t < T; t += 8) sum += att_exp_(lg[(int64_t)t * ldl + c]);
+    sum = sum8_(sum);
+    const float inv_tot = 1.0f / sum;
+    // pass 2: clipwise = sum_t norm_att * sigmoid(cla); cla -> LDS -> outputs
+    float acc = 0.f;
+    for (int t0 = 0; t0 < T; t0 += TC) {
+      const int nt = min(TC, T - t0);
+      __syncthreads();
+      if (act)
+        for (int t = l; t < nt; t += 8) {
+          const int64_t o = (int64_t)(t0 + t) * ldl + c;
+          const float cl = 1.0f / (1.0f + expf(-lg[o + C]));
+          acc += (att_exp_(lg[o]) * inv_tot) * cl;
+          s_cla[t][cs] = cl;
         }
-        __syncthreads();
-        if (tid < nc) {
-          const int c = tid;
-          if (pass == 0) {
-            for (int t = 0; t < nt; ++t) sum += expf(fminf(fmaxf(s_att[t][c], -10.0f), 10.0f)) + 1e-6f;
-          } else {
-            const float tot = s_sum[c];
-            for (int t = 0; t < nt; ++t) {
-              const float na = (expf(fminf(fmaxf(s_att[t][c], -10.0f), 10.0f)) + 1e-6f) / tot;
-              const float cl = sigmoidf_(s_cla[t][c]);
-              acc += na * cl;
-              s_cla[t][c] = cl;
-              last = cl;
-            }
-          }
-        }
-        if (pass == 1) {
-          __syncthreads();
-          // framewise: frames 8(t0+t) .. +7, classes c0..c0+nc
-          for (int i = tid; i < nt * 8 * nc; i += 256) {
-            const int c = i % nc, fr = i / nc;
-            const int t = fr >> 3;
-            fw[((int64_t)b * out_frames + 8 * t0 + fr) * C + c0 + c] = s_cla[t][c];
-          }
-          if (emb)
-            for (int i = tid; i < nt * nc; i += 256) {
-              const int t = i % nt, c = i / nt;
-              emb[((int64_t)b * C + c0 + c) * T + t0 + t] = s_cla[t][c];
-            }
-        }
+      __syncthreads();
+      for (int i = tid; i < nt * 8 * nc; i += 256) {
+        const int cc = i % nc, fr = i / nc;
+        fw[((int64_t)b * out_frames + 8 * t0 + fr) * C + c0 + cc] = s_cla[fr >> 3][cc];
       }
-      if (pass == 0) {
-        if (tid < nc) s_sum[tid] = sum;
-        __syncthreads();
-      }
+      if (emb)
+        for (int i = tid; i < nt * nc; i += 256) {
+          const int t = i % nt, cc = i / nt;
+          emb[((int64_t)b * C + c0 + cc) * T + t0 + t] = s_cla[t][cc];
+        }
+      if (t0 + nt == T && tid < nc) s_last[tid] = s_cla[nt - 1][tid];
     }
+    acc = sum8_(acc);
+    if (act && l == 0) clip[(int64_t)b * C + c] = acc;
     __syncthreads();
-    if (tid < nc) {
-      clip[(int64_t)b * C + c0 + tid] = acc;
-      s_sum[tid] = last;            // value repeated into the GRU padding frames
-    }
-    __syncthreads();
-    const int npad = out_frames - 8 * T;
+    const int npad = out_frames - 8 * T;          // GRU: last frame repeated
     for (int i = tid; i < npad * nc; i += 256) {
-      const int c = i % nc, f = 8 * T + i / nc;
-      fw[((int64_t)b * out_frames + f) * C + c0 + c] = s_sum[c];
+      const int cc = i % nc, f = 8 * T + i / nc;
+      fw[((int64_t)b * out_frames + f) * C + c0 + cc] = s_last[cc];
     }
-    __syncthreads();
   }
 }
 
