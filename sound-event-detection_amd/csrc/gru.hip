@@ -35,21 +35,26 @@ namespace sedx {
 typedef float f32x16_g __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8_g __attribute__((ext_vector_type(8)));
 
-__device__ __forceinline__ uint32_t g_bf16_rne(float x) {
-  const uint32_t u = __float_as_uint(x);
-  return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
-}
+typedef __bf16 bf16x2_g __attribute__((ext_vector_type(2)));
+// x = hi + lo, hi = bf16_rne(x), lo = bf16_rne(x - hi) (v_cvt_pk_bf16_f32)
 __device__ __forceinline__ void g_split8(const float* v, uint4& hi, uint4& lo) {
-  uint32_t hh[8], ll[8];
+  uint32_t hh[4], ll[4];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    hh[i] = g_bf16_rne(v[i]);
-    ll[i] = g_bf16_rne(v[i] - __uint_as_float(hh[i] << 16));
+  for (int i = 0; i < 4; ++i) {
+    const bf16x2_g h2 = {(__bf16)v[2 * i], (__bf16)v[2 * i + 1]};
+    hh[i] = __builtin_bit_cast(uint32_t, h2);
+    const bf16x2_g l2 = {(__bf16)(v[2 * i] - __uint_as_float(hh[i] << 16)),
+                         (__bf16)(v[2 * i + 1] - __uint_as_float(hh[i] & 0xFFFF0000u))};
+    ll[i] = __builtin_bit_cast(uint32_t, l2);
   }
-  hi = make_uint4(hh[0] | (hh[1] << 16), hh[2] | (hh[3] << 16), hh[4] | (hh[5] << 16), hh[6] | (hh[7] << 16));
-  lo = make_uint4(ll[0] | (ll[1] << 16), ll[2] | (ll[3] << 16), ll[4] | (ll[5] << 16), ll[6] | (ll[7] << 16));
+  hi = make_uint4(hh[0], hh[1], hh[2], hh[3]);
+  lo = make_uint4(ll[0], ll[1], ll[2], ll[3]);
 }
-__device__ __forceinline__ float g_sigmoid(float x) { return 1.0f / (1.0f + expf(-x)); }
+// gates on v_exp_f32 (__expf): |error| ~1e-7 against the libm forms, well
+// inside the 1e-3 framewise bar; tanh(x) = 2 / (1 + e^(-2x)) - 1 saturates
+// correctly at both ends
+__device__ __forceinline__ float g_sigmoid(float x) { return __frcp_rn(1.0f + __expf(-x)); }
+__device__ __forceinline__ float g_tanh(float x) { return 2.0f * __frcp_rn(1.0f + __expf(-2.0f * x)) - 1.0f; }
 __device__ __forceinline__ unsigned g_ld(const unsigned* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // sc1
 }
@@ -197,17 +202,27 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
         for (int i = tid; i < 32 * 32; i += 768) hprev[i >> 5][i & 31] = 0.f;
       } else {
         const float* src = Xs + ((gs - 1) & 1) * 32 * 256;
-        for (int it = tid; it < 32 * 32; it += 768) {
-          const int c = it >> 5, oct = it & 31;
+        // all of a thread's loads are issued before any is consumed (one L2
+        // round trip per step, not one per item)
+        float vv[2][8];
+#pragma unroll
+        for (int k2 = 0; k2 < 2; ++k2) {
+          const int it = min(tid + 768 * k2, 32 * 32 - 1);
           const unsigned long long* q =
-              reinterpret_cast<const unsigned long long*>(src + c * 256 + 8 * oct);
-          float v[8];
+              reinterpret_cast<const unsigned long long*>(src + (it >> 5) * 256 + 8 * (it & 31));
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const unsigned long long w = __hip_atomic_load(q + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            v[2 * e] = __uint_as_float((uint32_t)w);
-            v[2 * e + 1] = __uint_as_float((uint32_t)(w >> 32));
+            vv[k2][2 * e] = __uint_as_float((uint32_t)w);
+            vv[k2][2 * e + 1] = __uint_as_float((uint32_t)(w >> 32));
           }
+        }
+#pragma unroll
+        for (int k2 = 0; k2 < 2; ++k2) {
+          const int it = tid + 768 * k2;
+          if (it >= 32 * 32) break;
+          const int c = it >> 5, oct = it & 31;
+          const float* v = vv[k2];
           uint4 hi, lo;
           g_split8(v, hi, lo);
           const int ks = oct >> 1, hh = oct & 1, sw = (c >> 2) & 3;
@@ -255,7 +270,7 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
             const float ghn = (((part[0][2][c][u] + part[1][2][c][u]) + part[2][2][c][u]) + part[3][2][c][u]) + bn;
             const float r = g_sigmoid(gi[i][0] + ghr);
             const float z = g_sigmoid(gi[i][1] + ghz);
-            const float n = tanhf(gi[i][2] + r * ghn);
+            const float n = g_tanh(gi[i][2] + r * ghn);
             hvs[i] = n + z * (hprev[c][u] - n);
           }
           float* xp = dst + c * 256 + 32 * p + u;
