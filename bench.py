@@ -117,7 +117,8 @@ def measure(model, wave, args, world, rank, dev):
         step()
         torch.cuda.synchronize()
         lat.append((time.perf_counter() - a) * 1e3 / B)
-    return value, elapsed, statistics.median(lat)
+    lat.sort()
+    return value, elapsed, statistics.median(lat), lat[min(len(lat) - 1, int(0.99 * len(lat)))]
 
 
 def stage_times(model, wave, dev, reps):
@@ -142,7 +143,7 @@ def stage_times(model, wave, dev, reps):
 # command (tools/profile_round.sh -> tools/pmc_summary.py; FETCH_SIZE x2 per
 # the gfx950 correction + WRITE_SIZE), committed under profiles/.
 PROFILE_SUMMARY = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles',
-                               'r01b_kernel_summary.json')
+                               'r01c_kernel_summary.json')
 STAGE_KERNEL = {'b1c2': '<64, 64, 1', 'b2c1': '<32, 128, 0', 'b2c2': '<32, 128, 1',
                 'b3c1': '<16, 128, 0', 'b3c2': '<16, 128, 1', 'b4c1': '<8, 128, 0',
                 'b4c2': '<8, 128, 2'}
@@ -185,6 +186,44 @@ def roofline(stage_ms, B, precision):
             'conv_stack_tflops': round(total / (sum(conv.values()) * 1e-3) / 1e12, 2)}
 
 
+FRONTEND_BYTES_PER_CLIP = 160000 * 4 + 1001 * 64 * 4   # waveform in + X0 out
+
+
+def side_measurements(model, wave, args, dev, stage_ms):
+    """Secondary numbers on rank 0 (not the headline): the frontend's achieved
+    HBM rate, GPU event extraction for the batch, and window mode (predict.py
+    semantics: 6 x 5 s windows per 10 s clip, merged + averaged)."""
+    B = wave.shape[0]
+    out = {}
+    if stage_ms and stage_ms.get('frontend'):
+        out['frontend_gbps'] = round(B * FRONTEND_BYTES_PER_CLIP / (stage_ms['frontend'] * 1e-3) / 1e9, 1)
+    with torch.no_grad():
+        fw = model(wave)['framewise_output']
+    params = dict(inference.DEFAULT_PREDICT_PARAMS)
+    inference.event_pairs(fw, params)
+    torch.cuda.synchronize()
+    reps = 10
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        n_ev = len(inference.event_pairs(fw, params))
+    out['events_ms_per_batch'] = round((time.perf_counter() - t0) / reps * 1e3, 4)
+    out['events_per_batch'] = n_ev
+    with torch.no_grad():
+        for _ in range(2):
+            inference.predict_windows(model, wave, 5, 1)
+        torch.cuda.synchronize()
+        reps = max(3, min(args.steps, 10))
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            inference.predict_windows(model, wave, 5, 1)
+        torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    out['value_window_mode'] = {'value': round(B * reps / el, 2), 'unit': 'clips/s',
+                                'windows_per_clip': 6, 'note': '5 s windows, 1 s stride, merged + '
+                                                             'avg_merge on the GPU (predict.py:297-349)'}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -209,7 +248,7 @@ def main():
     B = args.batch
     wave = torch.from_numpy(synth.make_waveforms(B, 10.0, 16000, seed=1234 + rank)).to(dev)
 
-    value, elapsed, p50 = measure(model, wave, args, world, rank, dev)
+    value, elapsed, p50, p99 = measure(model, wave, args, world, rank, dev)
     stage_ms = roof = None
     if args.mode == 'clip':
         stage_ms = stage_times(model, wave, dev, max(3, min(args.steps, 10)))
@@ -217,11 +256,15 @@ def main():
     exact = None
     if not args.no_exact and args.precision != 'exact':
         model.set_precision('exact')
-        ev, _, ep50 = measure(model, wave, args, world, rank, dev)
+        ev, _, ep50, _ = measure(model, wave, args, world, rank, dev)
         exact = {'value': round(ev, 2), 'ms_per_clip_p50': round(ep50, 4)}
         if args.mode == 'clip':
             exact['roofline'] = roofline(stage_times(model, wave, dev, 3), B, 'exact')
         model.set_precision(args.precision)
+
+    extra = {}
+    if args.mode == 'clip' and rank == 0:
+        extra = side_measurements(model, wave, args, dev, stage_ms)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -240,9 +283,11 @@ def main():
                        'batch_per_gpu': B, 'global_batch': B * world, 'clip_seconds': 10,
                        'sample_rate': 16000, 'mode': args.mode, 'precision': args.precision,
                        'parallelism': 'dp%d clip-sharded, RCCL gather of framewise' % world},
+            'ms_per_clip_p99': round(p99, 4),
             'roofline': roof, 'cpu_baseline': cpu, 'stage_ms': stage_ms,
             'value_exact_fp32': exact,
         }
+        line.update(extra)
         if cpu:
             line['speedup_vs_cpu'] = round(value / cpu['value'], 1)
         print(json.dumps(line))

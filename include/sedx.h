@@ -103,6 +103,15 @@ sedx_status sedx_forward(sedx_handle* h, const float* d_wave, int64_t B, int64_t
                          float* d_framewise, float* d_clipwise, float* d_embedding,
                          void* d_workspace, size_t workspace_bytes, void* stream);
 
+/* Same forward on int16 waveforms as packed in the reference's HDF5 files
+ * (utils/features.py:313-317, :370): the loader's int16_to_float32
+ * (utils/data_generator.py:39, utils/utilities.py:78-79: float64 x / 32767
+ * rounded to float32) is fused into the frontend's loads, halving the input
+ * bytes.  Bit-identical to sedx_forward on the dequantised waveform. */
+sedx_status sedx_forward_i16(sedx_handle* h, const int16_t* d_wave, int64_t B, int64_t L,
+                             float* d_framewise, float* d_clipwise, float* d_embedding,
+                             void* d_workspace, size_t workspace_bytes, void* stream);
+
 /* Gamma branch (models.py:636-640): input is the [B, 64, T] feature matrix
  * that the reference model receives (int16-dequantised gammatone dB). */
 sedx_status sedx_forward_features(sedx_handle* h, const float* d_feat, int64_t B, int64_t T,
@@ -137,6 +146,17 @@ sedx_status sedx_forward_windows(sedx_handle* h, const float* d_audio, int64_t n
 sedx_status sedx_window_workspace_size(const sedx_handle* h, int64_t n_clips, int64_t L_clip,
                                        float sample_duration, float overlap_value,
                                        int32_t pad_clip, size_t* bytes);
+/* Voting variant (inference_prob_vote, pytorch/main_strong.py:1058-1097):
+ * every window's framewise output is binarised, x > bin_thres[k] (host f64
+ * [classes_num]; the reference passes sed_low_threshold, main_strong.py:1082,
+ * binarize_pred :870-883), and the 0/1 windows are overlap-added with
+ * utilities.merge — no avg_merge.  d_votes [n_clips, merged_frames,
+ * classes_num] holds the vote counts (exact small integers) for
+ * sedx_events_device(mode = 1).  Workspace: sedx_window_workspace_size. */
+sedx_status sedx_forward_windows_vote(sedx_handle* h, const float* d_audio, int64_t n_clips,
+                                      int64_t L_clip, float sample_duration, float overlap_value,
+                                      int32_t pad_clip, const double* bin_thres, float* d_votes,
+                                      void* d_workspace, size_t workspace_bytes, void* stream);
 
 /* Arithmetic of the 9-layer conv stack (96.8 % of the FLOPs).
  *  SEDX_PRECISION_X3    (default) bf16 MFMA with a 3-term hi/lo operand split
@@ -171,6 +191,30 @@ sedx_status sedx_events(const float* h_framewise, int64_t n_clips, int64_t T, in
                         int32_t use_low_thres, const int64_t* n_smooth,
                         const int64_t* n_salt, int32_t* h_events, int64_t capacity,
                         int64_t* n_events);
+
+/* The same thresholding on the GPU, one thread per (clip, class) series, no
+ * host round trip (asynchronous on `stream`; the device that owns d_x must be
+ * current).
+ *   mode 0: activity_detection (utils/vad.py:11-45) of framewise
+ *           probabilities, exactly as sedx_events;
+ *   mode 1: activity_detection_binary (utils/vad.py:47-106) of window vote
+ *           counts from sedx_forward_windows_vote, as
+ *           frame_binary_prediction_to_event_prediction
+ *           (utils/utilities.py:216-276) calls it; high_thres is unused there
+ *           (may be NULL), overlap_value / sample_duration give its blocks.
+ *   d_x       [n_clips, T, C] device
+ *   d_events  int32 [capacity][4] (clip, class, bgn, fin) in (clip, class,
+ *             time) order; events past capacity are dropped
+ *   d_info    int64 [2]: total number of events (may exceed capacity), and 1
+ *             where the reference raises IndexError (see sedx_events)
+ *   d_workspace >= sedx_events_workspace_size(n_clips, C) bytes. */
+sedx_status sedx_events_workspace_size(int64_t n_clips, int64_t C, size_t* bytes);
+sedx_status sedx_events_device(const float* d_x, int64_t n_clips, int64_t T, int64_t C,
+                               const double* high_thres, const double* low_thres,
+                               int32_t use_low_thres, const int64_t* n_smooth, const int64_t* n_salt,
+                               int32_t mode, float overlap_value, int32_t sample_duration,
+                               int32_t* d_events, int64_t capacity, int64_t* d_info,
+                               void* d_workspace, size_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -391,6 +391,85 @@ def activity_detection(x, thres, low_thres=None, n_smooth=1, n_salt=0):
     return remove_salt_noise(pairs, n_salt)
 
 
+def binarize_pred(pred, thres):
+    """pytorch/main_strong.py:870-883 (float64 0/1; per-class list or scalar
+    threshold).  The element compare is made in float64 (an np.float32 element
+    against a float64 threshold)."""
+    C = pred.shape[2]
+    t = np.asarray(list(thres) if isinstance(thres, (list, tuple, np.ndarray)) else [thres] * C,
+                   np.float64)
+    return (pred.astype(np.float64) > t[None, None, :]).astype(np.float64)
+
+
+def activity_detection_binary(x, overlap_value, sample_duration, thres, low_thres=None,
+                              n_smooth=1, n_salt=0):
+    """utils/vad.py:47-106: locts from 100*overlap-frame blocks with at least
+    num_overlaps votes (avg_merge schedule; the last block is never scanned);
+    ``thres`` is unused, as in the reference."""
+    ov = int(100 * overlap_value)
+    interval = sample_duration * 100 - ov
+    locts = []
+    for i in range(0, x.shape[0] - ov, ov):
+        if i < interval:
+            nov = i // ov + 1
+        elif i >= x.shape[0] - interval:
+            nov = ((x.shape[0] - i) // ov) + 1
+        else:
+            nov = sample_duration
+        locts.extend(int(j) + i for j in np.where(x[i:i + ov] >= nov)[0])
+    pairs = find_bgn_fin_pairs(locts)
+    if low_thres is not None:
+        pairs = second_threshold(x, pairs, low_thres)
+    pairs = smooth(pairs, n_smooth)
+    return remove_salt_noise(pairs, n_salt)
+
+
+def predict_windows_vote(sd, model_type, audio, sample_rate, sample_duration, overlap_value,
+                         bin_thres, pad_clip_to=None):
+    """inference_prob_vote window loop (pytorch/main_strong.py:1058-1097):
+    binarised windows merged with utilities.merge, no avg_merge."""
+    audio_duration = len(audio) / float(sample_rate)
+    if pad_clip_to is not None:
+        audio = pad_truncate_sequence(audio, pad_clip_to)
+    merged, prev = None, None
+    for num_segment, start in enumerate(window_starts(audio_duration, sample_duration,
+                                                      overlap_value), start=1):
+        s = int(start * sample_rate)
+        seg = audio[s:int(sample_duration * sample_rate) + s]
+        if pad_clip_to is None:
+            seg = pad_truncate_sequence(seg, int(sample_rate * sample_duration))
+        seg = torch.Tensor(np.asarray(seg))[None, :]
+        curr = binarize_pred(forward(sd, model_type, wave=seg)['framewise_output'].numpy(), bin_thres)
+        if num_segment == 1:
+            merged = curr
+        elif num_segment == 2:
+            merged = merge(prev, curr, sample_duration, num_segment, overlap_value)
+        else:
+            merged = merge(merged, curr, sample_duration, num_segment, overlap_value)
+        prev = curr
+    return merged
+
+
+def events_from_votes(votes, overlap_value, sample_duration, params, audio_name='test',
+                      frames_per_second=FRAMES_PER_SECOND):
+    """frame_binary_prediction_to_event_prediction (utils/utilities.py:216-276)."""
+    N, T, C = votes.shape
+
+    def as_list(v):
+        return list(v) if isinstance(v, (list, tuple, np.ndarray)) else [v] * C
+
+    lo = as_list(params['sed_low_threshold'])
+    ns, nsalt = as_list(params['n_smooth']), as_list(params['n_salt'])
+    ev = []
+    for n in range(N):
+        for k in range(C):
+            for b, f in activity_detection_binary(votes[n, :, k], overlap_value, sample_duration, None,
+                                                  lo[k], ns[k], nsalt[k]):
+                ev.append({'filename': audio_name, 'onset': b / float(frames_per_second),
+                           'offset': f / float(frames_per_second), 'event_label': LABELS[k]})
+    return ev
+
+
 def events_from_framewise(framewise, params, audio_name='test',
                           frames_per_second=FRAMES_PER_SECOND, sort=True):
     """frame_prediction_to_event_prediction_v2 (pytorch/predict.py:57-121 ==

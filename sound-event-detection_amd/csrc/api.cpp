@@ -836,14 +836,14 @@ sedx_status sedx_workspace_size(const sedx_handle* h, int64_t B, int64_t L_or_T,
   return SEDX_OK;
 }
 
-sedx_status sedx_forward(sedx_handle* h, const float* d_wave, int64_t B, int64_t L,
-                         float* d_framewise, float* d_clipwise, float* d_embedding,
-                         void* d_workspace, size_t workspace_bytes, void* stream) {
+static sedx_status forward_wave(sedx_handle* h, const float* d_wave, const int16_t* d_wave16, int64_t B,
+                                int64_t L, float* d_framewise, float* d_clipwise, float* d_embedding,
+                                void* d_workspace, size_t workspace_bytes, void* stream) {
   if (!h) return SEDX_EINVAL;
   if (!h->finalized) return fail(h, SEDX_ESTATE, "weights not finalised");
   if (h->cfg.feature_type != SEDX_FEATURE_LOGMEL)
     return fail(h, SEDX_EINVAL, "gamma models take features: use sedx_forward_features");
-  if (!d_wave || !d_framewise || !d_clipwise || B <= 0)
+  if ((!d_wave && !d_wave16) || !d_framewise || !d_clipwise || B <= 0)
     return fail(h, SEDX_EINVAL, "null pointer or empty batch");
   const int n2 = h->cfg.window_size / 2;
   if (L <= n2)
@@ -860,6 +860,7 @@ sedx_status sedx_forward(sedx_handle* h, const float* d_wave, int64_t B, int64_t
   if (st != SEDX_OK) return st;
   FrontendParams p{};
   p.audio = d_wave;
+  p.audio_i16 = d_wave16;
   p.clip_stride = L;
   p.n_clips = (int32_t)B;
   p.n_win = 1;
@@ -880,6 +881,22 @@ sedx_status sedx_forward(sedx_handle* h, const float* d_wave, int64_t B, int64_t
   mark(h, 0, s);
   launch_logmel(p, h->cfg.window_size, s);
   return run_body(h, B, g, ws, l, d_framewise, d_clipwise, d_embedding, s);
+}
+
+sedx_status sedx_forward(sedx_handle* h, const float* d_wave, int64_t B, int64_t L,
+                         float* d_framewise, float* d_clipwise, float* d_embedding,
+                         void* d_workspace, size_t workspace_bytes, void* stream) {
+  if (!d_wave) return fail(h, SEDX_EINVAL, "null waveform pointer");
+  return forward_wave(h, d_wave, nullptr, B, L, d_framewise, d_clipwise, d_embedding, d_workspace,
+                      workspace_bytes, stream);
+}
+
+sedx_status sedx_forward_i16(sedx_handle* h, const int16_t* d_wave, int64_t B, int64_t L,
+                             float* d_framewise, float* d_clipwise, float* d_embedding,
+                             void* d_workspace, size_t workspace_bytes, void* stream) {
+  if (!d_wave) return fail(h, SEDX_EINVAL, "null waveform pointer");
+  return forward_wave(h, nullptr, d_wave, B, L, d_framewise, d_clipwise, d_embedding, d_workspace,
+                      workspace_bytes, stream);
 }
 
 sedx_status sedx_forward_features(sedx_handle* h, const float* d_feat, int64_t B, int64_t T,
@@ -957,25 +974,17 @@ sedx_status sedx_window_geometry(const sedx_handle* h, int64_t L_clip, float sam
 static size_t window_ws_bytes(const sedx_handle* h, int64_t n_clips, const WinGeom& wg) {
   const int64_t items = n_clips * wg.n_win;
   const WsLayout l = ws_layout(h, items, wg.g);
-  const size_t extra = (size_t)items * (wg.Tw * h->cfg.classes_num + h->cfg.classes_num) + 128;
+  // + per-window framewise, clipwise and (vote mode) the f64 binarisation thresholds
+  const size_t extra = (size_t)items * (wg.Tw * h->cfg.classes_num + h->cfg.classes_num) + 2 * h->cfg.classes_num +
+                       256;
   return l.total_bytes + extra * sizeof(float);
 }
 
-sedx_status sedx_window_workspace_size(const sedx_handle* h, int64_t n_clips, int64_t L_clip,
-                                       float sample_duration, float overlap_value,
-                                       int32_t pad_clip, size_t* bytes) {
-  if (!h || !bytes || n_clips <= 0) return SEDX_EINVAL;
-  WinGeom wg;
-  sedx_status st = window_geometry(h, L_clip, sample_duration, overlap_value, pad_clip, &wg);
-  if (st != SEDX_OK) return st;
-  *bytes = window_ws_bytes(h, n_clips, wg);
-  return SEDX_OK;
-}
-
-sedx_status sedx_forward_windows(sedx_handle* h, const float* d_audio, int64_t n_clips,
-                                 int64_t L_clip, float sample_duration, float overlap_value,
-                                 int32_t pad_clip, float* d_merged, void* d_workspace,
-                                 size_t workspace_bytes, void* stream) {
+// one batch of all windows of all clips, then the merge (avg or vote)
+static sedx_status forward_windows_impl(sedx_handle* h, const float* d_audio, int64_t n_clips,
+                                        int64_t L_clip, float sample_duration, float overlap_value,
+                                        int32_t pad_clip, const double* h_vote_thres, float* d_merged,
+                                        void* d_workspace, size_t workspace_bytes, void* stream) {
   if (!h) return SEDX_EINVAL;
   if (!h->finalized) return fail(h, SEDX_ESTATE, "weights not finalised");
   if (h->cfg.feature_type != SEDX_FEATURE_LOGMEL)
@@ -993,8 +1002,11 @@ sedx_status sedx_forward_windows(sedx_handle* h, const float* d_audio, int64_t n
   float* ws = nullptr;
   st = get_ws(h, window_ws_bytes(h, n_clips, wg), d_workspace, workspace_bytes, &ws);
   if (st != SEDX_OK) return st;
+  const int C = h->cfg.classes_num;
   float* fw = ws + l.total_bytes / sizeof(float);
-  float* clip = fw + align_up((size_t)items * wg.Tw * h->cfg.classes_num);
+  float* clip = fw + align_up((size_t)items * wg.Tw * C);
+  double* vthr = reinterpret_cast<double*>(clip + align_up((size_t)items * C));
+  if (h_vote_thres) HIP_TRY(h, hipMemcpyAsync(vthr, h_vote_thres, C * sizeof(double), hipMemcpyHostToDevice, s));
   FrontendParams p{};
   p.audio = d_audio;
   p.clip_stride = L_clip;
@@ -1018,10 +1030,88 @@ sedx_status sedx_forward_windows(sedx_handle* h, const float* d_audio, int64_t n
   launch_logmel(p, h->cfg.window_size, s);
   st = run_body(h, items, wg.g, ws, l, fw, clip, nullptr, s);
   if (st != SEDX_OK) return st;
-  launch_merge(fw, (int)n_clips, wg.n_win, (int)wg.Tw, h->cfg.classes_num, wg.step, (int)wg.N,
-               wg.interval, wg.sd, d_merged, s);
+  launch_merge(fw, (int)n_clips, wg.n_win, (int)wg.Tw, C, wg.step, (int)wg.N, wg.interval, wg.sd,
+               h_vote_thres ? vthr : nullptr, d_merged, s);
   HIP_TRY(h, hipGetLastError());
   return SEDX_OK;
+}
+
+sedx_status sedx_window_workspace_size(const sedx_handle* h, int64_t n_clips, int64_t L_clip,
+                                       float sample_duration, float overlap_value,
+                                       int32_t pad_clip, size_t* bytes) {
+  if (!h || !bytes || n_clips <= 0) return SEDX_EINVAL;
+  WinGeom wg;
+  sedx_status st = window_geometry(h, L_clip, sample_duration, overlap_value, pad_clip, &wg);
+  if (st != SEDX_OK) return st;
+  *bytes = window_ws_bytes(h, n_clips, wg);
+  return SEDX_OK;
+}
+
+sedx_status sedx_forward_windows(sedx_handle* h, const float* d_audio, int64_t n_clips,
+                                 int64_t L_clip, float sample_duration, float overlap_value,
+                                 int32_t pad_clip, float* d_merged, void* d_workspace,
+                                 size_t workspace_bytes, void* stream) {
+  return forward_windows_impl(h, d_audio, n_clips, L_clip, sample_duration, overlap_value, pad_clip,
+                              nullptr, d_merged, d_workspace, workspace_bytes, stream);
+}
+
+sedx_status sedx_forward_windows_vote(sedx_handle* h, const float* d_audio, int64_t n_clips,
+                                      int64_t L_clip, float sample_duration, float overlap_value,
+                                      int32_t pad_clip, const double* bin_thres, float* d_votes,
+                                      void* d_workspace, size_t workspace_bytes, void* stream) {
+  if (!bin_thres) return fail(h, SEDX_EINVAL, "vote mode needs the per-class binarisation thresholds");
+  return forward_windows_impl(h, d_audio, n_clips, L_clip, sample_duration, overlap_value, pad_clip,
+                              bin_thres, d_votes, d_workspace, workspace_bytes, stream);
+}
+
+sedx_status sedx_events_workspace_size(int64_t n_clips, int64_t C, size_t* bytes) {
+  if (!bytes || n_clips < 0 || C <= 0) return SEDX_EINVAL;
+  *bytes = events_workspace_bytes(n_clips * C, C);
+  return SEDX_OK;
+}
+
+sedx_status sedx_events_device(const float* d_x, int64_t n_clips, int64_t T, int64_t C,
+                               const double* high_thres, const double* low_thres,
+                               int32_t use_low_thres, const int64_t* n_smooth, const int64_t* n_salt,
+                               int32_t mode, float overlap_value, int32_t sample_duration,
+                               int32_t* d_events, int64_t capacity, int64_t* d_info,
+                               void* d_workspace, size_t workspace_bytes, void* stream) {
+  if (n_clips < 0 || T < 0 || C <= 0 || !d_info || !n_smooth || !n_salt || (mode != 0 && mode != 1) ||
+      (n_clips > 0 && !d_x) || (capacity > 0 && !d_events) || capacity < 0 ||
+      (use_low_thres && !low_thres) || (mode == 0 && !high_thres))
+    return SEDX_EINVAL;
+  const int64_t step = (int64_t)(100 * (double)overlap_value);
+  if (mode == 1 && (step <= 0 || sample_duration <= 0)) return SEDX_EINVAL;
+  const size_t need = events_workspace_bytes(n_clips * C, C);
+  if (!d_workspace || workspace_bytes < need) return SEDX_EINVAL;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  // per-class parameters -> workspace (f32 high: the mode-0 compare is float32)
+  auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+  char* p = static_cast<char*>(d_workspace);
+  int64_t* counts = reinterpret_cast<int64_t*>(p);
+  p += al(n_clips * C * 8);
+  float* d_hi = reinterpret_cast<float*>(p);
+  p += al(C * 4);
+  double* d_lo = reinterpret_cast<double*>(p);
+  p += al(C * 8);
+  int64_t* d_ns = reinterpret_cast<int64_t*>(p);
+  p += al(C * 8);
+  int64_t* d_nsalt = reinterpret_cast<int64_t*>(p);
+  std::vector<float> hi(C, 0.f);
+  std::vector<double> lo(C, 0.0);
+  for (int64_t k = 0; k < C; ++k) {
+    if (high_thres) hi[k] = (float)high_thres[k];
+    if (use_low_thres) lo[k] = low_thres[k];
+  }
+  if (hipMemcpyAsync(d_hi, hi.data(), C * 4, hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipMemcpyAsync(d_lo, lo.data(), C * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipMemcpyAsync(d_ns, n_smooth, C * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipMemcpyAsync(d_nsalt, n_salt, C * 8, hipMemcpyHostToDevice, s) != hipSuccess)
+    return SEDX_EHIP;
+  EventArgs a{d_x, n_clips, T, C, d_hi, d_lo, d_ns, d_nsalt, use_low_thres,
+              step, (int64_t)sample_duration, counts, d_info, d_events, capacity};
+  launch_events(a, mode, s);
+  return hipGetLastError() == hipSuccess ? SEDX_OK : SEDX_EHIP;
 }
 
 }  // extern "C"

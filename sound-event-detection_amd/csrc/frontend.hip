@@ -84,7 +84,7 @@ __device__ __forceinline__ float2 real_bin(const float2* Z, const float2* tw, in
   return cadd(E, cmul(tw[k], O));
 }
 
-template <int NFFT>
+template <int NFFT, bool I16>
 __global__ __launch_bounds__(256) void logmel_kernel(FrontendParams p) {
   constexpr int N2 = NFFT / 2;
   __shared__ float2 s_tw[NFFT];
@@ -110,7 +110,9 @@ __global__ __launch_bounds__(256) void logmel_kernel(FrontendParams p) {
       const int64_t clip = item / p.n_win;
       const int w = (int)(item - clip * p.n_win);
       const int64_t wstart = p.win_start[w];
-      const float* src = p.audio + clip * p.clip_stride + wstart;
+      const int64_t src_off = clip * p.clip_stride + wstart;
+      const float* src = p.audio + src_off;
+      const int16_t* src16 = p.audio_i16 + src_off;
       const int64_t avail = p.clip_len - wstart;  // samples of this item backed by audio
       const int64_t pos0 = (int64_t)t * p.hop - N2;   // start in un-padded coordinates
       for (int m = lane; m < N2; m += 64) {
@@ -120,7 +122,10 @@ __global__ __launch_bounds__(256) void logmel_kernel(FrontendParams p) {
           int64_t j = pos0 + 2 * m + e;
           if (j < 0) j = -j;                       // reflect (F.pad mode='reflect')
           if (j >= L) j = 2 * (L - 1) - j;
-          v[e] = (j < avail) ? src[j] : 0.0f;      // pad_truncate zeros
+          if (I16)   // int16_to_float32: float64 x / 32767, rounded to float32
+            v[e] = (j < avail) ? (float)((double)src16[j] / 32767.0) : 0.0f;
+          else
+            v[e] = (j < avail) ? src[j] : 0.0f;    // pad_truncate zeros
           v[e] *= p.window[2 * m + e];
         }
         X[m] = make_float2(v[0], v[1]);
@@ -156,10 +161,20 @@ void launch_logmel(const FrontendParams& p, int n_fft, hipStream_t s) {
   int64_t blocks = (total + 3) / 4;
   if (blocks > 8192) blocks = 8192;
   if (blocks < 1) blocks = 1;
+  const bool i16 = p.audio_i16 != nullptr;
   switch (n_fft) {
-    case 256: hipLaunchKernelGGL(logmel_kernel<256>, dim3(blocks), dim3(256), 0, s, p); break;
-    case 512: hipLaunchKernelGGL(logmel_kernel<512>, dim3(blocks), dim3(256), 0, s, p); break;
-    case 1024: hipLaunchKernelGGL(logmel_kernel<1024>, dim3(blocks), dim3(256), 0, s, p); break;
+    case 256:
+      if (i16) hipLaunchKernelGGL((logmel_kernel<256, true>), dim3(blocks), dim3(256), 0, s, p);
+      else hipLaunchKernelGGL((logmel_kernel<256, false>), dim3(blocks), dim3(256), 0, s, p);
+      break;
+    case 512:
+      if (i16) hipLaunchKernelGGL((logmel_kernel<512, true>), dim3(blocks), dim3(256), 0, s, p);
+      else hipLaunchKernelGGL((logmel_kernel<512, false>), dim3(blocks), dim3(256), 0, s, p);
+      break;
+    case 1024:
+      if (i16) hipLaunchKernelGGL((logmel_kernel<1024, true>), dim3(blocks), dim3(256), 0, s, p);
+      else hipLaunchKernelGGL((logmel_kernel<1024, false>), dim3(blocks), dim3(256), 0, s, p);
+      break;
     default: break;
   }
 }

@@ -12,7 +12,8 @@ namespace sedx {
 
 // ---- frontend -------------------------------------------------------------
 struct FrontendParams {
-  const float* audio;       // base pointer
+  const float* audio;       // base pointer (fp32 samples)
+  const int16_t* audio_i16; // or int16 samples, dequantised x / 32767 on load (utilities.py:78-79)
   int64_t clip_stride;      // samples between clips
   int32_t n_clips;          // items = n_clips * n_win
   int32_t n_win;            // windows per clip (1 in clip mode)
@@ -110,7 +111,28 @@ void launch_transpose_btd(const float* E, int B, int T, int D, float* out, hipSt
 // window overlap-add + avg_merge schedule.  fw [n_clips*n_win][Tw][C] ->
 // merged [n_clips][N][C]; step = int(100*overlap) frames, interval =
 // sample_duration*100 - step, sd = sample_duration (utilities.py:425-446).
+// vote_thr != nullptr (device, [C] f64): inference_prob_vote merge instead —
+// every window binarised (x > thr[k], pytorch/main_strong.py:870-883) and
+// summed, no avg_merge division (main_strong.py:1082-1097).
 void launch_merge(const float* fw, int n_clips, int n_win, int Tw, int C, int step, int N,
-                  int interval, int sd, float* merged, hipStream_t s);
+                  int interval, int sd, const double* vote_thr, float* merged, hipStream_t s);
+
+// ---- events (events.hip) --------------------------------------------------
+struct EventArgs {
+  const float* x;            // [N][T][C] framewise probabilities (mode 0) / vote counts (mode 1)
+  int64_t N, T, C;
+  const float* hi;           // [C] high threshold (mode 0)
+  const double* lo;          // [C] low threshold
+  const int64_t* n_smooth;   // [C]
+  const int64_t* n_salt;     // [C]
+  int32_t use_lo;
+  int64_t step, sd;          // mode 1: int(100*overlap), sample_duration
+  int64_t* counts;           // [N*C] scratch
+  int64_t* info;             // [2]: number of events, IndexError flag
+  int32_t* events;           // [capacity][4] (clip, class, bgn, fin)
+  int64_t capacity;
+};
+size_t events_workspace_bytes(int64_t n_series, int64_t C);
+void launch_events(const EventArgs& a, int mode, hipStream_t s);
 
 }  // namespace sedx

@@ -310,6 +310,7 @@ void launch_transpose_btd(const float* E, int B, int T, int D, float* out, hipSt
 __global__ __launch_bounds__(256) void merge_kernel(const float* __restrict__ fw, int n_clips,
                                                     int n_win, int Tw, int C, int step, int N,
                                                     int interval, int sd,
+                                                    const double* __restrict__ vote_thr,
                                                     float* __restrict__ merged) {
   const int64_t total = (int64_t)n_clips * N * C;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total;
@@ -323,9 +324,16 @@ __global__ __launch_bounds__(256) void merge_kernel(const float* __restrict__ fw
     for (int w = 0; w < n_win; ++w) {
       const int lf = f - w * step;
       if (lf < 0 || lf >= Tw) continue;
-      const float v = fw[((c * n_win + w) * Tw + lf) * C + k];
+      float v = fw[((c * n_win + w) * Tw + lf) * C + k];
+      // binarize_pred: float64 0/1 (the comparison of a float32 element with
+      // a float64 threshold is made in float64); sums of 0/1 are exact in f32
+      if (vote_thr) v = ((double)v > vote_thr[k]) ? 1.0f : 0.0f;
       s = first ? v : s + v;
       first = false;
+    }
+    if (vote_thr) {      // inference_prob_vote: no avg_merge (main_strong.py:1097)
+      merged[i] = s;
+      continue;
     }
     // avg_merge: blocks [i, i+step) for i in range(step, N-step, step)
     const int blk = (f / step) * step;
@@ -340,12 +348,12 @@ __global__ __launch_bounds__(256) void merge_kernel(const float* __restrict__ fw
 }
 
 void launch_merge(const float* fw, int n_clips, int n_win, int Tw, int C, int step, int N,
-                  int interval, int sd, float* merged, hipStream_t s) {
+                  int interval, int sd, const double* vote_thr, float* merged, hipStream_t s) {
   const int64_t total = (int64_t)n_clips * N * C;
   int64_t blocks = (total + 255) / 256;
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(merge_kernel, dim3(blocks), dim3(256), 0, s, fw, n_clips, n_win, Tw, C, step,
-                     N, interval, sd, merged);
+                     N, interval, sd, vote_thr, merged);
 }
 
 }  // namespace sedx

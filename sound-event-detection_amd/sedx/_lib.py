@@ -19,7 +19,9 @@ EXPORTS = ['sedx_create', 'sedx_destroy', 'sedx_last_error', 'sedx_version', 'se
            'sedx_finalize_weights', 'sedx_output_geometry', 'sedx_workspace_size',
            'sedx_forward', 'sedx_forward_features', 'sedx_gamma_features',
            'sedx_window_geometry', 'sedx_forward_windows', 'sedx_window_workspace_size',
-           'sedx_events', 'sedx_set_profiling', 'sedx_stage_times', 'sedx_set_precision']
+           'sedx_events', 'sedx_set_profiling', 'sedx_stage_times', 'sedx_set_precision',
+           'sedx_forward_windows_vote', 'sedx_events_workspace_size', 'sedx_events_device',
+           'sedx_forward_i16']
 PRECISION = {'exact': 0, 'x3': 1}
 STAGES = ['frontend', 'b1c1', 'b1c2', 'b2c1', 'b2c2', 'b3c1', 'b3c2', 'b4c1', 'b4c2', 'seq', 'head']
 
@@ -63,11 +65,16 @@ def lib():
         'sedx_workspace_size': ([P, I64, I64, PSZ], I32),
         'sedx_forward': ([P, P, I64, I64, P, P, P, P, SZ, P], I32),
         'sedx_forward_features': ([P, P, I64, I64, P, P, P, P, SZ, P], I32),
+        'sedx_forward_i16': ([P, P, I64, I64, P, P, P, P, SZ, P], I32),
         'sedx_gamma_features': ([P, P, I64, I64, P, PI64, P, SZ, P], I32),
         'sedx_window_geometry': ([P, I64, F32, F32, I32, PI64, PI64, PI64], I32),
         'sedx_forward_windows': ([P, P, I64, I64, F32, F32, I32, P, P, SZ, P], I32),
         'sedx_window_workspace_size': ([P, I64, I64, F32, F32, I32, PSZ], I32),
         'sedx_events': ([P, I64, I64, I64, P, P, I32, P, P, P, I64, PI64], I32),
+        'sedx_forward_windows_vote': ([P, P, I64, I64, F32, F32, I32, P, P, P, SZ, P], I32),
+        'sedx_events_workspace_size': ([I64, I64, PSZ], I32),
+        'sedx_events_device': ([P, I64, I64, I64, P, P, I32, P, P, I32, F32, I32, P, I64, P, P, SZ, P],
+                               I32),
         'sedx_set_profiling': ([P, I32], I32),
         'sedx_set_precision': ([P, I32], I32),
         'sedx_stage_times': ([P, ctypes.POINTER(ctypes.c_float), I32, ctypes.POINTER(I32)], I32),

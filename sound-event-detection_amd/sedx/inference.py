@@ -6,9 +6,18 @@ extraction.  All compute goes through libsedx.
                      pytorch/main_strong.py:790-833 (pad_clip=True): every
                      window of every clip in ONE native batch, GPU overlap-add
                      + avg_merge divisor schedule (utils/utilities.py:405-446).
+ - predict_windows_vote   inference_prob_vote (pytorch/main_strong.py:1058-1097):
+                     binarised windows overlap-added on the GPU.
  - events_from_framewise   frame_prediction_to_event_prediction_v2
                      (pytorch/predict.py:57-121; utils/utilities.py:155-214)
-                     over native activity_detection (utils/vad.py).
+                     over native activity_detection (utils/vad.py): on the
+                     GPU for HIP tensors (events.hip), host C++ otherwise.
+ - events_from_votes frame_binary_prediction_to_event_prediction
+                     (utils/utilities.py:216-276, vad.activity_detection_binary)
+                     on the GPU.
+ - sweep_overlap     the [overlap, duration] sweeps of inference_prob_overlap /
+                     inference_prob_vote (main_strong.py:746, :1011);
+                     write_submission (utils/utilities.py:278-291).
  - gamma_features    utils/gammatone/fftweight.py:126-168 + utils/features.py:361-370
                      + utils/utilities.py:73-79, on the GPU.
  - inference_prob    pytorch/pytorch_utils.py:25-78 loop (batches of clips).
@@ -46,13 +55,11 @@ def window_geometry(model, clip_samples, sample_duration=5, overlap_value=1, pad
     return nw.value, ws.value, nf.value
 
 
-def predict_windows(model, audio, sample_duration=5, overlap_value=1, pad_clip=False):
-    """audio: [n_clips, L] (HIP tensor, every clip L samples long).  Returns the
-    merged + averaged framewise predictions [n_clips, N, classes]."""
+def _windows(model, audio, sample_duration, overlap_value, pad_clip, vote_thres):
     if model.training:
         raise RuntimeError('call model.eval() first')
     if audio.device.type != 'cuda':
-        raise RuntimeError('predict_windows needs a HIP tensor (no CPU fallback)')
+        raise RuntimeError('windowed inference needs a HIP tensor (no CPU fallback)')
     x = audio.to(torch.float32).contiguous()
     if x.dim() == 1:
         x = x[None]
@@ -70,10 +77,31 @@ def predict_windows(model, audio, sample_duration=5, overlap_value=1, pad_clip=F
     ws = torch.empty(wsz.value, dtype=torch.uint8, device=x.device)
     merged = torch.empty((n_clips, nf.value, model.classes_num), dtype=torch.float32, device=x.device)
     stream = ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
-    _lib.check(L.sedx_forward_windows(nat.h, _ptr(x), n_clips, clip_len, float(sample_duration),
-                                      float(overlap_value), int(bool(pad_clip)), _ptr(merged),
-                                      _ptr(ws), wsz.value, stream), nat.h, 'forward_windows')
+    if vote_thres is None:
+        _lib.check(L.sedx_forward_windows(nat.h, _ptr(x), n_clips, clip_len, float(sample_duration),
+                                          float(overlap_value), int(bool(pad_clip)), _ptr(merged),
+                                          _ptr(ws), wsz.value, stream), nat.h, 'forward_windows')
+    else:
+        thr = np.ascontiguousarray(_as_list(vote_thres, model.classes_num), dtype=np.float64)
+        _lib.check(L.sedx_forward_windows_vote(nat.h, _ptr(x), n_clips, clip_len, float(sample_duration),
+                                               float(overlap_value), int(bool(pad_clip)),
+                                               thr.ctypes.data_as(ctypes.c_void_p), _ptr(merged),
+                                               _ptr(ws), wsz.value, stream), nat.h, 'forward_windows_vote')
     return merged
+
+
+def predict_windows(model, audio, sample_duration=5, overlap_value=1, pad_clip=False):
+    """audio: [n_clips, L] (HIP tensor, every clip L samples long).  Returns the
+    merged + averaged framewise predictions [n_clips, N, classes]."""
+    return _windows(model, audio, sample_duration, overlap_value, pad_clip, None)
+
+
+def predict_windows_vote(model, audio, sample_duration, overlap_value, bin_threshold, pad_clip=True):
+    """inference_prob_vote window loop (pytorch/main_strong.py:1058-1097): every
+    window binarised with ``bin_threshold`` (the reference passes
+    sed_low_threshold, :1082) and overlap-added without averaging.  Returns
+    the vote counts [n_clips, N, classes] (float32, exact integers)."""
+    return _windows(model, audio, sample_duration, overlap_value, pad_clip, bin_threshold)
 
 
 def gamma_features(model, audio):
@@ -102,18 +130,64 @@ def _as_list(v, C):
     return [v] * C
 
 
-def event_pairs(framewise, params):
-    """Native activity_detection over every (clip, class).  framewise [N, T, C]
-    (numpy or tensor).  Returns int32 array [n_events, 4] = (clip, class, bgn, fin)."""
-    fw = framewise.detach().cpu().numpy() if isinstance(framewise, torch.Tensor) else np.asarray(framewise)
-    fw = np.ascontiguousarray(fw, dtype=np.float32)
-    N, T, C = fw.shape
-    hi = np.ascontiguousarray(_as_list(params['sed_high_threshold'], C), dtype=np.float64)
+def _event_params(params, C):
+    hi_v = params.get('sed_high_threshold', None)
+    hi = np.ascontiguousarray(_as_list(hi_v if hi_v is not None else 0.0, C), dtype=np.float64)
     lo_v = params.get('sed_low_threshold', None)
     use_lo = lo_v is not None
     lo = np.ascontiguousarray(_as_list(lo_v if use_lo else 0.0, C), dtype=np.float64)
     ns = np.ascontiguousarray(_as_list(params['n_smooth'], C), dtype=np.int64)
     nsalt = np.ascontiguousarray(_as_list(params['n_salt'], C), dtype=np.int64)
+    return hi, lo, use_lo, ns, nsalt
+
+
+def event_pairs_device(x, params, mode=0, overlap_value=1, sample_duration=5):
+    """Thresholding on the GPU (sedx_events_device): x [N, T, C] HIP tensor of
+    framewise probabilities (mode 0, activity_detection) or window vote counts
+    (mode 1, activity_detection_binary).  Returns int32 [n_events, 4] =
+    (clip, class, bgn, fin) in the reference's (clip, class, time) order."""
+    if x.device.type != 'cuda':
+        raise RuntimeError('event_pairs_device needs a HIP tensor')
+    x = x.to(torch.float32).contiguous()
+    N, T, C = x.shape
+    hi, lo, use_lo, ns, nsalt = _event_params(params, C)
+    L = _lib.lib()
+    wsz = ctypes.c_size_t()
+    _lib.check(L.sedx_events_workspace_size(N, C, ctypes.byref(wsz)), None, 'events_workspace_size')
+    dev = x.device
+    ws = torch.empty(max(wsz.value, 1), dtype=torch.uint8, device=dev)
+    info = torch.zeros(2, dtype=torch.int64, device=dev)
+    stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    cap = max(64, N * C * 4)
+    with torch.cuda.device(dev):
+        while True:
+            ev = torch.empty((cap, 4), dtype=torch.int32, device=dev)
+            st = L.sedx_events_device(_ptr(x), N, T, C, hi.ctypes.data_as(ctypes.c_void_p),
+                                      lo.ctypes.data_as(ctypes.c_void_p), int(use_lo),
+                                      ns.ctypes.data_as(ctypes.c_void_p),
+                                      nsalt.ctypes.data_as(ctypes.c_void_p), int(mode),
+                                      float(overlap_value), int(sample_duration), _ptr(ev), cap,
+                                      _ptr(info), _ptr(ws), wsz.value, stream)
+            _lib.check(st, None, 'events_device')
+            n, bad = (int(v) for v in info.cpu().tolist())
+            if bad:
+                raise RuntimeError('sedx_events_device: a run begins at the last frame after the '
+                                   'find_bgn_fin_pairs quirk (the reference raises IndexError there)')
+            if n <= cap:
+                return ev[:n].cpu().numpy()
+            cap = n
+
+
+def event_pairs(framewise, params):
+    """activity_detection over every (clip, class): on the GPU for a HIP tensor
+    (sedx_events_device), else the host C++ path (sedx_events).  framewise
+    [N, T, C].  Returns int32 array [n_events, 4] = (clip, class, bgn, fin)."""
+    if isinstance(framewise, torch.Tensor) and framewise.device.type == 'cuda':
+        return event_pairs_device(framewise, params, mode=0)
+    fw = framewise.detach().cpu().numpy() if isinstance(framewise, torch.Tensor) else np.asarray(framewise)
+    fw = np.ascontiguousarray(fw, dtype=np.float32)
+    N, T, C = fw.shape
+    hi, lo, use_lo, ns, nsalt = _event_params(params, C)
     L = _lib.lib()
     n = ctypes.c_int64()
     cap = max(16, N * C * 4)
@@ -133,12 +207,7 @@ def event_pairs(framewise, params):
                            'find_bgn_fin_pairs quirk (the reference raises IndexError there)')
 
 
-def events_from_framewise(framewise, params, audio_name='test', frames_per_second=FRAMES_PER_SECOND,
-                          labels=LABELS, sort=True):
-    """List of {'filename','onset','offset','event_label'} exactly like
-    frame_prediction_to_event_prediction_v2 (+ the stable onset sort of
-    predict.py:353)."""
-    pairs = event_pairs(framewise, params)
+def _to_events(pairs, audio_name, frames_per_second, labels, sort):
     names = audio_name if isinstance(audio_name, (list, tuple)) else None
     out = []
     for clip, k, b, f in pairs.tolist():
@@ -147,6 +216,50 @@ def events_from_framewise(framewise, params, audio_name='test', frames_per_secon
                     'event_label': labels[k]})
     if sort:
         out = sorted(out, key=lambda e: e['onset'])
+    return out
+
+
+def events_from_framewise(framewise, params, audio_name='test', frames_per_second=FRAMES_PER_SECOND,
+                          labels=LABELS, sort=True):
+    """List of {'filename','onset','offset','event_label'} exactly like
+    frame_prediction_to_event_prediction_v2 (+ the stable onset sort of
+    predict.py:353; main_strong.py:834 does not sort: sort=False)."""
+    return _to_events(event_pairs(framewise, params), audio_name, frames_per_second, labels, sort)
+
+
+def events_from_votes(votes, overlap_value, sample_duration, params, audio_name='test',
+                      frames_per_second=FRAMES_PER_SECOND, labels=LABELS):
+    """frame_binary_prediction_to_event_prediction (utils/utilities.py:216-276)
+    on vote counts from predict_windows_vote, on the GPU."""
+    pairs = event_pairs_device(votes, params, mode=1, overlap_value=overlap_value,
+                               sample_duration=sample_duration)
+    return _to_events(pairs, audio_name, frames_per_second, labels, False)
+
+
+def write_submission(event_list, submission_path):
+    """utils/utilities.py:278-291: one tab-separated line per event."""
+    with open(submission_path, 'w') as f:
+        for e in event_list:
+            f.write('{}\t{}\t{}\t{}\n'.format(e['filename'], e['onset'], e['offset'], e['event_label']))
+
+
+OVERLAP_SWEEP = [[0.5, 6], [0.5, 7], [1, 5], [1, 6], [1, 7]]   # main_strong.py:746, :1011
+
+
+def sweep_overlap(model, audio, audio_names, params, combos=OVERLAP_SWEEP, vote=False):
+    """inference_prob_overlap / inference_prob_vote parameter sweep
+    (pytorch/main_strong.py:762-835, :1028-1100): for every [overlap_value,
+    sample_duration] the clips (padded to 10 s) run as one windowed batch, then
+    events on the GPU.  audio [n_clips, L] HIP tensor.  Returns
+    {(overlap_value, sample_duration): event list} in the reference's order."""
+    out = {}
+    for ov, sd in combos:
+        if vote:
+            votes = predict_windows_vote(model, audio, sd, ov, params['sed_low_threshold'], pad_clip=True)
+            out[(ov, sd)] = events_from_votes(votes, ov, sd, params, list(audio_names))
+        else:
+            merged = predict_windows(model, audio, sd, ov, pad_clip=True)
+            out[(ov, sd)] = events_from_framewise(merged, params, list(audio_names), sort=False)
     return out
 
 

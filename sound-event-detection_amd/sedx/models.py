@@ -287,11 +287,14 @@ class _SedModel(nn.Module):
 
     def forward(self, input, mixup_lambda=None, timeshift=False, spec_augment=True):
         """Input: (batch_size, data_length) waveform [logmel] or
-        (batch_size, 64, frames) features [gamma].  Eval mode only."""
+        (batch_size, 64, frames) features [gamma].  Eval mode only.  An int16
+        waveform (the reference's HDF5 packing) is dequantised x / 32767 inside
+        the frontend (int16_to_float32, utils/utilities.py:78-79)."""
         self._check_eval(mixup_lambda, timeshift)
         if not isinstance(input, torch.Tensor) or input.device.type != 'cuda':
             raise RuntimeError('sedx forward needs a tensor on a HIP device (no CPU fallback)')
-        x = input.to(torch.float32).contiguous()
+        i16 = input.dtype == torch.int16 and self.feature_type != 'gamma'
+        x = input.contiguous() if i16 else input.to(torch.float32).contiguous()
         nat = self.native(x.device)
         L = _lib.lib()
         if self.feature_type == 'gamma':
@@ -315,7 +318,8 @@ class _SedModel(nn.Module):
         _lib.check(L.sedx_workspace_size(nat.h, B, length, ctypes.byref(wsz)), nat.h, 'workspace_size')
         ws = torch.empty(wsz.value, dtype=torch.uint8, device=dev)
         stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
-        fn = L.sedx_forward_features if self.feature_type == 'gamma' else L.sedx_forward
+        fn = L.sedx_forward_features if self.feature_type == 'gamma' else (
+            L.sedx_forward_i16 if i16 else L.sedx_forward)
         _lib.check(fn(nat.h, _ptr(x), B, length, _ptr(fw), _ptr(clip), _ptr(emb), _ptr(ws),
                       wsz.value, stream), nat.h, 'forward')
         return {'framewise_output': fw, 'clipwise_output': clip, 'embedding': emb}

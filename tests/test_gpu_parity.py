@@ -216,3 +216,19 @@ def test_errors_are_loud():
     m.train()
     with pytest.raises(RuntimeError):
         m(torch.zeros(1, 16000, device='cuda'))        # training mode out of scope
+
+
+@pytest.mark.parametrize('mt', [GRU, TRF])
+def test_int16_waveform_input(mt):
+    """HDF5 int16 batches (utils/data_generator.py:39): the fused dequantise is
+    bit-identical to feeding int16_to_float32(x) (utils/utilities.py:78-79)."""
+    m = build(mt)
+    q = (synth.make_waveforms(3, seconds=4.0, sample_rate=16000, seed=17) * 32767).astype(np.int16)
+    q[0, :5] = [32767, -32768, 0, 1, -1]
+    deq = O.int16_to_float32(q)
+    assert deq.dtype == np.float32
+    a = run(m, deq)
+    with torch.no_grad():
+        b = m(torch.from_numpy(q).cuda())
+    for k in ('framewise_output', 'clipwise_output', 'embedding'):
+        assert np.array_equal(a[k], b[k].cpu().numpy()), k

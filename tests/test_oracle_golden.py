@@ -116,3 +116,33 @@ def test_gamma(golden_dir):
     out = O.forward(_sd(GRU, '32k'), GRU, features=feats)
     for k in ('framewise_output', 'clipwise_output', 'embedding'):
         _close(out[k], g[k], 1e-5, k)
+
+
+def _vote_params(ev, which):
+    return ev['params_' + which]
+
+
+@pytest.mark.parametrize('mt', [GRU, TRF])
+def test_vote_and_overlap_sweep(golden_dir, mt):
+    """inference_prob_vote (binarize_pred + merge + activity_detection_binary)
+    and the inference_prob_overlap merge, oracle vs reference fixtures."""
+    g = np.load(os.path.join(golden_dir, 'vote_%s.npz' % mt))
+    ev = json.load(open(os.path.join(golden_dir, 'vote_events.json')))
+    for ov, sd in ev['settings'][mt]:
+        tag = '%s_%s' % (ov, sd)
+        wins = [g['windows_' + tag][i:i + 1] for i in range(g['windows_' + tag].shape[0])]
+        merged = wins[0]
+        for s in range(2, len(wins) + 1):
+            merged = O.merge(merged if s > 2 else wins[0], wins[s - 1], sd, s, ov)
+        np.testing.assert_array_equal(O.avg_merge(merged.copy(), sd, ov), g['avg_' + tag])
+        got = O.events_from_framewise(g['avg_' + tag], ev['params_default'], 'clip', sort=False)
+        assert got == ev[mt]['overlap_' + tag]
+        for which in ('default', 'synthetic', 'mid'):
+            p = _vote_params(ev, which)
+            votes = None
+            for s, w in enumerate(wins, start=1):
+                b = O.binarize_pred(w, p['sed_low_threshold'])
+                votes = b if s == 1 else O.merge(votes, b, sd, s, ov)
+            np.testing.assert_array_equal(votes, g['votes_%s_%s' % (which, tag)])
+            got = O.events_from_votes(votes, ov, sd, p, 'clip')
+            assert got == ev[mt]['vote_%s_%s' % (which, tag)], (tag, which)
