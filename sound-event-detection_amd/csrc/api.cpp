@@ -1064,9 +1064,9 @@ sedx_status sedx_forward_windows_vote(sedx_handle* h, const float* d_audio, int6
                               bin_thres, d_votes, d_workspace, workspace_bytes, stream);
 }
 
-sedx_status sedx_events_workspace_size(int64_t n_clips, int64_t C, size_t* bytes) {
-  if (!bytes || n_clips < 0 || C <= 0) return SEDX_EINVAL;
-  *bytes = events_workspace_bytes(n_clips * C, C);
+sedx_status sedx_events_workspace_size(int64_t n_clips, int64_t T, int64_t C, size_t* bytes) {
+  if (!bytes || n_clips < 0 || T < 0 || C <= 0) return SEDX_EINVAL;
+  *bytes = events_workspace_bytes(n_clips * C, T, C);
   return SEDX_OK;
 }
 
@@ -1082,34 +1082,34 @@ sedx_status sedx_events_device(const float* d_x, int64_t n_clips, int64_t T, int
     return SEDX_EINVAL;
   const int64_t step = (int64_t)(100 * (double)overlap_value);
   if (mode == 1 && (step <= 0 || sample_duration <= 0)) return SEDX_EINVAL;
-  const size_t need = events_workspace_bytes(n_clips * C, C);
+  if (C > 256) return SEDX_EINVAL;   // one workgroup of 256 threads per clip
+  const size_t need = events_workspace_bytes(n_clips * C, T, C);
   if (!d_workspace || workspace_bytes < need) return SEDX_EINVAL;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  // per-class parameters -> workspace (f32 high: the mode-0 compare is float32)
+  // per-class parameters -> one packed block in the workspace, one copy
+  // (f32 high: the mode-0 compare is float32)
   auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
   char* p = static_cast<char*>(d_workspace);
   int64_t* counts = reinterpret_cast<int64_t*>(p);
   p += al(n_clips * C * 8);
-  float* d_hi = reinterpret_cast<float*>(p);
-  p += al(C * 4);
-  double* d_lo = reinterpret_cast<double*>(p);
-  p += al(C * 8);
-  int64_t* d_ns = reinterpret_cast<int64_t*>(p);
-  p += al(C * 8);
-  int64_t* d_nsalt = reinterpret_cast<int64_t*>(p);
-  std::vector<float> hi(C, 0.f);
-  std::vector<double> lo(C, 0.0);
+  int64_t* slots = reinterpret_cast<int64_t*>(p);
+  p += al(n_clips * C * events_slot_cap(T) * 8);
+  const size_t o_hi = 0, o_lo = al(C * 4), o_ns = o_lo + al(C * 8), o_salt = o_ns + al(C * 8);
+  std::vector<char> blob(o_salt + C * 8, 0);
   for (int64_t k = 0; k < C; ++k) {
-    if (high_thres) hi[k] = (float)high_thres[k];
-    if (use_low_thres) lo[k] = low_thres[k];
+    reinterpret_cast<float*>(blob.data() + o_hi)[k] = high_thres ? (float)high_thres[k] : 0.f;
+    reinterpret_cast<double*>(blob.data() + o_lo)[k] = use_low_thres ? low_thres[k] : 0.0;
+    reinterpret_cast<int64_t*>(blob.data() + o_ns)[k] = n_smooth[k];
+    reinterpret_cast<int64_t*>(blob.data() + o_salt)[k] = n_salt[k];
   }
-  if (hipMemcpyAsync(d_hi, hi.data(), C * 4, hipMemcpyHostToDevice, s) != hipSuccess ||
-      hipMemcpyAsync(d_lo, lo.data(), C * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
-      hipMemcpyAsync(d_ns, n_smooth, C * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
-      hipMemcpyAsync(d_nsalt, n_salt, C * 8, hipMemcpyHostToDevice, s) != hipSuccess)
-    return SEDX_EHIP;
+  if (hipMemcpyAsync(p, blob.data(), blob.size(), hipMemcpyHostToDevice, s) != hipSuccess) return SEDX_EHIP;
+  const float* d_hi = reinterpret_cast<const float*>(p + o_hi);
+  const double* d_lo = reinterpret_cast<const double*>(p + o_lo);
+  const int64_t* d_ns = reinterpret_cast<const int64_t*>(p + o_ns);
+  const int64_t* d_nsalt = reinterpret_cast<const int64_t*>(p + o_salt);
   EventArgs a{d_x, n_clips, T, C, d_hi, d_lo, d_ns, d_nsalt, use_low_thres,
-              step, (int64_t)sample_duration, counts, d_info, d_events, capacity};
+              step, (int64_t)sample_duration, counts, slots, events_slot_cap(T), d_info, d_events,
+              capacity};
   launch_events(a, mode, s);
   return hipGetLastError() == hipSuccess ? SEDX_OK : SEDX_EHIP;
 }

@@ -128,11 +128,14 @@ struct EventArgs {
   int32_t use_lo;
   int64_t step, sd;          // mode 1: int(100*overlap), sample_duration
   int64_t* counts;           // [N*C] scratch
+  int64_t* slots;            // [N*C][slot_cap] (bgn, fin) int32 pairs, scratch
+  int64_t slot_cap;          // events_slot_cap(T)
   int64_t* info;             // [2]: number of events, IndexError flag
   int32_t* events;           // [capacity][4] (clip, class, bgn, fin)
   int64_t capacity;
 };
-size_t events_workspace_bytes(int64_t n_series, int64_t C);
+int64_t events_slot_cap(int64_t T);
+size_t events_workspace_bytes(int64_t n_series, int64_t T, int64_t C);
 void launch_events(const EventArgs& a, int mode, hipStream_t s);
 
 }  // namespace sedx

@@ -72,7 +72,7 @@ def lib():
         'sedx_window_workspace_size': ([P, I64, I64, F32, F32, I32, PSZ], I32),
         'sedx_events': ([P, I64, I64, I64, P, P, I32, P, P, P, I64, PI64], I32),
         'sedx_forward_windows_vote': ([P, P, I64, I64, F32, F32, I32, P, P, P, SZ, P], I32),
-        'sedx_events_workspace_size': ([I64, I64, PSZ], I32),
+        'sedx_events_workspace_size': ([I64, I64, I64, PSZ], I32),
         'sedx_events_device': ([P, I64, I64, I64, P, P, I32, P, P, I32, F32, I32, P, I64, P, P, SZ, P],
                                I32),
         'sedx_set_profiling': ([P, I32], I32),

@@ -153,7 +153,7 @@ def event_pairs_device(x, params, mode=0, overlap_value=1, sample_duration=5):
     hi, lo, use_lo, ns, nsalt = _event_params(params, C)
     L = _lib.lib()
     wsz = ctypes.c_size_t()
-    _lib.check(L.sedx_events_workspace_size(N, C, ctypes.byref(wsz)), None, 'events_workspace_size')
+    _lib.check(L.sedx_events_workspace_size(N, T, C, ctypes.byref(wsz)), None, 'events_workspace_size')
     dev = x.device
     ws = torch.empty(max(wsz.value, 1), dtype=torch.uint8, device=dev)
     info = torch.zeros(2, dtype=torch.int64, device=dev)
