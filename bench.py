@@ -143,7 +143,7 @@ def stage_times(model, wave, dev, reps):
 # command (tools/profile_round.sh -> tools/pmc_summary.py; FETCH_SIZE x2 per
 # the gfx950 correction + WRITE_SIZE), committed under profiles/.
 PROFILE_SUMMARY = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles',
-                               'r01c_kernel_summary.json')
+                               'r01d_kernel_summary.json')
 STAGE_KERNEL = {'b1c2': '<64, 64, 1', 'b2c1': '<32, 128, 0', 'b2c2': '<32, 128, 1',
                 'b3c1': '<16, 128, 0', 'b3c2': '<16, 128, 1', 'b4c1': '<8, 128, 0',
                 'b4c2': '<8, 128, 2'}
@@ -235,6 +235,9 @@ def main():
     ap.add_argument('--precision', choices=list(PEAK_TF), default='x3')
     ap.add_argument('--no-exact', action='store_true', help='skip timing the exact fp32 mode')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-side', action='store_true',
+                    help='skip the side measurements (events, window mode): profiling passes use it so '
+                         'that per-kernel rocprof averages cover only the headline launches')
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
     args = ap.parse_args()
 
@@ -263,7 +266,7 @@ def main():
         model.set_precision(args.precision)
 
     extra = {}
-    if args.mode == 'clip' and rank == 0:
+    if args.mode == 'clip' and rank == 0 and not args.no_side:
         extra = side_measurements(model, wave, args, dev, stage_ms)
 
     cpu = None

@@ -18,7 +18,8 @@ from collections import defaultdict
 
 
 def short(name):
-    return name.split('(')[0].replace('void ', '').strip()
+    name = name.replace('(anonymous namespace)::', '').replace('void ', '')
+    return name.split('(')[0].strip()
 
 
 def main(src, tag):
