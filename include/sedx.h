@@ -207,7 +207,8 @@ sedx_status sedx_events(const float* h_framewise, int64_t n_clips, int64_t T, in
  *             time) order; events past capacity are dropped
  *   d_info    int64 [2]: total number of events (may exceed capacity), and 1
  *             where the reference raises IndexError (see sedx_events)
- *   d_workspace >= sedx_events_workspace_size(n_clips, T, C) bytes; C <= 256. */
+ *   d_workspace >= sedx_events_workspace_size(n_clips, T, C) bytes;
+ *             T <= 655,360 frames (a series' bitmaps are held in LDS). */
 sedx_status sedx_events_workspace_size(int64_t n_clips, int64_t T, int64_t C, size_t* bytes);
 sedx_status sedx_events_device(const float* d_x, int64_t n_clips, int64_t T, int64_t C,
                                const double* high_thres, const double* low_thres,

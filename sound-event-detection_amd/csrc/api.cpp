@@ -1082,7 +1082,7 @@ sedx_status sedx_events_device(const float* d_x, int64_t n_clips, int64_t T, int
     return SEDX_EINVAL;
   const int64_t step = (int64_t)(100 * (double)overlap_value);
   if (mode == 1 && (step <= 0 || sample_duration <= 0)) return SEDX_EINVAL;
-  if (C > 256) return SEDX_EINVAL;   // one workgroup of 256 threads per clip
+  if (T > events_max_frames()) return SEDX_EINVAL;   // a series' two bitmaps live in LDS
   const size_t need = events_workspace_bytes(n_clips * C, T, C);
   if (!d_workspace || workspace_bytes < need) return SEDX_EINVAL;
   hipStream_t s = static_cast<hipStream_t>(stream);

@@ -28,9 +28,16 @@
 //     x >= num_overlaps(i), the avg_merge schedule (vad.py:62-85).
 // Output order = (clip, class, time), the reference's event_list order:
 // per-series slots, then one exclusive scan + copy (2 launches).
-// Memory: each clip's [T][C] block is read once, coalesced, into LDS; the
-// per-frame work of a series is then LDS-latency bound (800 series x 1000
-// frames at B=32).
+//
+// One wavefront per series.  Pass 1 turns the series into two bitmaps, 64
+// frames per ballot: on(t) (the locts test) and below(t) (x < low, the stop
+// test of the second-threshold walks), kept in LDS.  Pass 2 is wave-uniform
+// scalar code over runs of the on-bitmap (ctz over words) — the cost scales
+// with the number of runs, not frames — and the walks are bit scans over the
+// below-bitmap.  The streaming state machine of the reference's list stages
+// is unchanged.
+#include <algorithm>
+
 #include "sedx_internal.h"
 
 namespace sedx {
@@ -83,142 +90,154 @@ __device__ __forceinline__ void push1(SeriesState& st, int64_t b, int64_t f, int
   st.s1_pre = f;
 }
 
-template <int MODE, typename XF, typename Emit>
-__device__ __forceinline__ void push_pair(SeriesState& st, XF& X, int64_t T, int64_t b, int64_t f,
-                                          double lo, bool use_lo, int64_t n_smooth, int64_t n_salt,
-                                          Emit& emit) {
+constexpr int EV_WAVES = 4;                 // wavefronts per workgroup (at most)
+constexpr int64_t EV_LDS_BYTES = 160 * 1024;
+constexpr int64_t EV_MAX_WORDS = EV_LDS_BYTES / 16;   // bitmap words per series (T <= 655,360)
+
+__device__ __forceinline__ uint64_t ev_uniform(uint64_t v) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// below-bitmap scans: last set bit <= b (or -1), first set bit >= f (or T)
+struct BelowMask {
+  const uint64_t* m;
+  int64_t W, T;
+  __device__ int64_t prev_set(int64_t b) const {
+    int64_t w = b >> 6;
+    uint64_t bits = ev_uniform(m[w]) & (~0ull >> (63 - (b & 63)));
+    while (true) {
+      if (bits) return w * 64 + 63 - __builtin_clzll(bits);
+      if (--w < 0) return -1;
+      bits = ev_uniform(m[w]);
+    }
+  }
+  __device__ int64_t next_set(int64_t f) const {
+    int64_t w = f >> 6;
+    if (w >= W) return T;
+    uint64_t bits = ev_uniform(m[w]) & (~0ull << (f & 63));
+    while (true) {
+      if (bits) return w * 64 + __builtin_ctzll(bits);
+      if (++w >= W) return T;
+      bits = ev_uniform(m[w]);
+    }
+  }
+};
+
+template <typename Emit>
+__device__ __forceinline__ void push_pair_m(SeriesState& st, const BelowMask& bm, int64_t T, int64_t b,
+                                            int64_t f, bool use_lo, int64_t n_smooth, int64_t n_salt,
+                                            Emit& emit) {
   if (!use_lo) {
     push2(st, b, f, n_smooth, n_salt, emit);
     return;
   }
-  const float lo_f = (float)lo;
-  auto below = [&](int64_t i) { return MODE == 0 ? (X(i) < lo_f) : ((double)X(i) < lo); };
-  // activity_detection_with_second_thres vad.py:139-151
-  while (b != -1) {
-    if (b < 0 || b >= T) {                         // the reference's IndexError
-      st.ok = false;
-      return;
-    }
-    if (below(b)) break;
-    --b;
+  // activity_detection_with_second_thres vad.py:139-151: walk left from b
+  // while x >= low (x[b] read first: b == T is the reference's IndexError),
+  // right from f until x < low or T
+  if (b >= T || f > T) {
+    st.ok = false;
+    return;
   }
-  while (f != T) {
-    if (f < 0 || f > T) {
-      st.ok = false;
-      return;
-    }
-    if (below(f)) break;
-    ++f;
-  }
+  b = bm.prev_set(b);
+  if (f < T) f = bm.next_set(f);
   push1(st, b + 1, f, n_smooth, n_salt, emit);
 }
 
-// frames [c0, c1) of the series (find_bgn_fin_pairs over locts, streamed: a
-// completed run is held until the next one shows it was not the last)
-template <int MODE, typename XF, typename Emit>
-__device__ void series_frames(SeriesState& st, XF& X, int64_t T, int64_t c0, int64_t c1, float hi,
-                              double lo, bool use_lo, int64_t n_smooth, int64_t n_salt, int64_t step,
-                              int64_t sd, Emit& emit) {
-  // mode 1: scan limit and per-block vote requirement (vad.py:62-78)
-  const int64_t interval = sd * 100 - step;
-  int64_t lim = T;
-  if (MODE == 1) lim = (T - step > 0) ? ((T - step + step - 1) / step) * step : 0;
-  const int64_t e = c1 < lim ? c1 : lim;
-  for (int64_t t = c0; t < e && st.ok; ++t) {
-    bool on;
-    if (MODE == 0) {
-      on = X(t) > hi;
-    } else {
-      const int64_t i = (t / step) * step;
-      int64_t nov;
-      if (i < interval) nov = i / step + 1;
-      else if (i >= T - interval) nov = (T - i) / step + 1;
-      else nov = sd;
-      on = (double)X(t) >= (double)nov;
-    }
-    if (on) {
-      if (!st.in_run) {
-        st.in_run = true;
-        st.rs = t;
-      }
-      st.re = t;
-    } else if (st.in_run) {
-      st.in_run = false;
-      if (st.pending) push_pair<MODE>(st, X, T, st.pb, st.pe + 1, lo, use_lo, n_smooth, n_salt, emit);
-      st.pb = st.first ? st.rs : st.rs + 1;       // non-first run: bgn = first + 1
-      st.pe = st.re;
-      st.pending = true;
-      st.first = false;
-    }
-  }
-}
-
-template <int MODE, typename XF, typename Emit>
-__device__ void series_finish(SeriesState& st, XF& X, int64_t T, double lo, bool use_lo,
-                              int64_t n_smooth, int64_t n_salt, Emit& emit) {
-  if (!st.ok) return;
-  if (st.in_run) {
-    if (st.pending) push_pair<MODE>(st, X, T, st.pb, st.pe + 1, lo, use_lo, n_smooth, n_salt, emit);
-    if (!st.ok) return;
-    st.pb = st.first ? st.rs : st.rs + 1;
-    st.pe = st.re;
-    st.pending = true;
-  }
-  if (st.pending) push_pair<MODE>(st, X, T, st.pb, st.pe, lo, use_lo, n_smooth, n_salt, emit);  // last: fin = locts[-1]
-  if (!st.ok) return;
-  if (use_lo && st.s1_any) push2(st, st.s1_mem, st.s1_pre, n_smooth, n_salt, emit);
-  if (st.s2_any) final_out(st.s2_mem, st.s2_pre, n_salt, emit);
-}
-
-// One workgroup per clip: the clip's [T][C] block is staged through LDS in
-// chunks of TC frames (one coalesced contiguous copy per chunk; C <= 256), and
-// thread k < C runs series (clip, k) over the chunk from LDS.  The streaming
-// state machine carries across chunks; the second-threshold walks read LDS
-// inside the chunk and global memory (L2-resident) outside it.  Events go to
-// per-series slots (a series has at most T/2 + 2 events: consecutive events
-// are separated by at least one frame), compacted by events_compact_kernel.
-constexpr int EV_LDS_FLOATS = 16384;   // 64 KB chunk
-
+// dynamic LDS: [wpb][2][W] words (on, below); wpb series per workgroup
 template <int MODE>
-__global__ __launch_bounds__(256) void events_clip_kernel(EventArgs a) {
-  __shared__ float s_x[EV_LDS_FLOATS];
-  const int64_t n = blockIdx.x;
-  const int k = threadIdx.x;
+__global__ __launch_bounds__(64 * EV_WAVES) void events_series_kernel(EventArgs a, int64_t W, int wpb) {
+  extern __shared__ uint64_t ev_lds[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t C = a.C, T = a.T;
-  const int64_t TC = EV_LDS_FLOATS / C;
-  const float* xg = a.x + n * T * C;
-  const bool active = k < C;
-  const int64_t sid = n * C + k;
-  int2* slot = reinterpret_cast<int2*>(a.slots) + (active ? sid : 0) * a.slot_cap;
+  const int64_t sid = (int64_t)blockIdx.x * wpb + wave;
+  if (wave >= wpb || sid >= a.N * C) return;        // wave-uniform
+  const int64_t n = sid / C, k = sid - n * C;
+  uint64_t* om = ev_lds + (int64_t)wave * 2 * W;
+  uint64_t* lm = om + W;
+  const float* xs = a.x + n * T * C + k;
+  const float hi = a.hi[k];
+  const double lo = a.lo[k];
+  const float lo_f = (float)lo;
+  const bool use_lo = a.use_lo != 0;
+  // mode 1: scan limit and per-block vote requirement (vad.py:62-78)
+  const int64_t step = a.step, sd = a.sd, interval = sd * 100 - step;
+  const int64_t lim = MODE == 0 ? T : ((T - step > 0) ? ((T - step + step - 1) / step) * step : 0);
+
+  // pass 1: bitmaps, 8 words (512 frames) of loads in flight per lane
+  for (int64_t w0 = 0; w0 < W; w0 += 8) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int64_t t = (w0 + j) * 64 + lane;
+      v[j] = t < T ? xs[t * C] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (w0 + j >= W) break;
+      const int64_t t = (w0 + j) * 64 + lane;
+      bool on;
+      if (MODE == 0) {
+        on = t < T && v[j] > hi;                    // float32 compare (numpy f32 row vs python float)
+      } else {
+        const int64_t i = (t / step) * step;
+        const int64_t nov = i < interval ? i / step + 1 : (i >= T - interval ? (T - i) / step + 1 : sd);
+        on = t < lim && (double)v[j] >= (double)nov;
+      }
+      const bool below = t < T && (MODE == 0 ? (v[j] < lo_f) : ((double)v[j] < lo));
+      const uint64_t bon = __ballot(on), bbe = __ballot(below);
+      if (lane == 0) {
+        om[w0 + j] = bon;
+        lm[w0 + j] = bbe;
+      }
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+  // pass 2: runs of the on-bitmap through the reference's list stages
+  const int64_t ns = a.n_smooth[k], nsalt = a.n_salt[k];
+  int2* slot = reinterpret_cast<int2*>(a.slots) + sid * a.slot_cap;
   int64_t cnt = 0;
-  int64_t t0 = 0, t1 = 0;              // frames [t0, t1) in LDS
-  auto X = [&](int64_t i) -> float {
-    return (i >= t0 && i < t1) ? s_x[(i - t0) * C + k] : xg[i * C + k];
-  };
-  SeriesState st;
-  series_init(st);
-  const float hi = active ? a.hi[k] : 0.f;
-  const double lo = active ? a.lo[k] : 0.0;
-  const int64_t ns = active ? a.n_smooth[k] : 0, nsalt = active ? a.n_salt[k] : 0;
   auto emit = [&](int64_t b, int64_t f) {
-    if (cnt < a.slot_cap) slot[cnt] = make_int2((int)b, (int)f);
+    if (lane == 0 && cnt < a.slot_cap) slot[cnt] = make_int2((int)b, (int)f);
     ++cnt;
   };
-  for (int64_t c0 = 0; c0 < T; c0 += TC) {
-    const int64_t c1 = min(T, c0 + TC);
-    __syncthreads();
-    const float* src = xg + c0 * C;
-    for (int64_t i = threadIdx.x; i < (c1 - c0) * C; i += 256) s_x[i] = src[i];
-    __syncthreads();
-    t0 = c0;
-    t1 = c1;
-    if (active && st.ok)
-      series_frames<MODE>(st, X, T, c0, c1, hi, lo, a.use_lo != 0, ns, nsalt, a.step, a.sd, emit);
+  const BelowMask bm{lm, W, T};
+  SeriesState st;
+  series_init(st);
+  int64_t w = 0;
+  uint64_t cur = W > 0 ? ev_uniform(om[0]) : 0;     // on-bits of word w not yet consumed
+  while (st.ok) {
+    while (!cur && ++w < W) cur = ev_uniform(om[w]);
+    if (!cur) break;
+    const int64_t rs = w * 64 + __builtin_ctzll(cur);
+    // run end: first off bit after rs
+    uint64_t off = ~ev_uniform(om[w]) & (~0ull << (rs & 63));
+    int64_t we = w;
+    while (!off && ++we < W) off = ~ev_uniform(om[we]);
+    const int64_t re1 = off ? we * 64 + __builtin_ctzll(off) : W * 64;   // one past the run
+    const int64_t re = (re1 < T ? re1 : T) - 1;
+    // find_bgn_fin_pairs vad.py:115-121: a completed run is held until the
+    // next one shows it was not the last
+    if (st.pending) push_pair_m(st, bm, T, st.pb, st.pe + 1, use_lo, ns, nsalt, emit);
+    st.pb = st.first ? rs : rs + 1;
+    st.pe = re;
+    st.pending = true;
+    st.first = false;
+    if (re1 >= W * 64) break;
+    w = re1 >> 6;
+    cur = ev_uniform(om[w]) & (~0ull << (re1 & 63));
   }
-  if (!active) return;
-  if (st.ok) series_finish<MODE>(st, X, T, lo, a.use_lo != 0, ns, nsalt, emit);
-  a.counts[sid] = st.ok ? cnt : 0;
-  if (!st.ok) atomicOr(reinterpret_cast<unsigned long long*>(a.info + 1), 1ull);
+  if (st.ok && st.pending) push_pair_m(st, bm, T, st.pb, st.pe, use_lo, ns, nsalt, emit);  // fin = locts[-1]
+  if (st.ok && use_lo && st.s1_any) push2(st, st.s1_mem, st.s1_pre, ns, nsalt, emit);
+  if (st.ok && st.s2_any) final_out(st.s2_mem, st.s2_pre, nsalt, emit);
+  if (lane == 0) {
+    a.counts[sid] = st.ok ? cnt : 0;
+    if (!st.ok) atomicOr(reinterpret_cast<unsigned long long*>(a.info + 1), 1ull);
+  }
 }
 
 // exclusive scan of the per-series counts + copy of the slots into the
@@ -268,13 +287,28 @@ size_t events_workspace_bytes(int64_t n_series, int64_t T, int64_t C) {
   return al(n_series * 8) + al(n_series * events_slot_cap(T) * 8) + al(C * 4) + 3 * al(C * 8);
 }
 
+int64_t events_max_frames() { return EV_MAX_WORDS * 64; }
+
 void launch_events(const EventArgs& a, int mode, hipStream_t s) {
   (void)hipMemsetAsync(a.info, 0, 2 * sizeof(int64_t), s);
-  if (a.N * a.C == 0) return;
+  const int64_t n = a.N * a.C;
+  if (n == 0) return;
+  const int64_t W = (a.T + 63) / 64;              // <= EV_MAX_WORDS (api.cpp checks)
+  int wpb = (int)std::min<int64_t>(EV_WAVES, std::max<int64_t>(1, EV_LDS_BYTES / (16 * std::max<int64_t>(W, 1))));
+  const unsigned blocks = (unsigned)((n + wpb - 1) / wpb);
+  const size_t lds = (size_t)wpb * 2 * W * 8;
+  static bool attr = false;                      // > 64 KB of dynamic LDS must be opted into
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(events_series_kernel<0>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)EV_LDS_BYTES);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(events_series_kernel<1>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)EV_LDS_BYTES);
+    attr = true;
+  }
   if (mode == 0)
-    hipLaunchKernelGGL(events_clip_kernel<0>, dim3((unsigned)a.N), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(events_series_kernel<0>, dim3(blocks), dim3(64 * wpb), lds, s, a, W, wpb);
   else
-    hipLaunchKernelGGL(events_clip_kernel<1>, dim3((unsigned)a.N), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(events_series_kernel<1>, dim3(blocks), dim3(64 * wpb), lds, s, a, W, wpb);
   hipLaunchKernelGGL(events_compact_kernel, dim3(1), dim3(1024), 0, s, a);
 }
 

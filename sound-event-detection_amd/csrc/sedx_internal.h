@@ -135,6 +135,7 @@ struct EventArgs {
   int64_t capacity;
 };
 int64_t events_slot_cap(int64_t T);
+int64_t events_max_frames();
 size_t events_workspace_bytes(int64_t n_series, int64_t T, int64_t C);
 void launch_events(const EventArgs& a, int mode, hipStream_t s);
 

@@ -63,6 +63,32 @@ def test_device_events_match_host_and_oracle():
             assert got == ref
 
 
+def test_device_events_edge_lengths():
+    """Word boundaries of the per-series bitmaps: runs that end exactly at a
+    64-frame boundary or at T, all-on / all-off series, dense alternation,
+    long series; device == host C++ path bit for bit."""
+    rng = np.random.default_rng(5)
+    for T in (1, 2, 63, 64, 65, 127, 128, 129, 1000, 4096, 5003):
+        C = 7
+        fw = _series(rng, 2, T, C)
+        fw[0, :, 0] = 0.9                                   # one run over the whole series
+        fw[0, :, 1] = 0.1                                   # no run
+        fw[0, :, 2] = np.where(np.arange(T) % 2 == 0, 0.9, 0.1)      # alternating
+        fw[0, :, 3] = np.where((np.arange(T) // 64) % 2 == 0, 0.9, 0.35)  # 64-frame blocks
+        fw[0, :, 4] = np.where(np.arange(T) >= T - 1, 0.9, 0.1)  # last frame only
+        for low in (None, 0.3, -0.1):
+            params = {'sed_high_threshold': 0.5, 'sed_low_threshold': low,
+                      'n_smooth': int(rng.integers(0, 4)), 'n_salt': int(rng.integers(0, 4))}
+            try:
+                host = inference.event_pairs(fw, params)
+            except RuntimeError:
+                with pytest.raises(RuntimeError):
+                    inference.event_pairs(torch.from_numpy(fw).cuda(), params)
+                continue
+            dev = inference.event_pairs(torch.from_numpy(fw).cuda(), params)
+            np.testing.assert_array_equal(dev, host, err_msg='T=%d low=%s' % (T, low))
+
+
 def test_device_events_vad_kat(golden_dir):
     kat = json.load(open(os.path.join(golden_dir, 'vad_kat.json')))
     for case in kat:
