@@ -31,6 +31,7 @@ struct DevWeights {
   float* mel_w = nullptr;
   int32_t* mel_off = nullptr;
   int32_t* mel_lo = nullptr;
+  int32_t mel_nnz = 0;
   float* bn0_scale = nullptr;
   float* bn0_mean = nullptr;
   float* bn0_bias = nullptr;
@@ -728,6 +729,7 @@ sedx_status sedx_finalize_weights(sedx_handle* h) {
   add((void**)&W.mel_w, mel_w.data(), mel_w.size() * 4);
   add((void**)&W.mel_off, mel_off.data(), mel_off.size() * 4);
   add((void**)&W.mel_lo, mel_lo.data(), mel_lo.size() * 4);
+  W.mel_nnz = mel_off[64];
   add((void**)&W.bn0_scale, sc0f.data(), 64 * 4);
   add((void**)&W.bn0_mean, mu0.data(), 64 * 4);
   add((void**)&W.bn0_bias, bi0.data(), 64 * 4);
@@ -874,6 +876,7 @@ static sedx_status forward_wave(sedx_handle* h, const float* d_wave, const int16
   p.mel_w = h->w.mel_w;
   p.mel_off = h->w.mel_off;
   p.mel_lo = h->w.mel_lo;
+  p.mel_nnz = h->w.mel_nnz;
   p.bn_scale = h->w.bn0_scale;
   p.bn_mean = h->w.bn0_mean;
   p.bn_bias = h->w.bn0_bias;
@@ -1022,6 +1025,7 @@ static sedx_status forward_windows_impl(sedx_handle* h, const float* d_audio, in
   p.mel_w = h->w.mel_w;
   p.mel_off = h->w.mel_off;
   p.mel_lo = h->w.mel_lo;
+  p.mel_nnz = h->w.mel_nnz;
   p.bn_scale = h->w.bn0_scale;
   p.bn_mean = h->w.bn0_mean;
   p.bn_bias = h->w.bn0_bias;

@@ -22,54 +22,69 @@ __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
 __device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
 
+// LDS hand-off inside one wavefront: a wave's LDS operations complete in
+// issue order, so waiting for its own (lgkmcnt) and fencing the compiler is
+// enough — no workgroup barrier, and global loads in flight are not drained.
+__device__ __forceinline__ void wave_lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+struct BlockSync {
+  __device__ void operator()() const { __syncthreads(); }
+};
+struct WaveSync {
+  __device__ void operator()() const { wave_lds_sync(); }
+};
+
 // In-LDS Stockham FFT of N2 complex points (forward, e^{-2 pi i}); one wave.
-// tw = exp(-2 pi i m / NFFT) with NFFT = 2*N2.  Result lands in *res.
-// Every lane of the block must call it (block barriers inside).
-template <int N2>
-__device__ __forceinline__ void stockham_fft(float2* X, float2* Y, const float2* tw, int lane,
-                                             float2** res) {
-  constexpr int NFFT = 2 * N2;
-  int Ns = 1;
+// tw = exp(-2 pi i m / NFFT) with NFFT = 2*N2.  Radix 4 while N2/Ns allows,
+// then radix 2; every stage's geometry is a compile-time constant.
+// BlockSync: every lane of the block calls it (block barriers inside).
+template <int N2, int Ns, typename Sync>
+__device__ __forceinline__ float2* stockham_stages(float2* X, float2* Y, const float2* tw, int lane) {
+  if constexpr (Ns >= N2) {
+    return X;
+  } else {
+    constexpr int NFFT = 2 * N2;
+    constexpr int R = ((N2 / Ns) % 4 == 0) ? 4 : 2;
+    constexpr int nb = N2 / R;
+    constexpr int step = NFFT / (Ns * R);
 #pragma unroll
-  for (int stage = 0; stage < 12; ++stage) {
-    if (Ns >= N2) break;
-    const int R = ((N2 / Ns) % 4 == 0) ? 4 : 2;
-    const int nb = N2 / R;
-    if (R == 4) {
-      for (int j = lane; j < nb; j += 64) {
-        const int k = j & (Ns - 1);
+    for (int j0 = 0; j0 < nb; j0 += 64) {
+      const int j = j0 + lane;
+      if (j >= nb) break;
+      const int k = j & (Ns - 1);
+      const int base = (j - k) * R + k;
+      if constexpr (R == 4) {
         float2 v0 = X[j], v1 = X[j + nb], v2 = X[j + 2 * nb], v3 = X[j + 3 * nb];
-        const int step = NFFT / (Ns * 4);
-        if (Ns > 1) {
+        if constexpr (Ns > 1) {
           v1 = cmul(v1, tw[k * step]);
           v2 = cmul(v2, tw[2 * k * step]);
           v3 = cmul(v3, tw[3 * k * step]);
         }
         const float2 a0 = cadd(v0, v2), a1 = csub(v0, v2);
         const float2 b0 = cadd(v1, v3), b1 = csub(v1, v3);
-        // -i * b1
-        const float2 mib1 = make_float2(b1.y, -b1.x);
-        const int base = (j - k) * 4 + k;
+        const float2 mib1 = make_float2(b1.y, -b1.x);   // -i * b1
         Y[base] = cadd(a0, b0);
         Y[base + Ns] = cadd(a1, mib1);
         Y[base + 2 * Ns] = csub(a0, b0);
         Y[base + 3 * Ns] = csub(a1, mib1);
-      }
-    } else {
-      for (int j = lane; j < nb; j += 64) {
-        const int k = j & (Ns - 1);
+      } else {
         float2 v0 = X[j], v1 = X[j + nb];
-        if (Ns > 1) v1 = cmul(v1, tw[k * (NFFT / (Ns * 2))]);
-        const int base = (j - k) * 2 + k;
+        if constexpr (Ns > 1) v1 = cmul(v1, tw[k * step]);
         Y[base] = cadd(v0, v1);
         Y[base + Ns] = csub(v0, v1);
       }
     }
-    __syncthreads();
-    float2* t = X; X = Y; Y = t;
-    Ns *= R;
+    Sync()();
+    return stockham_stages<N2, Ns * R, Sync>(Y, X, tw, lane);
   }
-  *res = X;
+}
+
+template <int N2, typename Sync = BlockSync>
+__device__ __forceinline__ void stockham_fft(float2* X, float2* Y, const float2* tw, int lane,
+                                             float2** res) {
+  *res = stockham_stages<N2, 1, Sync>(X, Y, tw, lane);
 }
 
 // Real-input spectrum bin k (0..N2) from the N2-point complex FFT Z of
@@ -84,96 +99,154 @@ __device__ __forceinline__ float2 real_bin(const float2* Z, const float2* tw, in
   return cadd(E, cmul(tw[k], O));
 }
 
+// One wavefront per frame, the four waves of a workgroup independent (no
+// workgroup barrier after the table staging).  Twiddles, window and the
+// packed mel weights sit in LDS; a lane's mel band geometry and bn0 constants
+// sit in registers; the next frame's samples are loaded into registers while
+// the current frame is transformed.
+constexpr int MEL_LDS_CAP = 8192;     // packed mel weights staged in (dynamic) LDS up to this many
+
 template <int NFFT, bool I16>
-__global__ __launch_bounds__(256) void logmel_kernel(FrontendParams p) {
+__global__ __launch_bounds__(256, 8) void logmel_kernel(FrontendParams p) {
   constexpr int N2 = NFFT / 2;
+  constexpr int NS = NFFT / 64;          // samples per lane per frame
   __shared__ float2 s_tw[NFFT];
+  __shared__ float s_win[NFFT];
   __shared__ float2 s_buf[4][2][N2];
+  extern __shared__ float s_melw[];      // [nnz] when nnz <= MEL_LDS_CAP (launch sizes it)
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  for (int i = threadIdx.x; i < NFFT; i += 256) s_tw[i] = p.twiddle[i];
+  const int nnz = p.mel_off[64];
+  const bool mel_in_lds = nnz <= MEL_LDS_CAP;
+  for (int i = threadIdx.x; i < NFFT; i += 256) {
+    s_tw[i] = p.twiddle[i];
+    s_win[i] = p.window[i];
+  }
+  if (mel_in_lds)
+    for (int i = threadIdx.x; i < nnz; i += 256) s_melw[i] = p.mel_w[i];
+  const int m = lane;                    // mel band of this lane
+  const int mlo = p.mel_lo[m], o0 = p.mel_off[m], o1 = p.mel_off[m + 1];
+  const float bmu = p.bn_mean[m], bsc = p.bn_scale[m], bbi = p.bn_bias[m];
   __syncthreads();
 
-  const int64_t items = (int64_t)p.n_clips * p.n_win;
-  const int64_t total = items * p.T;
+  const int64_t total = (int64_t)p.n_clips * p.n_win * p.T;
   const int64_t L = p.sig_len;
-  for (int64_t f0 = (int64_t)blockIdx.x * 4; f0 < total; f0 += (int64_t)gridDim.x * 4) {
-    const int64_t fr = f0 + wave;
-    const bool valid = fr < total;
-    float2* X = s_buf[wave][0];
-    float2* Y = s_buf[wave][1];
-    int64_t item = 0;
-    int t = 0;
-    if (valid) {
-      item = fr / p.T;
-      t = (int)(fr - item * p.T);
-      const int64_t clip = item / p.n_win;
-      const int w = (int)(item - clip * p.n_win);
-      const int64_t wstart = p.win_start[w];
-      const int64_t src_off = clip * p.clip_stride + wstart;
-      const float* src = p.audio + src_off;
-      const int16_t* src16 = p.audio_i16 + src_off;
-      const int64_t avail = p.clip_len - wstart;  // samples of this item backed by audio
-      const int64_t pos0 = (int64_t)t * p.hop - N2;   // start in un-padded coordinates
-      for (int m = lane; m < N2; m += 64) {
-        float v[2];
+  float2* X = s_buf[wave][0];
+  float2* Y = s_buf[wave][1];
+  // samples of frame fr: lane holds j = pos0 + 2 (lane + 64 i) + e
+  auto load = [&](int64_t fr, float* v) {
+    const int64_t item = fr / p.T;
+    const int t = (int)(fr - item * p.T);
+    const int64_t clip = item / p.n_win;
+    const int w = (int)(item - clip * p.n_win);
+    const int64_t wstart = p.win_start[w];
+    const int64_t src_off = clip * p.clip_stride + wstart;
+    const int64_t avail = p.clip_len - wstart;      // samples of this item backed by audio
+    const int64_t pos0 = (int64_t)t * p.hop - N2;   // start in un-padded coordinates
 #pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          int64_t j = pos0 + 2 * m + e;
-          if (j < 0) j = -j;                       // reflect (F.pad mode='reflect')
-          if (j >= L) j = 2 * (L - 1) - j;
-          if (I16)   // int16_to_float32: float64 x / 32767, rounded to float32
-            v[e] = (j < avail) ? (float)((double)src16[j] / 32767.0) : 0.0f;
-          else
-            v[e] = (j < avail) ? src[j] : 0.0f;    // pad_truncate zeros
-          v[e] *= p.window[2 * m + e];
-        }
-        X[m] = make_float2(v[0], v[1]);
+    for (int i = 0; i < NS / 2; ++i)
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        int64_t j = pos0 + 2 * (lane + 64 * i) + e;
+        if (j < 0) j = -j;                           // reflect (F.pad mode='reflect')
+        if (j >= L) j = 2 * (L - 1) - j;
+        const bool ok = j < avail;                   // pad_truncate zeros
+        const int64_t jc = ok ? j : 0;
+        if (I16)   // int16_to_float32: float64 x / 32767, rounded to float32
+          v[2 * i + e] = ok ? (float)((double)p.audio_i16[src_off + jc] / 32767.0) : 0.0f;
+        else
+          v[2 * i + e] = ok ? p.audio[src_off + jc] : 0.0f;
       }
+  };
+  int64_t fr = (int64_t)blockIdx.x * 4 + wave;
+  const int64_t fstride = (int64_t)gridDim.x * 4;
+  float v[NS];
+  if (fr < total) load(fr, v);
+  for (; fr < total; fr += fstride) {
+#pragma unroll
+    for (int i = 0; i < NS / 2; ++i) {
+      const int mm = lane + 64 * i;
+      X[mm] = make_float2(v[2 * i] * s_win[2 * mm], v[2 * i + 1] * s_win[2 * mm + 1]);
     }
-    __syncthreads();
+    if (fr + fstride < total) load(fr + fstride, v);   // next frame, in flight during the FFT
+    wave_lds_sync();
     float2* Z;
-    stockham_fft<N2>(X, Y, s_tw, lane, &Z);
+    stockham_fft<N2, WaveSync>(X, Y, s_tw, lane, &Z);
     float* P = reinterpret_cast<float*>(Z == X ? Y : X);   // the other buffer
-    if (valid) {
-      for (int k = lane; k <= N2; k += 64) {
-        const float2 Xk = real_bin<N2>(Z, s_tw, k);
-        P[k] = Xk.x * Xk.x + Xk.y * Xk.y;
+#pragma unroll
+    for (int i = 0; i < N2 / 64; ++i) {
+      const int k = lane + 64 * i;
+      const float2 Xk = real_bin<N2>(Z, s_tw, k);
+      P[k] = Xk.x * Xk.x + Xk.y * Xk.y;
+    }
+    if (lane == 0) {                      // Nyquist bin
+      const float2 Xk = real_bin<N2>(Z, s_tw, N2);
+      P[N2] = Xk.x * Xk.x + Xk.y * Xk.y;
+    }
+    wave_lds_sync();
+    // band sum in bin order (the fma chain of the sparse dot product), four
+    // bins' loads issued together
+    float acc = 0.0f;
+    if (mel_in_lds) {
+      for (int i = o0; i < o1; i += 4) {
+        float pw[4], ww[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const bool ok = i + e < o1;
+          pw[e] = ok ? P[mlo + (i + e - o0)] : 0.f;
+          ww[e] = ok ? s_melw[i + e] : 0.f;
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (i + e < o1) acc = fmaf(pw[e], ww[e], acc);
       }
+    } else {
+      for (int i = o0; i < o1; ++i) acc = fmaf(P[mlo + (i - o0)], p.mel_w[i], acc);
     }
-    __syncthreads();
-    if (valid) {
-      const int m = lane;
-      const int lo = p.mel_lo[m];
-      const int o0 = p.mel_off[m], o1 = p.mel_off[m + 1];
-      float acc = 0.0f;
-      for (int i = o0; i < o1; ++i) acc = fmaf(P[lo + (i - o0)], p.mel_w[i], acc);
-      float db = 10.0f * log10f(fmaxf(acc, 1e-10f));
-      db = (db - p.bn_mean[m]) * p.bn_scale[m] + p.bn_bias[m];
-      p.out[fr * 64 + m] = db;
-    }
-    __syncthreads();
+    float db = 10.0f * log10f(fmaxf(acc, 1e-10f));
+    db = (db - bmu) * bsc + bbi;
+    p.out[fr * 64 + m] = db;
+    wave_lds_sync();                      // P / Z reads done before the next frame's writes
   }
+}
+
+// persistent-style grid: every resident wave walks several frames, so the
+// register prefetch of the next frame overlaps the current FFT
+template <int NFFT, bool I16>
+static void launch_logmel_t(const FrontendParams& p, int64_t total, hipStream_t s) {
+  // dynamic LDS = the packed mel weights (host copy of mel_off[64] kept in p)
+  const size_t dyn = p.mel_nnz <= MEL_LDS_CAP ? (size_t)p.mel_nnz * 4 : 0;
+  static int resident = 0;
+  static size_t resident_dyn = ~size_t(0);
+  if (resident_dyn != dyn) {
+    int dev = 0, ncu = 0, per_cu = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, logmel_kernel<NFFT, I16>, 256, dyn);
+    resident = (ncu > 0 ? ncu : 256) * (per_cu > 0 ? per_cu : 1);
+    resident_dyn = dyn;
+  }
+  int64_t blocks = (total + 3) / 4;
+  if (blocks > resident) blocks = resident;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL((logmel_kernel<NFFT, I16>), dim3((unsigned)blocks), dim3(256), dyn, s, p);
 }
 
 void launch_logmel(const FrontendParams& p, int n_fft, hipStream_t s) {
   const int64_t total = (int64_t)p.n_clips * p.n_win * p.T;
-  int64_t blocks = (total + 3) / 4;
-  if (blocks > 8192) blocks = 8192;
-  if (blocks < 1) blocks = 1;
   const bool i16 = p.audio_i16 != nullptr;
   switch (n_fft) {
     case 256:
-      if (i16) hipLaunchKernelGGL((logmel_kernel<256, true>), dim3(blocks), dim3(256), 0, s, p);
-      else hipLaunchKernelGGL((logmel_kernel<256, false>), dim3(blocks), dim3(256), 0, s, p);
+      if (i16) launch_logmel_t<256, true>(p, total, s);
+      else launch_logmel_t<256, false>(p, total, s);
       break;
     case 512:
-      if (i16) hipLaunchKernelGGL((logmel_kernel<512, true>), dim3(blocks), dim3(256), 0, s, p);
-      else hipLaunchKernelGGL((logmel_kernel<512, false>), dim3(blocks), dim3(256), 0, s, p);
+      if (i16) launch_logmel_t<512, true>(p, total, s);
+      else launch_logmel_t<512, false>(p, total, s);
       break;
     case 1024:
-      if (i16) hipLaunchKernelGGL((logmel_kernel<1024, true>), dim3(blocks), dim3(256), 0, s, p);
-      else hipLaunchKernelGGL((logmel_kernel<1024, false>), dim3(blocks), dim3(256), 0, s, p);
+      if (i16) launch_logmel_t<1024, true>(p, total, s);
+      else launch_logmel_t<1024, false>(p, total, s);
       break;
     default: break;
   }

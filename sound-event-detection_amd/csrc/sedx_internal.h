@@ -27,6 +27,7 @@ struct FrontendParams {
   const float* mel_w;       // packed band weights
   const int32_t* mel_off;   // [65] offsets into mel_w
   const int32_t* mel_lo;    // [64] first fft bin of each band
+  int32_t mel_nnz;          // host copy of mel_off[64] (sizes the LDS copy of mel_w)
   const float* bn_scale;    // [64] bn0 folded
   const float* bn_mean;     // [64]
   const float* bn_bias;     // [64]
