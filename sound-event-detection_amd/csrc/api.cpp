@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -31,7 +32,6 @@ struct DevWeights {
   float* mel_w = nullptr;
   int32_t* mel_off = nullptr;
   int32_t* mel_lo = nullptr;
-  int32_t mel_nnz = 0;
   float* bn0_scale = nullptr;
   float* bn0_mean = nullptr;
   float* bn0_bias = nullptr;
@@ -82,10 +82,12 @@ struct sedx_handle {
   // optional per-stage timing (sedx_set_profiling): events at stage boundaries
   int precision = SEDX_PRECISION_X3;   // conv stack arithmetic (sedx_set_precision)
   bool gru_simple = getenv("SEDX_GRU_SIMPLE") != nullptr;   // A/B: per-(clip,dir) recurrence
+  bool debug_x0 = getenv("SEDX_DEBUG_X0") != nullptr;      // diagnostic: X0 snapshot after the frontend
   bool profiling = false;
   hipEvent_t ev[SEDX_N_STAGES + 1] = {};
   bool ev_recorded[SEDX_N_STAGES + 1] = {};
 };
+
 
 namespace {
 inline void mark(sedx_handle* h, int i, hipStream_t s) {
@@ -192,7 +194,7 @@ Geometry geometry_from_T(const sedx_handle* h, int64_t T) {
 
 // workspace layout (floats), 256-B aligned regions
 struct WsLayout {
-  size_t x0, bufA, bufB, total_bytes;
+  size_t x0, bufA, bufB, sched, dbg, total_bytes;
 };
 
 size_t align_up(size_t x) { return (x + 63) & ~size_t(63); }
@@ -217,6 +219,10 @@ WsLayout ws_layout(const sedx_handle* h, int64_t B, const Geometry& g) {
   b = std::max(b, (size_t)B * g.T3 * 512);
   l.bufB = off;
   off += align_up(b);
+  l.sched = off;                                  // 7 conv launches x CONV_SCHED_INTS claim counters
+  off += align_up(7 * CONV_SCHED_INTS);
+  l.dbg = off;                                    // SEDX_DEBUG_X0: copy of X0 taken after the frontend
+  if (h->debug_x0) off += align_up((size_t)B * g.T * 64);
   l.total_bytes = off * sizeof(float);
   return l;
 }
@@ -249,10 +255,12 @@ sedx_status run_body(sedx_handle* h, int64_t B, const Geometry& g, float* ws, co
   const int iB = (int)B;
   mark(h, 1, s);
   const bool x3 = h->precision == SEDX_PRECISION_X3;
+  int* sched = reinterpret_cast<int*>(ws + l.sched);
   if (x3) {
+    HIP_TRY(h, hipMemsetAsync(sched, 0, 7 * CONV_SCHED_INTS * sizeof(int), s));
     // block 1 as one launch: conv1 computed inside conv2's halo staging (the
     // b1c1 stage is then just the zero-bordered copy of the bn0 output)
-    launch_block1_fused_x3(X0, iB, (int)g.T, A, w.c1_wt, w.c1_b, w.wx3[1], w.cb[1], nullptr, s);
+    launch_block1_fused_x3(X0, iB, (int)g.T, A, w.c1_wt, w.c1_b, w.wx3[1], w.cb[1], nullptr, nullptr, s);
   } else {
     launch_conv_c1(X0, iB, (int)g.T, w.c1_w, w.c1_b, A, s);
   }
@@ -272,9 +280,11 @@ sedx_status run_body(sedx_handle* h, int64_t B, const Geometry& g, float* ws, co
     const L& c = layers[i];
     mark(h, 2 + i, s);
     if (x3 && i == 0)
-      launch_block1_fused_x3(nullptr, iB, c.T, A, w.c1_wt, w.c1_b, w.wx3[c.idx], w.cb[c.idx], c.out, s);
+      launch_block1_fused_x3(nullptr, iB, c.T, A, w.c1_wt, w.c1_b, w.wx3[c.idx], w.cb[c.idx], c.out,
+                             sched, s);
     else if (x3)
-      launch_conv3x3_x3(c.in, iB, c.T, c.F, c.cin, c.cout, w.wx3[c.idx], w.cb[c.idx], c.out, c.epi, s);
+      launch_conv3x3_x3(c.in, iB, c.T, c.F, c.cin, c.cout, w.wx3[c.idx], w.cb[c.idx], c.out, c.epi,
+                        sched + i * CONV_SCHED_INTS, s);
     else
       launch_conv3x3(c.in, iB, c.T, c.F, c.cin, c.cout, w.wp[c.idx], w.cb[c.idx], c.out, c.epi, s);
   }
@@ -729,7 +739,6 @@ sedx_status sedx_finalize_weights(sedx_handle* h) {
   add((void**)&W.mel_w, mel_w.data(), mel_w.size() * 4);
   add((void**)&W.mel_off, mel_off.data(), mel_off.size() * 4);
   add((void**)&W.mel_lo, mel_lo.data(), mel_lo.size() * 4);
-  W.mel_nnz = mel_off[64];
   add((void**)&W.bn0_scale, sc0f.data(), 64 * 4);
   add((void**)&W.bn0_mean, mu0.data(), 64 * 4);
   add((void**)&W.bn0_bias, bi0.data(), 64 * 4);
@@ -876,13 +885,15 @@ static sedx_status forward_wave(sedx_handle* h, const float* d_wave, const int16
   p.mel_w = h->w.mel_w;
   p.mel_off = h->w.mel_off;
   p.mel_lo = h->w.mel_lo;
-  p.mel_nnz = h->w.mel_nnz;
   p.bn_scale = h->w.bn0_scale;
   p.bn_mean = h->w.bn0_mean;
   p.bn_bias = h->w.bn0_bias;
   p.out = ws + l.x0;
   mark(h, 0, s);
   launch_logmel(p, h->cfg.window_size, s);
+  if (h->debug_x0)
+    HIP_TRY(h, hipMemcpyAsync(ws + l.dbg, ws + l.x0, (size_t)B * g.T * 64 * sizeof(float),
+                              hipMemcpyDeviceToDevice, s));
   return run_body(h, B, g, ws, l, d_framewise, d_clipwise, d_embedding, s);
 }
 
@@ -1025,7 +1036,6 @@ static sedx_status forward_windows_impl(sedx_handle* h, const float* d_audio, in
   p.mel_w = h->w.mel_w;
   p.mel_off = h->w.mel_off;
   p.mel_lo = h->w.mel_lo;
-  p.mel_nnz = h->w.mel_nnz;
   p.bn_scale = h->w.bn0_scale;
   p.bn_mean = h->w.bn0_mean;
   p.bn_bias = h->w.bn0_bias;

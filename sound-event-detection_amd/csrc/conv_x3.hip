@@ -85,11 +85,17 @@ __device__ __forceinline__ void rowmap(int R, int& tl, int& f) {
 }
 
 // Tiles (b, t-tile, n-tile), n-tile fastest so tiles sharing an input halo
-// run side by side, are dealt in 8 contiguous ranges, one per XCD (workgroup
-// i runs on XCD i % 8), so neighbouring t-tiles share one L2.  A workgroup's
-// units (tile, chunk) form one stream: the pipeline runs straight through
-// tile boundaries, where only the epilogue (stores from the accumulators)
-// is inserted.
+// run side by side, are cut into 8 contiguous ranges, one per XCD, so
+// neighbouring t-tiles share one L2.  Workgroups claim tiles dynamically: a
+// workgroup takes the next tile of its own XCD's range (HW_REG_XCC_ID, one
+// atomic counter per range) and, once that range is empty, steals from the
+// others.  So a workgroup that starts late — its CU was busy with a kernel of
+// another stream, e.g. the GRU recurrence of the previous batch — finds the
+// work already shared out instead of holding the layer back.  A tile's claim
+// is issued one tile ahead and lands in a 4-entry LDS ring read by decode().
+// A workgroup's units (tile, chunk) form one stream: the pipeline runs
+// straight through tile boundaries, where only the epilogue (stores from the
+// accumulators) is inserted.
 #ifdef SEDX_CONV_STAMPS
 // diagnostic build (tools/conv_bench.cpp): per-wave s_memtime sums
 __device__ unsigned long long g_conv_stamps[8];
@@ -145,7 +151,8 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
                                                          const float* __restrict__ bias,
                                                          float* __restrict__ out,
                                                          const float* __restrict__ w1,
-                                                         const float* __restrict__ b1) {
+                                                         const float* __restrict__ b1,
+                                                         int* __restrict__ sched) {
   constexpr int BM = ConvGeom<F, BN>::BM, TT = ConvGeom<F, BN>::TT;
   constexpr int RT = TT + 2, CS = F + 2;
   constexpr int CSP = (EPI == EPI_POOL2) ? (F == 64 ? 72 : F == 32 ? 40 : 24)
@@ -165,6 +172,7 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
 
   // W ring first so every fragment read is (lane base VGPR) + immediate
   __shared__ uint4 lds[2 * WS_U4 + 2 * A_U4];
+  __shared__ int s_tiles[4];              // claimed tile of the workgroup's k-th tile, at k & 3
   uint4* const Wbuf = lds;
   uint4* const Abuf = lds + 2 * WS_U4;
 
@@ -176,17 +184,47 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
   const int nN = Cout / BN;
   const int ntiles = B * tiles_t * nN;
   const int per_xcd = (ntiles + 7) >> 3;
-  const int xcd = blockIdx.x & 7, slot0 = blockIdx.x >> 3, slots = gridDim.x >> 3;
   const int nchunks = Cin >> 4;           // even for every layer (host checks)
 
+  // ---- dynamic tile claims (thread 0) ----
+  unsigned xid;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xid));
+  const int xcd = (int)(xid & 7u);
+  auto range_len = [&](int x) { return min(per_xcd, ntiles - x * per_xcd); };
+  // claim from ranges xcd+r, r >= r0; returns a tile or -1
+  auto steal = [&](int r0) -> int {
+    for (int r = r0; r < 8; ++r) {
+      const int x = (xcd + r) & 7;
+      if (range_len(x) <= 0) continue;
+      const int v = atomicAdd(&sched[32 * x], 1);
+      if (v < range_len(x)) return x * per_xcd + v;
+    }
+    return -1;
+  };
+  int g_pend = 0, g_k = 0;                // thread 0: own-range claim in flight for tile g_k
+  bool g_have = false, g_done = false;
+  auto claim_issue = [&](int k) {         // at decode of tile k - 1 (thread 0)
+    if (g_done) return;
+    g_k = k;
+    g_have = true;
+    g_pend = range_len(xcd) > 0 ? atomicAdd(&sched[32 * xcd], 1) : 0x7fffffff;
+  };
+  auto claim_land = [&]() {               // >= 1 barrier before decode of tile g_k (thread 0)
+    if (!g_have) return;
+    g_have = false;
+    int t = g_pend < range_len(xcd) ? xcd * per_xcd + g_pend : steal(1);
+    if (t < 0) g_done = true;
+    s_tiles[g_k & 3] = t;
+  };
+
   auto decode = [&](ConvCursor& c) {
-    const int within = slot0 + c.k * slots;
-    const int tile = xcd * per_xcd + within;
-    c.valid = within < per_xcd && tile < ntiles;
+    const int tile = s_tiles[c.k & 3];
+    c.valid = tile >= 0;
     const int m = c.valid ? tile / nN : 0;   // past the end: loads stay in bounds
     c.nb = c.valid ? tile - m * nN : 0;
     c.b = m / tiles_t;
     c.t0 = (m - c.b * tiles_t) * TT;
+    if (tid == 0 && c.valid) claim_issue(c.k + 1);
   };
   auto advance = [&](ConvCursor& c) {
     if (++c.chunk == nchunks) {
@@ -419,6 +457,12 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
   };
 
   SEDX_ST_DECL
+  if (tid == 0) {
+    const int t = steal(0);
+    if (t < 0) g_done = true;
+    s_tiles[0] = t;
+  }
+  __syncthreads();
   // cur = unit being computed, n1 / n2 = the next two units of the stream
   ConvCursor cur{0, 0, 0, 0, 0, false};
   decode(cur);
@@ -501,6 +545,7 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
       }                                                                                 \
     } else {                                                                            \
       SEDX_ABL_STORE_W((U) & 1, (U) & 1);                                               \
+      if (tid == 0) claim_land();                                                       \
       SEDX_ABL_LOAD_W((U) & 1, n2, 0);                                                  \
     }                                                                                   \
   }
@@ -559,7 +604,7 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
 
 template <int F, int BN, int EPI, bool FUSE = false>
 static void launch_x3_epi(const float* in, int B, int T, int Cin, int Cout, const uint4* wp,
-                          const float* bias, float* out, hipStream_t s,
+                          const float* bias, float* out, int* sched, hipStream_t s,
                           const float* w1 = nullptr, const float* b1 = nullptr) {
   constexpr int TT = ConvGeom<F, BN>::TT;
   static int resident = 0;           // workgroups resident on the whole device
@@ -570,53 +615,54 @@ static void launch_x3_epi(const float* in, int B, int T, int Cin, int Cout, cons
     (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, conv3x3_x3_kernel<F, BN, EPI, FUSE>, 512, 0);
     resident = (ncu > 0 ? ncu : 256) * (per_cu > 0 ? per_cu : 1);
   }
+  const size_t pad = mfma_cu_exclusive_lds(reinterpret_cast<const void*>(conv3x3_x3_kernel<F, BN, EPI, FUSE>), 512);
   const int ntiles = B * ((T + TT - 1) / TT) * (Cout / BN);
   const int per_xcd = (ntiles + 7) / 8;
   int grid = resident & ~7;
   if (grid < 8) grid = 8;
   if (grid > 8 * per_xcd) grid = 8 * per_xcd;
-  hipLaunchKernelGGL((conv3x3_x3_kernel<F, BN, EPI, FUSE>), dim3(grid), dim3(512), 0, s, in, B, T, Cin,
-                     Cout, wp, bias, out, w1, b1);
+  hipLaunchKernelGGL((conv3x3_x3_kernel<F, BN, EPI, FUSE>), dim3(grid), dim3(512), pad, s, in, B, T, Cin,
+                     Cout, wp, bias, out, w1, b1, sched);
 }
 
 template <int F, int BN>
 static void launch_x3(const float* in, int B, int T, int Cin, int Cout, const uint4* wp,
-                      const float* bias, float* out, int epi, hipStream_t s) {
+                      const float* bias, float* out, int epi, int* sched, hipStream_t s) {
   // only the (F, epilogue) pairs of the model are instantiated
   if constexpr (F == 8) {
     if (epi == EPI_STORE)
-      launch_x3_epi<8, BN, EPI_STORE>(in, B, T, Cin, Cout, wp, bias, out, s);
+      launch_x3_epi<8, BN, EPI_STORE>(in, B, T, Cin, Cout, wp, bias, out, sched, s);
     else if (epi == EPI_FMEAN)
-      launch_x3_epi<8, BN, EPI_FMEAN>(in, B, T, Cin, Cout, wp, bias, out, s);
+      launch_x3_epi<8, BN, EPI_FMEAN>(in, B, T, Cin, Cout, wp, bias, out, sched, s);
   } else if constexpr (F == 64) {
     if (epi == EPI_POOL2)
-      launch_x3_epi<F, BN, EPI_POOL2>(in, B, T, Cin, Cout, wp, bias, out, s);
+      launch_x3_epi<F, BN, EPI_POOL2>(in, B, T, Cin, Cout, wp, bias, out, sched, s);
   } else {
     if (epi == EPI_STORE)
-      launch_x3_epi<F, BN, EPI_STORE>(in, B, T, Cin, Cout, wp, bias, out, s);
+      launch_x3_epi<F, BN, EPI_STORE>(in, B, T, Cin, Cout, wp, bias, out, sched, s);
     else if (epi == EPI_POOL2)
-      launch_x3_epi<F, BN, EPI_POOL2>(in, B, T, Cin, Cout, wp, bias, out, s);
+      launch_x3_epi<F, BN, EPI_POOL2>(in, B, T, Cin, Cout, wp, bias, out, sched, s);
   }
 }
 
 // Shapes: Cin a multiple of 32 (the unit stream pairs chunks), Cout a
 // multiple of the n-tile; api.cpp routes only such layers here.
 void launch_conv3x3_x3(const float* in, int B, int T, int F, int Cin, int Cout, const void* wp,
-                       const float* bias, float* out, int epi, hipStream_t s) {
+                       const float* bias, float* out, int epi, int* sched, hipStream_t s) {
   const uint4* w = static_cast<const uint4*>(wp);
-  if (Cin % 32 != 0) return;
+  if (Cin % 32 != 0 || Cin < 64) return;   // the claim of tile k+1 lands >= 1 unit before its decode
   switch (F) {
     case 64:   // block 1 conv2 (Cout 64)
-      if (Cout % 64 == 0) launch_x3<64, 64>(in, B, T, Cin, Cout, w, bias, out, epi, s);
+      if (Cout % 64 == 0) launch_x3<64, 64>(in, B, T, Cin, Cout, w, bias, out, epi, sched, s);
       break;
     case 32:
-      if (Cout % 128 == 0) launch_x3<32, 128>(in, B, T, Cin, Cout, w, bias, out, epi, s);
+      if (Cout % 128 == 0) launch_x3<32, 128>(in, B, T, Cin, Cout, w, bias, out, epi, sched, s);
       break;
     case 16:
-      if (Cout % 128 == 0) launch_x3<16, 128>(in, B, T, Cin, Cout, w, bias, out, epi, s);
+      if (Cout % 128 == 0) launch_x3<16, 128>(in, B, T, Cin, Cout, w, bias, out, epi, sched, s);
       break;
     case 8:
-      if (Cout % 128 == 0) launch_x3<8, 128>(in, B, T, Cin, Cout, w, bias, out, epi, s);
+      if (Cout % 128 == 0) launch_x3<8, 128>(in, B, T, Cin, Cout, w, bias, out, epi, sched, s);
       break;
     default: break;
   }
@@ -637,15 +683,15 @@ __global__ __launch_bounds__(256) void pad_x0_kernel(const float* __restrict__ x
 }
 
 void launch_block1_fused_x3(const float* x0, int B, int T, float* xpad, const float* w1, const float* b1,
-                            const void* wp, const float* bias, float* out, hipStream_t s) {
+                            const void* wp, const float* bias, float* out, int* sched, hipStream_t s) {
   if (x0) {
     const int64_t n = (int64_t)B * (T + 2) * 66;
     const int blocks = (int)std::min<int64_t>((n + 255) / 256, 4096);
     hipLaunchKernelGGL(pad_x0_kernel, dim3(blocks), dim3(256), 0, s, x0, B, T, xpad);
   }
   if (out)
-    launch_x3_epi<64, 64, EPI_POOL2, true>(xpad, B, T, 64, 64, static_cast<const uint4*>(wp), bias, out, s,
-                                           w1, b1);
+    launch_x3_epi<64, 64, EPI_POOL2, true>(xpad, B, T, 64, 64, static_cast<const uint4*>(wp), bias, out,
+                                           sched, s, w1, b1);
 }
 
 size_t block1_pad_floats(int B, int T) { return (size_t)B * (T + 2) * 66; }

@@ -99,31 +99,40 @@ __device__ __forceinline__ float2 real_bin(const float2* Z, const float2* tw, in
   return cadd(E, cmul(tw[k], O));
 }
 
-// One wavefront per frame, the four waves of a workgroup independent (no
+// One wavefront per frame, the waves of a workgroup independent (no
 // workgroup barrier after the table staging).  Twiddles, window and the
 // packed mel weights sit in LDS; a lane's mel band geometry and bn0 constants
 // sit in registers; the next frame's samples are loaded into registers while
 // the current frame is transformed.
-constexpr int MEL_LDS_CAP = 8192;     // packed mel weights staged in (dynamic) LDS up to this many
+//
+// One 1024-thread workgroup per CU, and the workgroup claims the CU's whole
+// LDS (the dynamic part beyond the mel weights is padding): no workgroup of
+// another kernel can share its CU.  Measured on MI355X (tools/fe_race.cpp):
+// this FFT, sharing a CU with MFMA (or other heavy) waves of a kernel on
+// another stream, intermittently produced wrong spectra (11 of 32 launches);
+// CU-exclusive, 0 of 64.  MFMA kernels are padded the same way
+// (mfma_cu_exclusive_lds).
+constexpr int FE_WAVES = 16;
+constexpr int LDS_PER_CU = 160 * 1024;
 
 template <int NFFT, bool I16>
-__global__ __launch_bounds__(256, 8) void logmel_kernel(FrontendParams p) {
+__global__ __launch_bounds__(64 * FE_WAVES) void logmel_kernel(FrontendParams p) {
   constexpr int N2 = NFFT / 2;
   constexpr int NS = NFFT / 64;          // samples per lane per frame
   __shared__ float2 s_tw[NFFT];
   __shared__ float s_win[NFFT];
-  __shared__ float2 s_buf[4][2][N2];
-  extern __shared__ float s_melw[];      // [nnz] when nnz <= MEL_LDS_CAP (launch sizes it)
+  __shared__ float2 s_buf[FE_WAVES][2][N2];
+  extern __shared__ float s_melw[];      // [p.mel_lds_floats]: packed mel weights, then padding
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int nnz = p.mel_off[64];
-  const bool mel_in_lds = nnz <= MEL_LDS_CAP;
-  for (int i = threadIdx.x; i < NFFT; i += 256) {
+  const bool mel_in_lds = nnz <= p.mel_lds_floats;
+  for (int i = threadIdx.x; i < NFFT; i += 64 * FE_WAVES) {
     s_tw[i] = p.twiddle[i];
     s_win[i] = p.window[i];
   }
   if (mel_in_lds)
-    for (int i = threadIdx.x; i < nnz; i += 256) s_melw[i] = p.mel_w[i];
+    for (int i = threadIdx.x; i < nnz; i += 64 * FE_WAVES) s_melw[i] = p.mel_w[i];
   const int m = lane;                    // mel band of this lane
   const int mlo = p.mel_lo[m], o0 = p.mel_off[m], o1 = p.mel_off[m + 1];
   const float bmu = p.bn_mean[m], bsc = p.bn_scale[m], bbi = p.bn_bias[m];
@@ -158,8 +167,8 @@ __global__ __launch_bounds__(256, 8) void logmel_kernel(FrontendParams p) {
           v[2 * i + e] = ok ? p.audio[src_off + jc] : 0.0f;
       }
   };
-  int64_t fr = (int64_t)blockIdx.x * 4 + wave;
-  const int64_t fstride = (int64_t)gridDim.x * 4;
+  int64_t fr = (int64_t)blockIdx.x * FE_WAVES + wave;
+  const int64_t fstride = (int64_t)gridDim.x * FE_WAVES;
   float v[NS];
   if (fr < total) load(fr, v);
   for (; fr < total; fr += fstride) {
@@ -210,26 +219,29 @@ __global__ __launch_bounds__(256, 8) void logmel_kernel(FrontendParams p) {
   }
 }
 
-// persistent-style grid: every resident wave walks several frames, so the
+// one CU-exclusive workgroup per CU; every wave walks several frames, so the
 // register prefetch of the next frame overlaps the current FFT
 template <int NFFT, bool I16>
-static void launch_logmel_t(const FrontendParams& p, int64_t total, hipStream_t s) {
-  // dynamic LDS = the packed mel weights (host copy of mel_off[64] kept in p)
-  const size_t dyn = p.mel_nnz <= MEL_LDS_CAP ? (size_t)p.mel_nnz * 4 : 0;
-  static int resident = 0;
-  static size_t resident_dyn = ~size_t(0);
-  if (resident_dyn != dyn) {
-    int dev = 0, ncu = 0, per_cu = 0;
+static void launch_logmel_t(const FrontendParams& p0, int64_t total, hipStream_t s) {
+  static size_t dyn = 0;
+  static int ncu = 0;
+  if (!ncu) {
+    hipFuncAttributes fa{};
+    (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(logmel_kernel<NFFT, I16>));
+    dyn = (LDS_PER_CU - fa.sharedSizeBytes) & ~size_t(511);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(logmel_kernel<NFFT, I16>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
+    int dev = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, logmel_kernel<NFFT, I16>, 256, dyn);
-    resident = (ncu > 0 ? ncu : 256) * (per_cu > 0 ? per_cu : 1);
-    resident_dyn = dyn;
+    if (ncu <= 0) ncu = 256;
   }
-  int64_t blocks = (total + 3) / 4;
-  if (blocks > resident) blocks = resident;
+  FrontendParams p = p0;
+  p.mel_lds_floats = (int32_t)(dyn / 4);
+  int64_t blocks = (total + FE_WAVES - 1) / FE_WAVES;
+  if (blocks > ncu) blocks = ncu;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL((logmel_kernel<NFFT, I16>), dim3((unsigned)blocks), dim3(256), dyn, s, p);
+  hipLaunchKernelGGL((logmel_kernel<NFFT, I16>), dim3((unsigned)blocks), dim3(64 * FE_WAVES), dyn, s, p);
 }
 
 void launch_logmel(const FrontendParams& p, int n_fft, hipStream_t s) {
@@ -392,12 +404,17 @@ void launch_gamma(const GammaParams& p, hipStream_t s) {
   const int64_t total = (int64_t)p.B * p.T;
   int64_t blocks = (total + 1) / 2;
   if (blocks > 4096) blocks = 4096;
+  // the same in-LDS FFT as the logmel frontend: CU-exclusive LDS footprint
+  // (mfma_cu_exclusive_lds keeps the kernel's own workgroups per CU)
+  auto go = [&](const void* k, auto kern) {
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), mfma_cu_exclusive_lds(k, 256), s, p, mm);
+  };
   if (p.nfft == 2048)
-    hipLaunchKernelGGL(gamma_frames_kernel<2048>, dim3(blocks), dim3(256), 0, s, p, mm);
+    go(reinterpret_cast<const void*>(gamma_frames_kernel<2048>), gamma_frames_kernel<2048>);
   else if (p.nfft == 1024)
-    hipLaunchKernelGGL(gamma_frames_kernel<1024>, dim3(blocks), dim3(256), 0, s, p, mm);
+    go(reinterpret_cast<const void*>(gamma_frames_kernel<1024>), gamma_frames_kernel<1024>);
   else if (p.nfft == 512)
-    hipLaunchKernelGGL(gamma_frames_kernel<512>, dim3(blocks), dim3(256), 0, s, p, mm);
+    go(reinterpret_cast<const void*>(gamma_frames_kernel<512>), gamma_frames_kernel<512>);
   hipLaunchKernelGGL(gamma_quant_kernel, dim3(2048), dim3(256), 0, s, p, mm);
 }
 

@@ -318,7 +318,9 @@ void launch_gru_coop(const float* G, int B, int T, const float* whh, const float
   float* X = reinterpret_cast<float*>(static_cast<char*>(ws) + ((sizeof(GruSync) + 255) & ~size_t(255)));
   const int allow_fast = getenv("SEDX_GRU_GLOBAL_ONLY") ? 0 : 1;   // A/B switch
   (void)hipMemsetAsync(sync, 0, sizeof(GruSync), s);
-  hipLaunchKernelGGL(gru_coop_kernel, dim3(64), dim3(768), 0, s, G, B, T, whh, bhh, H, X, sync,
+  hipLaunchKernelGGL(gru_coop_kernel, dim3(64), dim3(768),
+                     mfma_cu_exclusive_lds(reinterpret_cast<const void*>(gru_coop_kernel), 768), s, G, B, T,
+                     whh, bhh, H, X, sync,
                      nslots, allow_fast);
 }
 

@@ -6,6 +6,11 @@
 //   seq       [items][T4][512]                 CNN output after freq-mean (GRU/MHA input)
 #pragma once
 #include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <map>
+#include <mutex>
 #include <stdint.h>
 
 namespace sedx {
@@ -27,7 +32,7 @@ struct FrontendParams {
   const float* mel_w;       // packed band weights
   const int32_t* mel_off;   // [65] offsets into mel_w
   const int32_t* mel_lo;    // [64] first fft bin of each band
-  int32_t mel_nnz;          // host copy of mel_off[64] (sizes the LDS copy of mel_w)
+  int32_t mel_lds_floats;   // set by launch_logmel: LDS room for the packed mel weights
   const float* bn_scale;    // [64] bn0 folded
   const float* bn_mean;     // [64]
   const float* bn_bias;     // [64]
@@ -70,13 +75,46 @@ void launch_conv3x3(const float* in, int B, int T, int F, int Cin, int Cout,
 // Same contract on bf16 MFMA with a 3-term hi/lo split (fp32-class accuracy).
 // wp = host-packed split weights [Cout/BN][Cin/16][9][BN][4 x 16 B] (BN = 64 if
 // Cout == 64 else 128), slots XOR-swizzled by ((n >> 2) & 3).
+// MFMA kernels are launched with a dynamic-LDS pad that makes their
+// workgroups fill a CU's LDS (LDS per CU / the kernel's own workgroups per
+// CU): no workgroup of another kernel can then share a CU with MFMA waves.
+// Measured on MI355X (tools/fe_race.cpp, tools/mfma_corun.cpp, DESIGN.md
+// "Concurrent streams"): a frontend workgroup sharing a CU with MFMA waves of
+// another kernel (another stream) intermittently produced wrong FFT results;
+// with the pad, 0 of 128 runs differ.  Same-kernel sharing is unaffected.
+// Returns the pad in bytes (cached per kernel; thread-safe).
+inline size_t mfma_cu_exclusive_lds(const void* kernel, int block_threads) {
+  static std::mutex mu;
+  static std::map<const void*, size_t> cache;
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = cache.find(kernel);
+  if (it != cache.end()) return it->second;
+  constexpr int lds_cu = 160 * 1024;   // gfx950 LDS per CU (the device attribute reports 64 KB)
+  int per_cu = 0;
+  hipFuncAttributes fa{};
+  (void)hipFuncGetAttributes(&fa, kernel);
+  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block_threads, 0);
+  if (per_cu < 1) per_cu = 1;
+  const size_t per_wg = ((size_t)lds_cu / (size_t)per_cu) & ~size_t(511);
+  size_t pad = per_wg > fa.sharedSizeBytes ? per_wg - fa.sharedSizeBytes : 0;
+  if (pad && hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pad) != hipSuccess)
+    pad = 0;
+  cache[kernel] = pad;
+  if (getenv("SEDX_DEBUG_LDS"))
+    fprintf(stderr, "sedx: kernel %p static LDS %zu B, %d workgroups/CU -> pad %zu B\n", kernel,
+            (size_t)fa.sharedSizeBytes, per_cu, pad);
+  return pad;
+}
+
+// sched: CONV_SCHED_INTS zeroed ints per launch (the 8 per-XCD tile-claim counters)
+constexpr int CONV_SCHED_INTS = 256;
 void launch_conv3x3_x3(const float* in, int B, int T, int F, int Cin, int Cout, const void* wp,
-                       const float* bias, float* out, int epi, hipStream_t s);
+                       const float* bias, float* out, int epi, int* sched, hipStream_t s);
 // block 1 of the CNN in one conv launch (x3): with x0, pads the bn0 output
 // into xpad (block1_pad_floats(B, T) floats); with out, runs conv2 with conv1
 // computed while its halo is staged (conv_x3.hip)
 void launch_block1_fused_x3(const float* x0, int B, int T, float* xpad, const float* w1, const float* b1,
-                            const void* wp, const float* bias, float* out, hipStream_t s);
+                            const void* wp, const float* bias, float* out, int* sched, hipStream_t s);
 size_t block1_pad_floats(int B, int T);
 
 // ---- sequence / head ------------------------------------------------------

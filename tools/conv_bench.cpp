@@ -28,6 +28,8 @@ int main(int argc, char** argv) {
   }
   float *in, *out, *bias;
   void* w;
+  int* sched;   // per-launch tile-claim counters (zeroed before every launch)
+  hipMalloc(&sched, 256 * 4 * 64);
   hipMalloc(&in, max_in * 4); hipMalloc(&out, max_in * 4); hipMalloc(&bias, 512 * 4); hipMalloc(&w, max_w);
   {
     std::vector<float> h(max_in);
@@ -43,14 +45,17 @@ int main(int argc, char** argv) {
   hipEventCreate(&e0); hipEventCreate(&e1);
   double tot_ms = 0, tot_f = 0;
   for (const Layer& l : L) {
-    sedx::launch_conv3x3_x3(in, B, l.T, l.F, l.cin, l.cout, w, bias, out, l.epi, 0);
+    hipMemsetAsync(sched, 0, 256 * 4, 0);
+    sedx::launch_conv3x3_x3(in, B, l.T, l.F, l.cin, l.cout, w, bias, out, l.epi, sched, 0);
     hipDeviceSynchronize();
+    hipMemsetAsync(sched, 0, 256 * 4 * 64, 0);
 #ifdef SEDX_CONV_STAMPS
     unsigned long long st[8];
     sedx::conv_stamps_rw(st, true);
 #endif
     hipEventRecord(e0, 0);
-    for (int r = 0; r < reps; ++r) sedx::launch_conv3x3_x3(in, B, l.T, l.F, l.cin, l.cout, w, bias, out, l.epi, 0);
+    for (int r = 0; r < reps; ++r)   // reps <= 64: one counter block per launch, zeroed up front
+      sedx::launch_conv3x3_x3(in, B, l.T, l.F, l.cin, l.cout, w, bias, out, l.epi, sched + 256 * (r & 63), 0);
     hipEventRecord(e1, 0);
     hipEventSynchronize(e1);
     float ms = 0;

@@ -1,0 +1,306 @@
+// Diagnostic: is the logmel frontend bit-deterministic while another
+// kernel runs on a second stream?  mode 0: linear_x3 on stream 1; mode 1:
+// conv3x3_x3 on stream 1; mode 2: logmel on both streams.  Every logmel
+// output is compared bit for bit with a serial reference.
+#include <hip/hip_runtime.h>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+#include "../sound-event-detection_amd/csrc/sedx_internal.h"
+
+// synthetic co-runners (mode 3: MFMA only, 72 KB LDS declared; mode 4: LDS
+// b128 traffic inside 72 KB, no MFMA; mode 5: VALU only)
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+__global__ __launch_bounds__(256) void mfma_spin(float* out, int iters) {
+  __shared__ uint4 big[4608];
+  bf16x8 a, b;
+  for (int i = 0; i < 8; ++i) { a[i] = (__bf16)(threadIdx.x * 0.001f + i); b[i] = (__bf16)(0.5f - i * 0.01f); }
+  f32x16 acc = {};
+  for (int it = 0; it < iters; ++it) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
+  if (threadIdx.x == 0 && acc[0] == 12345.f) big[0] = make_uint4(1, 2, 3, 4);
+  __syncthreads();
+  if (acc[3] == -1.f) out[blockIdx.x] = acc[0] + (float)big[threadIdx.x].x;
+}
+__global__ __launch_bounds__(256) void lds_spin(float* out, int iters) {
+  __shared__ uint4 big[4608];
+  uint4 v = make_uint4(threadIdx.x, 1, 2, 3);
+  for (int it = 0; it < iters; ++it) {
+    big[(threadIdx.x + it * 256) % 4608] = v;
+    __syncthreads();
+    v = big[(threadIdx.x * 7 + it) % 4608];
+    v.x += 1;
+  }
+  if (v.x == 0xdeadbeef) out[blockIdx.x] = (float)v.y;
+}
+__global__ __launch_bounds__(256) void valu_spin(float* out, int iters) {
+  float x = threadIdx.x * 1e-3f;
+  for (int it = 0; it < iters; ++it) x = fmaf(x, 0.999f, 1e-4f);
+  if (x == 12345.f) out[blockIdx.x] = x;
+}
+
+// Variants of the frontend kernel for bisection (same structure as
+// csrc/frontend.hip logmel_kernel<512, false>):
+//   V0 copy, V1 synthetic input (no audio/window loads), V2 output power bins,
+//   V3 output raw FFT bins, V4 output the windowed input
+__device__ __forceinline__ float2 cmul_(float2 a, float2 b) {
+  return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__device__ __forceinline__ float2 cadd_(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 csub_(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+template <int V>
+__global__ __launch_bounds__(256) void lm_variant(sedx::FrontendParams p) {
+  constexpr int NFFT = 512, N2 = 256;
+  __shared__ float2 s_tw[NFFT];
+  __shared__ float2 s_buf[4][2][N2];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  for (int i = threadIdx.x; i < NFFT; i += 256) s_tw[i] = p.twiddle[i];
+  __syncthreads();
+  const int64_t total = (int64_t)p.n_clips * p.T;
+  const int64_t L = p.sig_len;
+  for (int64_t f0 = (int64_t)blockIdx.x * 4; f0 < total; f0 += (int64_t)gridDim.x * 4) {
+    const int64_t fr = f0 + wave;
+    const bool valid = fr < total;
+    float2* X = s_buf[wave][0];
+    float2* Y = s_buf[wave][1];
+    if (valid) {
+      const int64_t item = fr / p.T;
+      const int t = (int)(fr - item * p.T);
+      const float* src = p.audio + item * p.clip_stride;
+      const int64_t pos0 = (int64_t)t * p.hop - N2;
+      for (int m = lane; m < N2; m += 64) {
+        float v[2];
+        for (int e = 0; e < 2; ++e) {
+          int64_t j = pos0 + 2 * m + e;
+          if (j < 0) j = -j;
+          if (j >= L) j = 2 * (L - 1) - j;
+          if (V == 1) v[e] = (float)((fr * 7 + 2 * m + e) % 97) * 0.01f;
+          else v[e] = src[j] * p.window[2 * m + e];
+        }
+        X[m] = make_float2(v[0], v[1]);
+      }
+    }
+    __syncthreads();
+    if (V == 4) {
+      if (valid) p.out[fr * 64 + lane] = X[lane].x + X[lane + 64].y;
+      __syncthreads();
+      continue;
+    }
+    int Ns = 1;
+    float2* A = X;
+    float2* Bf = Y;
+    for (int stage = 0; stage < 4; ++stage) {
+      const int nb = 64;
+      const int j = lane;
+      const int k = j & (Ns - 1);
+      float2 v0 = A[j], v1 = A[j + nb], v2 = A[j + 2 * nb], v3 = A[j + 3 * nb];
+      const int step = NFFT / (Ns * 4);
+      if (Ns > 1) {
+        v1 = cmul_(v1, s_tw[k * step]);
+        v2 = cmul_(v2, s_tw[2 * k * step]);
+        v3 = cmul_(v3, s_tw[3 * k * step]);
+      }
+      const float2 a0 = cadd_(v0, v2), a1 = csub_(v0, v2);
+      const float2 b0 = cadd_(v1, v3), b1 = csub_(v1, v3);
+      const float2 mib1 = make_float2(b1.y, -b1.x);
+      const int base = (j - k) * 4 + k;
+      Bf[base] = cadd_(a0, b0);
+      Bf[base + Ns] = cadd_(a1, mib1);
+      Bf[base + 2 * Ns] = csub_(a0, b0);
+      Bf[base + 3 * Ns] = csub_(a1, mib1);
+      __syncthreads();
+      float2* tt = A; A = Bf; Bf = tt;
+      Ns *= 4;
+    }
+    float2* Z = A;
+    if (V == 3) {
+      if (valid) p.out[fr * 64 + lane] = Z[lane].x + Z[lane + 128].y;
+      __syncthreads();
+      continue;
+    }
+    float* P = reinterpret_cast<float*>(Bf);
+    if (valid) {
+      for (int k = lane; k <= N2; k += 64) {
+        const float2 Aa = Z[k & (N2 - 1)];
+        const float2 Bz = Z[(N2 - k) & (N2 - 1)];
+        const float2 Bc = make_float2(Bz.x, -Bz.y);
+        const float2 E = make_float2(0.5f * (Aa.x + Bc.x), 0.5f * (Aa.y + Bc.y));
+        const float2 O = make_float2(0.5f * (Aa.y - Bc.y), -0.5f * (Aa.x - Bc.x));
+        const float2 Xk = cadd_(E, cmul_(s_tw[k], O));
+        P[k] = Xk.x * Xk.x + Xk.y * Xk.y;
+      }
+    }
+    __syncthreads();
+    if (valid) {
+      if (V == 2) {
+        p.out[fr * 64 + lane] = P[lane] + P[lane + 64] + P[lane + 128];
+      } else {
+        const int m = lane;
+        const int lo = p.mel_lo[m];
+        const int o0 = p.mel_off[m], o1 = p.mel_off[m + 1];
+        float acc = 0.0f;
+        for (int i = o0; i < o1; ++i) acc = fmaf(P[lo + (i - o0)], p.mel_w[i], acc);
+        float db = 10.0f * log10f(fmaxf(acc, 1e-10f));
+        db = (db - p.bn_mean[m]) * p.bn_scale[m] + p.bn_bias[m];
+        p.out[fr * 64 + m] = db;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+static size_t g_pad = 0;   // FE_PAD=1: unused dynamic LDS so that no other workgroup shares the CU
+static void launch_variant(int V, const sedx::FrontendParams& p, hipStream_t s) {
+  const int64_t total = (int64_t)p.n_clips * p.T;
+  int64_t blocks = (total + 3) / 4;
+  if (blocks > 8192) blocks = 8192;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(lm_variant<0>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                        163840 - 20480);
+    attr = true;
+    g_pad = getenv("FE_PAD") ? (size_t)(163840 - 20480) : 0;
+  }
+  switch (V) {
+    case 0: hipLaunchKernelGGL(lm_variant<0>, dim3(blocks), dim3(256), g_pad, s, p); break;
+    case 1: hipLaunchKernelGGL(lm_variant<1>, dim3(blocks), dim3(256), 0, s, p); break;
+    case 2: hipLaunchKernelGGL(lm_variant<2>, dim3(blocks), dim3(256), 0, s, p); break;
+    case 3: hipLaunchKernelGGL(lm_variant<3>, dim3(blocks), dim3(256), 0, s, p); break;
+    case 4: hipLaunchKernelGGL(lm_variant<4>, dim3(blocks), dim3(256), 0, s, p); break;
+  }
+}
+
+int main(int argc, char** argv) {
+  int mode = argc > 1 ? atoi(argv[1]) : 0;
+  const int variant = mode >= 10 ? mode - 10 : -1;
+  if (variant >= 0) mode = 3;
+  auto run_fe = [&](const sedx::FrontendParams& pp, hipStream_t s) {
+    if (variant >= 0) launch_variant(variant, pp, s);
+    else sedx::launch_logmel(pp, 512, s);
+  };
+  const int R = argc > 2 ? atoi(argv[2]) : 20;
+  const int B = 32, L = 160000, NFFT = 512, hop = 160, T = L / hop + 1;
+  hipStream_t st[2];
+  hipStreamCreateWithFlags(&st[0], hipStreamNonBlocking);
+  hipStreamCreateWithFlags(&st[1], hipStreamNonBlocking);
+  // frontend tables
+  std::vector<float> tw(2 * NFFT), win(NFFT), melw(64 * 8), bns(64), bnm(64), bnb(64);
+  std::vector<int32_t> moff(65), mlo(64);
+  for (int m = 0; m < NFFT; ++m) {
+    tw[2 * m] = (float)cos(-2.0 * M_PI * m / NFFT);
+    tw[2 * m + 1] = (float)sin(-2.0 * M_PI * m / NFFT);
+    win[m] = (float)(0.5 - 0.5 * cos(2.0 * M_PI * m / NFFT));
+  }
+  for (int m = 0; m < 64; ++m) {
+    moff[m] = 8 * m;
+    mlo[m] = 2 * m;
+    for (int i = 0; i < 8; ++i) melw[8 * m + i] = 0.05f + 0.01f * i;
+    bns[m] = 0.05f; bnm[m] = -40.f; bnb[m] = 0.1f;
+  }
+  moff[64] = 512;
+  std::vector<float> audio((size_t)B * L);
+  srand(3);
+  for (auto& v : audio) v = (rand() / (float)RAND_MAX - 0.5f) * 0.2f;
+  auto up = [](const void* h, size_t n) { void* d; hipMalloc(&d, n); hipMemcpy(d, h, n, hipMemcpyHostToDevice); return d; };
+  float* d_audio = (float*)up(audio.data(), audio.size() * 4);
+  sedx::FrontendParams p{};
+  p.audio = d_audio;
+  p.clip_stride = L; p.n_clips = B; p.n_win = 1; p.win_start[0] = 0; p.clip_len = L; p.sig_len = L;
+  p.T = T; p.hop = hop;
+  p.twiddle = (const float2*)up(tw.data(), tw.size() * 4);
+  p.window = (const float*)up(win.data(), win.size() * 4);
+  p.mel_w = (const float*)up(melw.data(), melw.size() * 4);
+  p.mel_off = (const int32_t*)up(moff.data(), moff.size() * 4);
+  p.mel_lo = (const int32_t*)up(mlo.data(), mlo.size() * 4);
+  p.bn_scale = (const float*)up(bns.data(), 256); p.bn_mean = (const float*)up(bnm.data(), 256);
+  p.bn_bias = (const float*)up(bnb.data(), 256);
+  const size_t nout = (size_t)B * T * 64;
+  constexpr int NL = 8;
+  float* outs[NL];
+  for (int i = 0; i < NL; ++i) hipMalloc(&outs[i], nout * 4);
+  p.out = outs[0];
+  run_fe(p, 0);
+  hipDeviceSynchronize();
+  std::vector<float> ref(nout), got(nout);
+  hipMemcpy(ref.data(), outs[0], nout * 4, hipMemcpyDeviceToHost);
+  // the other stream's work
+  const int M = B * 125, K = 512, N = 1536;
+  float *A, *C, *bias;
+  void* W;
+  hipMalloc(&A, (size_t)M * K * 4); hipMemset(A, 0, (size_t)M * K * 4);
+  hipMalloc(&C, (size_t)M * N * 4);
+  hipMalloc(&bias, N * 4); hipMemset(bias, 0, N * 4);
+  hipMalloc(&W, (size_t)N * K * 4); hipMemset(W, 0, (size_t)N * K * 4);
+  float *cin, *cout;
+  hipMalloc(&cin, (size_t)B * 500 * 32 * 128 * 4); hipMemset(cin, 0, (size_t)B * 500 * 32 * 128 * 4);
+  hipMalloc(&cout, (size_t)B * 500 * 32 * 128 * 4);
+  int* sched;
+  hipMalloc(&sched, 64 * 256 * 4);
+  int bad = 0;
+  for (int r = 0; r < R; ++r) {
+    for (int i = 0; i < NL; ++i) hipMemset(outs[i], 0xff, nout * 4);
+    hipMemset(sched, 0, 64 * 256 * 4);
+    hipDeviceSynchronize();
+    for (int k = 0; k < NL; ++k) {
+      p.out = outs[k];
+      run_fe(p, st[0]);
+      for (int j = 0; j < 4; ++j) {
+        if (mode == 0) sedx::launch_linear_x3(A, M, K, W, N, 128, bias, C, 0, st[1]);
+        else if (mode == 3) {
+          static size_t spad = 0;
+          static bool sattr = false;
+          if (!sattr) {
+            hipFuncSetAttribute(reinterpret_cast<const void*>(mfma_spin), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                163840 - 73728);
+            spad = getenv("SPIN_PAD") ? (size_t)(163840 - 73728) : 0;
+            sattr = true;
+          }
+          hipLaunchKernelGGL(mfma_spin, dim3(512), dim3(256), spad, st[1], C, 4000);
+        }
+        else if (mode == 4) hipLaunchKernelGGL(lds_spin, dim3(512), dim3(256), 0, st[1], C, 2000);
+        else if (mode == 5) hipLaunchKernelGGL(valu_spin, dim3(512), dim3(256), 0, st[1], C, 20000);
+        else if (mode == 1)
+          sedx::launch_conv3x3_x3(cin, B, 500, 32, 128, 128, W, bias, cout, sedx::EPI_POOL2,
+                                  sched + 256 * ((k * 4 + j) & 63), st[1]);
+      }
+      if (mode == 2) { p.out = outs[(k + 1) % NL]; }
+    }
+    if (mode == 2)
+      for (int k = 0; k < NL; ++k) { p.out = outs[k]; sedx::launch_logmel(p, NFFT, st[k & 1]); }
+    hipDeviceSynchronize();
+    for (int i = 0; i < NL; ++i) {
+      hipMemcpy(got.data(), outs[i], nout * 4, hipMemcpyDeviceToHost);
+      size_t nd = 0, first = 0;
+      for (size_t j = 0; j < nout; ++j)
+        if (memcmp(&got[j], &ref[j], 4) != 0) { if (!nd) first = j; ++nd; }
+      if (nd) {
+        ++bad;
+        printf("  round %d out %d: %zu differ (first frame %zu mel %zu)\n", r, i, nd, first / 64, first % 64);
+        if (bad <= 3) {
+          int shown = 0;
+          for (size_t f = 0; f < nout / 64 && shown < 4; ++f) {
+            char mask[65];
+            int any = 0;
+            for (int m = 0; m < 64; ++m) {
+              const bool d = memcmp(&got[f * 64 + m], &ref[f * 64 + m], 4) != 0;
+              mask[m] = d ? 'x' : '.';
+              any |= d;
+            }
+            mask[64] = 0;
+            if (any) {
+              printf("    frame %6zu (wave slot %zu) %s  got[0] %.5g ref[0] %.5g\n", f, f % 4, mask, got[f * 64],
+                     ref[f * 64]);
+              ++shown;
+            }
+          }
+        }
+      }
+    }
+  }
+  printf("mode %d variant %d: %d of %d logmel outputs differ (%s)\n", mode, variant, bad, NL * R, hipGetErrorString(hipGetLastError()));
+  (void)variant;
+  return 0;
+}
