@@ -151,7 +151,7 @@ def stage_times(model, wave, dev, reps):
 # command (tools/profile_round.sh -> tools/pmc_summary.py; FETCH_SIZE x2 per
 # the gfx950 correction + WRITE_SIZE), committed under profiles/.
 PROFILE_SUMMARY = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles',
-                               'r01d_kernel_summary.json')
+                               'r01e_kernel_summary.json')
 STAGE_KERNEL = {'b1c2': '<64, 64, 1', 'b2c1': '<32, 128, 0', 'b2c2': '<32, 128, 1',
                 'b3c1': '<16, 128, 0', 'b3c2': '<16, 128, 1', 'b4c1': '<8, 128, 0',
                 'b4c2': '<8, 128, 2'}
@@ -159,13 +159,16 @@ STAGE_KERNEL = {'b1c2': '<64, 64, 1', 'b2c1': '<32, 128, 0', 'b2c2': '<32, 128, 
 STAGE_FUSE = {'b1c2': 'true'}
 
 
-def profiled_traffic(kernel):
+def profiled(kernel):
+    """(HBM bytes per launch, rocprofv3 average duration in ms) of ``kernel``
+    from the committed profile summary (None where absent)."""
     try:
         with open(PROFILE_SUMMARY) as f:
             v = json.load(f).get(kernel, {})
-        return v.get('hbm_bytes_corrected')
+        ns = v.get('avg_ns')
+        return v.get('hbm_bytes_corrected'), (round(ns * 1e-6, 4) if ns else None)
     except (OSError, ValueError):
-        return None
+        return None, None
 
 
 def roofline(stage_ms, B, precision):
@@ -173,6 +176,10 @@ def roofline(stage_ms, B, precision):
     conv = {s: stage_ms[s] for s in CONV_STAGES}
     dom = max(conv, key=conv.get)
     flops = conv_flops(dom, B, T)
+    if precision == 'x3' and dom == 'b1c2':
+        # the fused block-1 launch also computes conv1 (Cin 1 -> 64, 9 taps) for
+        # every conv2 input pixel it stages: 2 * B * T * 64 * 64 * 9 flops
+        flops += 2.0 * B * T * 64 * 64 * 9
     achieved = flops / (conv[dom] * 1e-3) / 1e12
     peak = PEAK_TF[precision]
     total = sum(conv_flops(s, B, T) for s in CONV_STAGES)
@@ -180,7 +187,7 @@ def roofline(stage_ms, B, precision):
         kname = 'sedx::conv3x3_x3_kernel%s, %s>' % (STAGE_KERNEL[dom], STAGE_FUSE.get(dom, 'false'))
     else:
         kname = 'sedx::conv3x3_kernel%s>' % STAGE_KERNEL[dom]
-    traffic = profiled_traffic(kname) if B == 32 else None
+    traffic, rocprof_ms = profiled(kname) if B == 32 else (None, None)
     return {'bound': 'mfma',
             'kernel': 'conv3x3_%s (%s)' % ('x3_kernel' if precision == 'x3' else 'kernel', dom),
             'arith': '3xbf16-split MFMA 32x32x16, fp32 acc (peak = bf16 dense 2.5 PF / 3)'
@@ -191,6 +198,10 @@ def roofline(stage_ms, B, precision):
             'traffic_source': os.path.relpath(PROFILE_SUMMARY, os.path.dirname(os.path.abspath(__file__)))
             if traffic is not None else None,
             'flops_per_launch': flops, 'avg_launch_ms': conv[dom],
+            'avg_launch_ms_rocprof': rocprof_ms,
+            'timing': 'avg_launch_ms: HIP events on the launch stream (one batch at a time); '
+                      'avg_launch_ms_rocprof: rocprofv3 --kernel-trace --stats of this bench '
+                      '(--streams 1 --no-side), committed summary',
             'conv_stack_tflops': round(total / (sum(conv.values()) * 1e-3) / 1e12, 2)}
 
 
