@@ -217,6 +217,39 @@ sedx_status sedx_events_device(const float* d_x, int64_t n_clips, int64_t T, int
                                int32_t* d_events, int64_t capacity, int64_t* d_info,
                                void* d_workspace, size_t workspace_bytes, void* stream);
 
+/* ------------------------------------------------------------------------
+ * Input side: librosa.core.load(path, sr, mono=True) as
+ * pytorch/predict.py:295 and pytorch/main_strong.py:787 call it
+ * (librosa 0.8: soundfile read -> to_mono -> resample(res_type='kaiser_best')
+ * -> fix_length).  Handle-free; asynchronous on `stream`.
+ * ------------------------------------------------------------------------ */
+typedef enum { SEDX_WAV_PCM = 1, SEDX_WAV_FLOAT = 3 } sedx_wav_format;
+typedef struct {
+  int32_t format;           /* sedx_wav_format */
+  int32_t channels;
+  int32_t sample_rate;
+  int32_t bits_per_sample;  /* PCM 8/16/24/32, float 32/64 */
+  int64_t frames;
+  int64_t data_offset;      /* byte offset of the interleaved samples in the file */
+  int64_t data_bytes;
+} sedx_wav_info;
+/* Parse a RIFF/WAVE file image in host memory (PCM or IEEE float, including
+ * WAVE_FORMAT_EXTENSIBLE).  SEDX_EINVAL for anything else. */
+sedx_status sedx_wav_parse(const void* h_bytes, size_t n_bytes, sedx_wav_info* info);
+/* Interleaved samples (a device copy of the data chunk) -> mono float32
+ * d_out [frames]: libsndfile's float scaling, then the mean over channels
+ * (librosa.to_mono on the float32 array). */
+sedx_status sedx_wav_decode_mono(const void* d_data, const sedx_wav_info* info, float* d_out, void* stream);
+typedef enum { SEDX_RESAMPLE_KAISER_BEST = 0, SEDX_RESAMPLE_KAISER_FAST = 1 } sedx_resample_quality;
+/* librosa.resample(y, sr_in, sr_out, res_type) length: ceil(n_in * sr_out / sr_in). */
+sedx_status sedx_resample_size(int64_t n_in, int32_t sr_in, int32_t sr_out, int64_t* n_out);
+sedx_status sedx_resample_workspace_size(int64_t n_in, int32_t sr_in, int32_t sr_out, int32_t quality,
+                                         size_t* bytes);
+/* resampy band-limited interpolation (restated; resampy is not in the
+ * reference) + librosa fix_length; a device copy when sr_in == sr_out. */
+sedx_status sedx_resample(const float* d_in, int64_t n_in, int32_t sr_in, int32_t sr_out, int32_t quality,
+                          float* d_out, void* d_workspace, size_t workspace_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -21,9 +21,20 @@ EXPORTS = ['sedx_create', 'sedx_destroy', 'sedx_last_error', 'sedx_version', 'se
            'sedx_window_geometry', 'sedx_forward_windows', 'sedx_window_workspace_size',
            'sedx_events', 'sedx_set_profiling', 'sedx_stage_times', 'sedx_set_precision',
            'sedx_forward_windows_vote', 'sedx_events_workspace_size', 'sedx_events_device',
-           'sedx_forward_i16']
+           'sedx_forward_i16', 'sedx_wav_parse', 'sedx_wav_decode_mono', 'sedx_resample_size',
+           'sedx_resample_workspace_size', 'sedx_resample']
 PRECISION = {'exact': 0, 'x3': 1}
 STAGES = ['frontend', 'b1c1', 'b1c2', 'b2c1', 'b2c2', 'b3c1', 'b3c2', 'b4c1', 'b4c2', 'seq', 'head']
+
+
+class SedxWavInfo(ctypes.Structure):
+    _fields_ = [('format', ctypes.c_int32), ('channels', ctypes.c_int32),
+                ('sample_rate', ctypes.c_int32), ('bits_per_sample', ctypes.c_int32),
+                ('frames', ctypes.c_int64), ('data_offset', ctypes.c_int64),
+                ('data_bytes', ctypes.c_int64)]
+
+
+RESAMPLE = {'kaiser_best': 0, 'kaiser_fast': 1}
 
 
 class SedxConfig(ctypes.Structure):
@@ -78,6 +89,11 @@ def lib():
         'sedx_set_profiling': ([P, I32], I32),
         'sedx_set_precision': ([P, I32], I32),
         'sedx_stage_times': ([P, ctypes.POINTER(ctypes.c_float), I32, ctypes.POINTER(I32)], I32),
+        'sedx_wav_parse': ([P, SZ, ctypes.POINTER(SedxWavInfo)], I32),
+        'sedx_wav_decode_mono': ([P, ctypes.POINTER(SedxWavInfo), P, P], I32),
+        'sedx_resample_size': ([I64, I32, I32, PI64], I32),
+        'sedx_resample_workspace_size': ([I64, I32, I32, I32, PSZ], I32),
+        'sedx_resample': ([P, I64, I32, I32, I32, P, P, SZ, P], I32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
