@@ -160,15 +160,18 @@ STAGE_FUSE = {'b1c2': 'true'}
 
 
 def profiled(kernel):
-    """(HBM bytes per launch, rocprofv3 average duration in ms) of ``kernel``
-    from the committed profile summary (None where absent)."""
+    """(HBM bytes per launch, rocprofv3 average duration in ms, MFMA busy
+    fraction, effective clock GHz) of ``kernel`` from the committed profile
+    summary (None where absent)."""
     try:
         with open(PROFILE_SUMMARY) as f:
             v = json.load(f).get(kernel, {})
         ns = v.get('avg_ns')
-        return v.get('hbm_bytes_corrected'), (round(ns * 1e-6, 4) if ns else None)
+        util, clk = v.get('mfma_util'), v.get('clock_ghz')
+        return (v.get('hbm_bytes_corrected'), (round(ns * 1e-6, 4) if ns else None),
+                round(util, 4) if util else None, round(clk, 3) if clk else None)
     except (OSError, ValueError):
-        return None, None
+        return None, None, None, None
 
 
 def roofline(stage_ms, B, precision):
@@ -187,7 +190,7 @@ def roofline(stage_ms, B, precision):
         kname = 'sedx::conv3x3_x3_kernel%s, %s>' % (STAGE_KERNEL[dom], STAGE_FUSE.get(dom, 'false'))
     else:
         kname = 'sedx::conv3x3_kernel%s>' % STAGE_KERNEL[dom]
-    traffic, rocprof_ms = profiled(kname) if B == 32 else (None, None)
+    traffic, rocprof_ms, mfma_util, clock = profiled(kname) if B == 32 else (None, None, None, None)
     return {'bound': 'mfma',
             'kernel': 'conv3x3_%s (%s)' % ('x3_kernel' if precision == 'x3' else 'kernel', dom),
             'arith': '3xbf16-split MFMA 32x32x16, fp32 acc (peak = bf16 dense 2.5 PF / 3)'
@@ -199,6 +202,7 @@ def roofline(stage_ms, B, precision):
             if traffic is not None else None,
             'flops_per_launch': flops, 'avg_launch_ms': conv[dom],
             'avg_launch_ms_rocprof': rocprof_ms,
+            'mfma_busy_frac_pmc': mfma_util, 'clock_ghz_pmc': clock,
             'timing': 'avg_launch_ms: HIP events on the launch stream (one batch at a time); '
                       'avg_launch_ms_rocprof: rocprofv3 --kernel-trace --stats of this bench '
                       '(--streams 1 --no-side), committed summary',

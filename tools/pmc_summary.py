@@ -36,6 +36,23 @@ def main(src, tag):
                 acc[short(r['Kernel_Name'])].append(float(r['Counter_Value']))
         for k, v in acc.items():
             out.setdefault(k, {})[ctr.lower() + '_kib_avg'] = sum(v) / len(v)
+    mp = os.path.join(src, 'pmc_mfma', 'pmc_counter_collection.csv')
+    if os.path.exists(mp):
+        acc = defaultdict(lambda: defaultdict(list))
+        for r in csv.DictReader(open(mp)):
+            acc[short(r['Kernel_Name'])][r['Counter_Name']].append(float(r['Counter_Value']))
+        for k, cs in acc.items():
+            busy, gui = cs.get('SQ_VALU_MFMA_BUSY_CYCLES'), cs.get('GRBM_GUI_ACTIVE')
+            if not busy or not gui:
+                continue
+            v = out.setdefault(k, {})
+            v['mfma_busy_cycles_avg'] = sum(busy) / len(busy)
+            v['grbm_gui_active_avg'] = sum(gui) / len(gui)
+            # GRBM_GUI_ACTIVE is summed over the 8 XCDs; 1024 SIMDs issue MFMAs
+            cyc = v['grbm_gui_active_avg'] / 8
+            v['mfma_util'] = v['mfma_busy_cycles_avg'] / (cyc * 1024)
+            if v.get('avg_ns'):
+                v['clock_ghz'] = cyc / v['avg_ns']
     for k, v in out.items():
         if 'fetch_size_kib_avg' in v and 'write_size_kib_avg' in v:
             v['hbm_read_bytes_corrected'] = 2 * v['fetch_size_kib_avg'] * 1024
@@ -44,14 +61,16 @@ def main(src, tag):
     os.makedirs('profiles', exist_ok=True)
     with open(os.path.join('profiles', '%s_kernel_summary.json' % tag), 'w') as f:
         json.dump(out, f, indent=1, sort_keys=True)
-    lines = ['| kernel | calls | avg us | % | FETCH KiB (raw) | WRITE KiB | HBM MB (corrected) |',
-             '|---|---|---|---|---|---|---|']
+    lines = ['| kernel | calls | avg us | % | FETCH KiB (raw) | WRITE KiB | HBM MB (corrected) | MFMA util | clock GHz |',
+             '|---|---|---|---|---|---|---|---|---|']
     for k, v in sorted(out.items(), key=lambda kv: -kv[1].get('pct', 0)):
-        lines.append('| %s | %s | %.1f | %.2f | %s | %s | %s |' % (
+        lines.append('| %s | %s | %.1f | %.2f | %s | %s | %s | %s | %s |' % (
             k, v.get('calls', ''), v.get('avg_ns', 0) / 1e3, v.get('pct', 0),
             '%.0f' % v['fetch_size_kib_avg'] if 'fetch_size_kib_avg' in v else '',
             '%.0f' % v['write_size_kib_avg'] if 'write_size_kib_avg' in v else '',
-            '%.1f' % (v['hbm_bytes_corrected'] / 1e6) if 'hbm_bytes_corrected' in v else ''))
+            '%.1f' % (v['hbm_bytes_corrected'] / 1e6) if 'hbm_bytes_corrected' in v else '',
+            '%.3f' % v['mfma_util'] if v.get('mfma_busy_cycles_avg') else '',
+            '%.2f' % v['clock_ghz'] if v.get('clock_ghz') else ''))
     with open(os.path.join('profiles', '%s_kernel_summary.md' % tag), 'w') as f:
         f.write('\n'.join(lines) + '\n')
     print('\n'.join(lines))
