@@ -23,7 +23,8 @@ import sys
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
-for _p in (REPO, os.path.join(REPO, 'sound-event-detection_amd')):
+# SEDX_PKG: an alternative build of the package (A/B runs of kernel variants)
+for _p in (REPO, os.environ.get('SEDX_PKG') or os.path.join(REPO, 'sound-event-detection_amd')):
     if _p not in sys.path:
         sys.path.insert(0, _p)
 
@@ -88,6 +89,10 @@ def measure(model, wave, args, world, rank, dev):
     a single stream."""
     B = wave.shape[0]
     streams = [torch.cuda.Stream(dev) for _ in range(max(1, args.streams))]
+    # conv stacks in issue order (sedx_set_pipelined): without it the batches
+    # in flight can fall into lockstep, two conv stacks splitting the chip and
+    # the GRUs running side by side on 32 CUs (measured: ~10 % slower runs)
+    model.set_pipelined(len(streams) > 1 and not args.no_pipeline)
 
     def step(st=None):
         with torch.no_grad(), torch.cuda.stream(st or torch.cuda.current_stream(dev)):
@@ -118,6 +123,7 @@ def measure(model, wave, args, world, rank, dev):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     value = world * B * args.steps / elapsed
+    model.set_pipelined(False)
     lat = []
     for _ in range(max(5, min(args.steps, 20))):
         torch.cuda.synchronize()
@@ -151,7 +157,7 @@ def stage_times(model, wave, dev, reps):
 # command (tools/profile_round.sh -> tools/pmc_summary.py; FETCH_SIZE x2 per
 # the gfx950 correction + WRITE_SIZE), committed under profiles/.
 PROFILE_SUMMARY = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles',
-                               'r01e_kernel_summary.json')
+                               'r01f_kernel_summary.json')
 STAGE_KERNEL = {'b1c2': '<64, 64, 1', 'b2c1': '<32, 128, 0', 'b2c2': '<32, 128, 1',
                 'b3c1': '<16, 128, 0', 'b3c2': '<16, 128, 1', 'b4c1': '<8, 128, 0',
                 'b4c2': '<8, 128, 2'}
@@ -255,6 +261,8 @@ def main():
     ap.add_argument('--batch', type=int, default=32, help='clips per GPU per step')
     ap.add_argument('--streams', type=int, default=2,
                     help='batches in flight per GPU (HIP streams the steps rotate over)')
+    ap.add_argument('--no-pipeline', action='store_true',
+                    help='streams > 1 without ordering the conv stacks (A/B of sedx_set_pipelined)')
     ap.add_argument('--model', choices=list(MODEL_NAMES), default='gru')
     ap.add_argument('--mode', choices=['clip', 'window'], default='clip')
     ap.add_argument('--precision', choices=list(PEAK_TF), default='x3')
@@ -311,7 +319,8 @@ def main():
                        'batch_per_gpu': B, 'global_batch': B * world, 'clip_seconds': 10,
                        'sample_rate': 16000, 'mode': args.mode, 'precision': args.precision,
                        'parallelism': 'dp%d clip-sharded, RCCL gather of framewise' % world,
-                       'streams': args.streams},
+                       'streams': args.streams,
+                       'pipelined': args.streams > 1 and not args.no_pipeline},
             'ms_per_clip_p99': round(p99, 4),
             'roofline': roof, 'cpu_baseline': cpu, 'stage_ms': stage_ms,
             'value_exact_fp32': exact,

@@ -168,6 +168,14 @@ sedx_status sedx_forward_windows_vote(sedx_handle* h, const float* d_audio, int6
 typedef enum { SEDX_PRECISION_EXACT = 0, SEDX_PRECISION_X3 = 1 } sedx_precision;
 sedx_status sedx_set_precision(sedx_handle* h, int32_t mode);
 
+/* Serving with several batches in flight (one stream per request): when on,
+ * the conv stack of every forward on this handle starts only after the conv
+ * stack of the previously issued forward finished (a device-side event wait,
+ * no host sync), so batch i's GRU / MHA + head overlap batch i+1's conv stack
+ * instead of two conv stacks splitting the chip.  Results are unchanged;
+ * order = host issue order.  Off by default. */
+sedx_status sedx_set_pipelined(sedx_handle* h, int32_t on);
+
 /* Per-stage device timing (the reference only wall-clocks whole loops,
  * pytorch/main_strong.py:565-574).  When on, every forward records HIP events
  * on its stream at the stage boundaries; sedx_stage_times waits for them and

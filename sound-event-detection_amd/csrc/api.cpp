@@ -84,6 +84,13 @@ struct sedx_handle {
   bool gru_simple = getenv("SEDX_GRU_SIMPLE") != nullptr;   // A/B: per-(clip,dir) recurrence
   bool debug_x0 = getenv("SEDX_DEBUG_X0") != nullptr;      // diagnostic: X0 snapshot after the frontend
   bool profiling = false;
+  // sedx_set_pipelined: conv stacks of successive forwards run in issue order
+  // (each waits for the previous one's conv-done event), whatever streams
+  // they are issued on, so the sequence + head of batch i overlap the conv
+  // stack of batch i+1 instead of two conv stacks sharing the chip
+  bool pipelined = false;
+  bool conv_done_recorded = false;
+  hipEvent_t conv_done = nullptr;
   hipEvent_t ev[SEDX_N_STAGES + 1] = {};
   bool ev_recorded[SEDX_N_STAGES + 1] = {};
 };
@@ -254,6 +261,7 @@ sedx_status run_body(sedx_handle* h, int64_t B, const Geometry& g, float* ws, co
   float* P = ws + l.bufB;
   const int iB = (int)B;
   mark(h, 1, s);
+  if (h->pipelined && h->conv_done_recorded) HIP_TRY(h, hipStreamWaitEvent(s, h->conv_done, 0));
   const bool x3 = h->precision == SEDX_PRECISION_X3;
   int* sched = reinterpret_cast<int*>(ws + l.sched);
   if (x3) {
@@ -289,6 +297,10 @@ sedx_status run_body(sedx_handle* h, int64_t B, const Geometry& g, float* ws, co
       launch_conv3x3(c.in, iB, c.T, c.F, c.cin, c.cout, w.wp[c.idx], w.cb[c.idx], c.out, c.epi, s);
   }
   mark(h, 9, s);
+  if (h->pipelined) {
+    HIP_TRY(h, hipEventRecord(h->conv_done, s));
+    h->conv_done_recorded = true;
+  }
   float* S = P;                                   // [B][T3][512]
   const int M = (int)(B * g.T3);
   float* G = A;                                   // [M][1536]
@@ -430,6 +442,7 @@ void sedx_destroy(sedx_handle* h) {
     DeviceGuard g(h->device);
     for (auto& e : h->ev)
       if (e) (void)hipEventDestroy(e);
+    if (h->conv_done) (void)hipEventDestroy(h->conv_done);
     if (h->blob) (void)hipFree(h->blob);
     if (h->ws) (void)hipFree(h->ws);
   }
@@ -811,6 +824,15 @@ sedx_status sedx_set_profiling(sedx_handle* h, int32_t on) {
     for (auto& e : h->ev) HIP_TRY(h, hipEventCreate(&e));
   h->profiling = on != 0;
   for (auto& r : h->ev_recorded) r = false;
+  return SEDX_OK;
+}
+
+sedx_status sedx_set_pipelined(sedx_handle* h, int32_t on) {
+  if (!h) return SEDX_EINVAL;
+  DeviceGuard dg(h->device);
+  if (on && !h->conv_done) HIP_TRY(h, hipEventCreateWithFlags(&h->conv_done, hipEventDisableTiming));
+  h->pipelined = on != 0;
+  h->conv_done_recorded = false;
   return SEDX_OK;
 }
 

@@ -59,6 +59,28 @@ __device__ __forceinline__ void split8(const float4 a, const float4 b, uint4& hi
 
 __device__ __forceinline__ bf16x8 as_bf16x8(uint4 v) { return __builtin_bit_cast(bf16x8, v); }
 
+// 4x4 transpose across the 4 lanes of a quad (j = lane & 3): on entry lane j
+// holds column j of a 4x4 block in v[0..3] (v[k] = row k), on exit row j
+// (v[k] = column k).  Two butterfly stages (lane bit 0, lane bit 1), each a
+// DPP quad permute + select per register.
+template <int CTRL>
+__device__ __forceinline__ float quad_perm(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ void quad_transpose4(float* v, int j) {
+  const bool odd = j & 1, upper = j & 2;
+  const float t0 = quad_perm<0xB1>(v[1]), t1 = quad_perm<0xB1>(v[0]);   // lanes (1,0,3,2)
+  const float t2 = quad_perm<0xB1>(v[3]), t3 = quad_perm<0xB1>(v[2]);
+  const float a0 = odd ? t0 : v[0], a1 = odd ? v[1] : t1;
+  const float a2 = odd ? t2 : v[2], a3 = odd ? v[3] : t3;
+  const float u0 = quad_perm<0x4E>(a2), u1 = quad_perm<0x4E>(a3);      // lanes (2,3,0,1)
+  const float u2 = quad_perm<0x4E>(a0), u3 = quad_perm<0x4E>(a1);
+  v[0] = upper ? u0 : a0;
+  v[1] = upper ? u1 : a1;
+  v[2] = upper ? a2 : u2;
+  v[3] = upper ? a3 : u3;
+}
+
 // MFMA row R (0..BM-1 of the block tile) -> (t_local, f)
 template <int F, int EPI>
 __device__ __forceinline__ void rowmap(int R, int& tl, int& f) {
@@ -275,9 +297,13 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
   // select) so the compiler's vmcnt bookkeeping stays exact and each wait
   // covers only the loads it needs.  Per-item halo geometry is loop-invariant.
   int a_r[NA], a_f[NA], a_off[NA], a_rec[NA];
-  bool a_fok[NA];
+  bool a_fok[NA], a_live[NA];
 #pragma unroll
   for (int i = 0; i < NA; ++i) {
+    // FUSE: the last item round is ragged (660 halo positions over 512
+    // threads): whole waves past the end skip its conv1 work and LDS writes
+    // (their clamped loads stay, keeping the vmcnt bookkeeping branch-free)
+    a_live[i] = !FUSE || __builtin_amdgcn_readfirstlane(i * 512 + (tid & ~63)) < A_ITEMS;
     const int idx = min(tid + i * 512, A_ITEMS - 1);
     const int pos = FUSE ? idx : idx >> 1, hh = FUSE ? 0 : idx & 1;
     const int r = pos / CS, c = pos - r * CS;
@@ -316,6 +342,7 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
   {                                                                                     \
     uint4* dst_ = Abuf + (buf) * A_U4;                                                  \
     _Pragma("unroll") for (int i = (i0); i < (i1); ++i) {                               \
+      if (!a_live[i]) continue;  /* wave-uniform: no lane of this wave has item i */    \
       uint4 hi, lo;                                                                     \
       const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);                                 \
       if constexpr (FUSE) {                                                             \
@@ -422,6 +449,7 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
 #pragma unroll
         for (int i = 0; i < 16; ++i) r[i] = fmaxf(acc[mt][nt][i] + bv, 0.0f);
         if (EPI == EPI_STORE) {
+#ifdef SEDX_EPI_DWORD
           float* ob = out + ((int64_t)c.b * T + c.t0) * F * Cout + n;
           const int tlim = T - c.t0;
 #pragma unroll
@@ -431,6 +459,25 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
             if (live && tl < tlim) ob[(tl * F + f) * Cout] = r[i];
             if ((i & 3) == 3) __builtin_amdgcn_sched_barrier(0);
           }
+#else
+          // regs 4g..4g+3 are 4 consecutive pixels of this lane's channel; a
+          // 4x4 transpose inside each lane quad gives every lane 4 consecutive
+          // channels of one pixel: 4 dwordx4 stores instead of 16 dword stores,
+          // same bytes, the same 128-B lines per group of stores
+          const int j = lane_ & 3;
+          float* ob = out + ((int64_t)c.b * T + c.t0) * F * Cout + (n - j);
+          const int tlim = T - c.t0;
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            float* v = r + 4 * g;
+            quad_transpose4(v, j);
+            int tl, f;
+            rowmap<F, EPI>(Rbase + 8 * g + 4 * h + j, tl, f);
+            if (live && tl < tlim)
+              *reinterpret_cast<float4*>(ob + (tl * F + f) * Cout) = make_float4(v[0], v[1], v[2], v[3]);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+#endif
         } else if (EPI == EPI_POOL2) {
           constexpr int FO = F / 2;
           const int To = T / 2;
@@ -525,33 +572,70 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
 #else
 #define SEDX_ABL_SYNC() __syncthreads()
 #endif
-#define SEDX_STAGE_STORES(U, KY)                                                        \
+// After the stage barrier the wave interleaves the stage's LDS writes and
+// global refill loads with the 4 MFMA groups of the stage's last tap (whose
+// fragments were read before the barrier), so the matrix pipe is not idle
+// while both waves of a SIMD stage data:
+//   group (0,0) | W store | group (0,1) | W load | group (1,0) | halo work | group (1,1)
+// then the fragments of the next tap are read.
+#define SEDX_MFMA_G(set, mt, nt)                                                        \
   {                                                                                     \
+    acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[set][2 * (mt)], fb[set][2 * (nt)], acc[mt][nt], 0, 0, 0);     \
+    acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[set][2 * (mt)], fb[set][2 * (nt) + 1], acc[mt][nt], 0, 0, 0); \
+    acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[set][2 * (mt) + 1], fb[set][2 * (nt)], acc[mt][nt], 0, 0, 0); \
+    __builtin_amdgcn_sched_barrier(0);                                                  \
+  }
+#ifdef SEDX_NO_INTERLEAVE
+#define SEDX_MFMA_PIECE(set, mt, nt)
+#define SEDX_MFMA_REST(set) SEDX_MFMAS(set)
+#else
+#define SEDX_MFMA_PIECE(set, mt, nt) SEDX_MFMA_G(set, mt, nt)
+#define SEDX_MFMA_REST(set) SEDX_MFMA_G(set, 1, 1)
+#endif
+// FUSE: the conv1 work of n1's halo items (VALU-heavy) is issued between the
+// MFMAs of the stage's first tap, BEFORE the stage barrier.  Legal: A buffer
+// U^1 was last read by unit U-1 before its stage-2 barrier, and n1's inputs
+// were loaded two stages earlier.
+#define SEDX_STAGE_POST(U, KY, set)                                                     \
+  {                                                                                     \
+    SEDX_MFMA_PIECE(set, 0, 0);                                                         \
     if ((KY) == 0) {                                                                    \
       SEDX_ABL_STORE_W((U) & 1, U);                                                     \
-      SEDX_ABL_LOAD_W((U) & 1, n1, 1);                                                  \
-      if constexpr (FUSE) {  /* conv1 work spread over two stages */                    \
-        SEDX_STORE_A_ITEMS((U) ^ 1, n1, 0, 1);                                          \
-      } else {                                                                          \
-        SEDX_ABL_STORE_A((U) ^ 1, n1);                                                  \
-        SEDX_ABL_LOAD_A(n2);                                                            \
-      }                                                                                 \
     } else if ((KY) == 1) {                                                             \
       SEDX_ABL_STORE_W(((U) + 1) & 1, ((U) + 1) & 1);                                   \
-      SEDX_ABL_LOAD_W(((U) + 1) & 1, n1, 2);                                            \
-      if constexpr (FUSE) {                                                             \
-        SEDX_STORE_A_ITEMS((U) ^ 1, n1, 1, NA);                                         \
-        SEDX_LOAD_A(n2);                                                                \
-      }                                                                                 \
     } else {                                                                            \
       SEDX_ABL_STORE_W((U) & 1, (U) & 1);                                               \
+    }                                                                                   \
+    SEDX_MFMA_PIECE(set, 0, 1);                                                         \
+    if ((KY) == 0) {                                                                    \
+      SEDX_ABL_LOAD_W((U) & 1, n1, 1);                                                  \
+    } else if ((KY) == 1) {                                                             \
+      SEDX_ABL_LOAD_W(((U) + 1) & 1, n1, 2);                                            \
+    } else {                                                                            \
       if (tid == 0) claim_land();                                                       \
       SEDX_ABL_LOAD_W((U) & 1, n2, 0);                                                  \
     }                                                                                   \
+    SEDX_MFMA_PIECE(set, 1, 0);                                                         \
+    if constexpr (FUSE) {                                                               \
+      if ((KY) == 1) {                                                                  \
+        SEDX_LOAD_A(n2);                                                                \
+      }                                                                                 \
+    } else if ((KY) == 0) {                                                             \
+      SEDX_ABL_STORE_A((U) ^ 1, n1);                                                    \
+      SEDX_ABL_LOAD_A(n2);                                                              \
+    }                                                                                   \
+    SEDX_MFMA_REST(set);                                                                \
   }
 #define SEDX_STAGE(U, KY)                                                               \
   {                                                                                     \
     SEDX_READ_FRAGS(((U) + 3 * (KY) + 1) & 1, U, ((U) + (KY)) & 1, 3 * (KY) + 1);       \
+    if constexpr (FUSE) {                                                               \
+      if ((KY) == 0) {                                                                  \
+        SEDX_STORE_A_ITEMS((U) ^ 1, n1, 0, 1);                                          \
+      } else if ((KY) == 1) {                                                           \
+        SEDX_STORE_A_ITEMS((U) ^ 1, n1, 1, NA);                                         \
+      }                                                                                 \
+    }                                                                                   \
     SEDX_MFMAS(((U) + 3 * (KY)) & 1);                                                   \
     SEDX_READ_FRAGS(((U) + 3 * (KY) + 2) & 1, U, ((U) + (KY)) & 1, 3 * (KY) + 2);       \
     SEDX_MFMAS(((U) + 3 * (KY) + 1) & 1);                                               \
@@ -559,13 +643,12 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
     SEDX_ABL_SYNC();                                                                    \
     SEDX_ST_END(st_bar);                                                                \
     SEDX_ST_VMWAIT();                                                                   \
-    SEDX_STAGE_STORES(U, KY);                                                           \
+    SEDX_STAGE_POST(U, KY, ((U) + 3 * (KY) + 2) & 1);                                   \
     if ((KY) < 2) {                                                                     \
       SEDX_READ_FRAGS(((U) + 3 * (KY) + 3) & 1, U, ((U) + (KY) + 1) & 1, 3 * (KY) + 3); \
     } else {                                                                            \
       SEDX_READ_FRAGS(((U) + 1) & 1, (U) ^ 1, ((U) + 1) & 1, 0);                        \
     }                                                                                   \
-    SEDX_MFMAS(((U) + 3 * (KY) + 2) & 1);                                               \
   }
 
 #define SEDX_UNIT(U)                                                                    \
@@ -592,7 +675,10 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
   SEDX_ST_FLUSH();
 #undef SEDX_UNIT
 #undef SEDX_STAGE
-#undef SEDX_STAGE_STORES
+#undef SEDX_STAGE_POST
+#undef SEDX_MFMA_G
+#undef SEDX_MFMA_PIECE
+#undef SEDX_MFMA_REST
 #undef SEDX_READ_FRAGS
 #undef SEDX_MFMAS
 #undef SEDX_LOAD_W

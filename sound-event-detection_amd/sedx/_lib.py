@@ -19,7 +19,7 @@ EXPORTS = ['sedx_create', 'sedx_destroy', 'sedx_last_error', 'sedx_version', 'se
            'sedx_finalize_weights', 'sedx_output_geometry', 'sedx_workspace_size',
            'sedx_forward', 'sedx_forward_features', 'sedx_gamma_features',
            'sedx_window_geometry', 'sedx_forward_windows', 'sedx_window_workspace_size',
-           'sedx_events', 'sedx_set_profiling', 'sedx_stage_times', 'sedx_set_precision',
+           'sedx_events', 'sedx_set_profiling', 'sedx_stage_times', 'sedx_set_precision', 'sedx_set_pipelined',
            'sedx_forward_windows_vote', 'sedx_events_workspace_size', 'sedx_events_device',
            'sedx_forward_i16', 'sedx_wav_parse', 'sedx_wav_decode_mono', 'sedx_resample_size',
            'sedx_resample_workspace_size', 'sedx_resample']
@@ -88,6 +88,7 @@ def lib():
                                I32),
         'sedx_set_profiling': ([P, I32], I32),
         'sedx_set_precision': ([P, I32], I32),
+        'sedx_set_pipelined': ([P, I32], I32),
         'sedx_stage_times': ([P, ctypes.POINTER(ctypes.c_float), I32, ctypes.POINTER(I32)], I32),
         'sedx_wav_parse': ([P, SZ, ctypes.POINTER(SedxWavInfo)], I32),
         'sedx_wav_decode_mono': ([P, ctypes.POINTER(SedxWavInfo), P, P], I32),

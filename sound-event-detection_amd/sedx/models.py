@@ -219,6 +219,7 @@ class _SedModel(nn.Module):
         self.conv_block4 = ConvBlock(256, 512)
         self._natives = {}
         self.precision = 'x3'
+        self.pipelined = False
 
     def _config(self):
         cfg = _lib.SedxConfig()
@@ -257,6 +258,9 @@ class _SedModel(nn.Module):
             _lib.check(_lib.lib().sedx_set_precision(nat.h, _lib.PRECISION[self.precision]), nat.h,
                        'set_precision')
             nat.precision = self.precision
+        if getattr(nat, 'pipelined', False) != self.pipelined:
+            _lib.check(_lib.lib().sedx_set_pipelined(nat.h, int(self.pipelined)), nat.h, 'set_pipelined')
+            nat.pipelined = self.pipelined
         return nat
 
     def set_precision(self, mode):
@@ -265,6 +269,13 @@ class _SedModel(nn.Module):
         if mode not in _lib.PRECISION:
             raise ValueError('precision must be one of %s' % sorted(_lib.PRECISION))
         self.precision = mode
+        return self
+
+    def set_pipelined(self, on=True):
+        """Several batches in flight on different streams: run the conv
+        stacks in issue order so one batch's GRU / MHA + head overlap the next
+        batch's conv stack (sedx_set_pipelined)."""
+        self.pipelined = bool(on)
         return self
 
     def _check_eval(self, mixup_lambda, timeshift):

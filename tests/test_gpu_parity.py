@@ -104,10 +104,13 @@ def test_batch_invariance(model):
         assert np.array_equal(one['framewise_output'][0], full['framewise_output'][i])
 
 
-def test_concurrent_streams_bit_identical(model):
+@pytest.mark.parametrize('pipelined', [False, True])
+def test_concurrent_streams_bit_identical(model, pipelined):
     """Batches in flight on two HIP streams (bench.py --streams 2: one batch's
     GRU / head overlapping the next batch's conv stack, whose workgroups then
-    claim tiles dynamically) give bit-identical outputs to one batch at a time."""
+    claim tiles dynamically) give bit-identical outputs to one batch at a time,
+    with and without the conv stacks ordered across streams
+    (sedx_set_pipelined)."""
     mt, m = model
     waves = [torch.from_numpy(synth.make_waveforms(32, seconds=10.0, sample_rate=16000, seed=s)).cuda()
              for s in (5, 6, 7, 8)]
@@ -115,14 +118,18 @@ def test_concurrent_streams_bit_identical(model):
         ref = [m(w)['framewise_output'].clone() for w in waves]
         torch.cuda.synchronize()
         streams = [torch.cuda.Stream(), torch.cuda.Stream()]
-        for rep in range(3):
-            outs = []
-            for i, w in enumerate(waves):
-                with torch.cuda.stream(streams[i % 2]):
-                    outs.append(m(w)['framewise_output'])
-            torch.cuda.synchronize()
-            for i, (a, b) in enumerate(zip(outs, ref)):
-                assert torch.equal(a, b), (mt, rep, i, float((a - b).abs().max()))
+        m.set_pipelined(pipelined)
+        try:
+            for rep in range(3):
+                outs = []
+                for i, w in enumerate(waves):
+                    with torch.cuda.stream(streams[i % 2]):
+                        outs.append(m(w)['framewise_output'])
+                torch.cuda.synchronize()
+                for i, (a, b) in enumerate(zip(outs, ref)):
+                    assert torch.equal(a, b), (mt, rep, i, float((a - b).abs().max()))
+        finally:
+            m.set_pipelined(False)
 
 
 @pytest.mark.parametrize('n_clips,seconds', [(1, 1.0), (40, 1.0), (544, 0.5)])
