@@ -186,9 +186,12 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
   constexpr int A_U4 = NPOS * 5;          // one halo image
   constexpr int W_U4 = BN * 4;            // one tap
   constexpr int WS_U4 = 3 * W_U4;         // one stage (kernel row)
-  // staging items: (halo position, 8-channel half); FUSE: one item per halo
-  // position (all 16 channels: the chunk's conv1 weights are wave-uniform)
-  constexpr int A_ITEMS = FUSE ? RT * CS : 2 * RT * CS;
+  // staging items: (halo position, 4-channel quarter): the 4 lanes of a
+  // position read its chunk's 64 contiguous bytes, so one load instruction
+  // covers 16 positions (16 cache-line segments) instead of 32 positions at
+  // 16 B each; FUSE: one item per halo position (all 16 channels: the
+  // chunk's conv1 weights are wave-uniform)
+  constexpr int A_ITEMS = FUSE ? RT * CS : 4 * RT * CS;
   constexpr int NA = (A_ITEMS + 511) / 512;
   constexpr int NW = (WS_U4 + 511) / 512;
 
@@ -288,7 +291,7 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[mt][nt][r] = 0.0f;
 
-  float4 ra0[NA], ra1[NA];                // staged halo items (2 x 16 B each)
+  float4 ra0[NA];                         // staged halo items (16 B each)
   bool rok[NA];                           // ... inside the image (else zero)
   float xr[FUSE ? NA : 1][9];             // FUSE: conv1 input neighbourhoods
   uint4 rw0[NW], rw1[NW];                 // W stage x lives in rw(x & 1)
@@ -305,13 +308,15 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
     // (their clamped loads stay, keeping the vmcnt bookkeeping branch-free)
     a_live[i] = !FUSE || __builtin_amdgcn_readfirstlane(i * 512 + (tid & ~63)) < A_ITEMS;
     const int idx = min(tid + i * 512, A_ITEMS - 1);
-    const int pos = FUSE ? idx : idx >> 1, hh = FUSE ? 0 : idx & 1;
+    const int pos = FUSE ? idx : idx >> 2, qq = FUSE ? 0 : idx & 3;
     const int r = pos / CS, c = pos - r * CS;
     a_r[i] = r;
     a_f[i] = c - 1;
     a_fok[i] = c >= 1 && c <= F;
-    a_off[i] = FUSE ? min(max(c - 1, 0), F - 1) : min(max(c - 1, 0), F - 1) * Cin + 8 * hh;
-    a_rec[i] = (r * CSP + c) * 5 + hh;
+    a_off[i] = FUSE ? min(max(c - 1, 0), F - 1) : min(max(c - 1, 0), F - 1) * Cin + 4 * qq;
+    // FUSE: record index in uint4; else the quarter's hi slot in uint2 units
+    // (record = 10 x 8 B: hi quarters 0-3, lo quarters 4-7, pad)
+    a_rec[i] = FUSE ? (r * CSP + c) * 5 : (r * CSP + c) * 10 + qq;
   }
 #define SEDX_LOAD_A(c_)                                                                 \
   if constexpr (FUSE) {                                                                 \
@@ -330,9 +335,7 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
       const int t = (c_).t0 - 1 + a_r[i];                                               \
       const bool ok = a_fok[i] && t >= 0 && t < T;                                      \
       const int tc = min(max(t, 0), T - 1);                                             \
-      const float4* src = reinterpret_cast<const float4*>(in_b_ + (tc * F * Cin + a_off[i])); \
-      ra0[i] = src[0];                                                                  \
-      ra1[i] = src[1];                                                                  \
+      ra0[i] = *reinterpret_cast<const float4*>(in_b_ + (tc * F * Cin + a_off[i]));     \
       rok[i] = ok;     /* halo zeroes applied at the LDS write, not here */             \
     }                                                                                   \
     asm volatile("" ::: "memory"); /* issue here: not sunk to the use */                \
@@ -368,9 +371,15 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
           dst_[a_rec[i] + 2 + hh] = lo;                                                 \
         }                                                                               \
       } else {                                                                          \
-        split8(rok[i] ? ra0[i] : z, rok[i] ? ra1[i] : z, hi, lo);                       \
-        dst_[a_rec[i]] = hi;                                                            \
-        dst_[a_rec[i] + 2] = lo;                                                        \
+        const float4 v_ = rok[i] ? ra0[i] : z;                                          \
+        uint2 h2, l2;                                                                   \
+        split2(v_.x, v_.y, h2.x, l2.x);                                                 \
+        split2(v_.z, v_.w, h2.y, l2.y);                                                 \
+        uint2* d2_ = reinterpret_cast<uint2*>(dst_);                                    \
+        d2_[a_rec[i]] = h2;                                                             \
+        d2_[a_rec[i] + 4] = l2;                                                         \
+        (void)hi;                                                                       \
+        (void)lo;                                                                       \
       }                                                                                 \
     }                                                                                   \
     asm volatile("" ::: "memory");                                                      \
