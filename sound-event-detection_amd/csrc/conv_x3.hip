@@ -626,7 +626,9 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
     }                                                                                   \
     SEDX_MFMA_PIECE(set, 1, 0);                                                         \
     if constexpr (FUSE) {                                                               \
-      if ((KY) == 1) {                                                                  \
+      /* conv1's input (one channel) is the same for every chunk of a tile: */          \
+      /* the neighbourhoods in xr are reloaded only when n2 starts a new tile */        \
+      if ((KY) == 1 && n2.chunk == 0) {                                                 \
         SEDX_LOAD_A(n2);                                                                \
       }                                                                                 \
     } else if ((KY) == 0) {                                                             \

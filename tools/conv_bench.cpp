@@ -17,12 +17,21 @@ struct Layer { const char* name; int T, F, cin, cout, epi; };
 int main(int argc, char** argv) {
   const int B = argc > 1 ? atoi(argv[1]) : 32;
   const int reps = argc > 2 ? atoi(argv[2]) : 20;
-  const Layer L[] = {{"b1c2", 1001, 64, 64, 64, sedx::EPI_POOL2},  {"b2c1", 500, 32, 64, 128, sedx::EPI_STORE},
-                     {"b2c2", 500, 32, 128, 128, sedx::EPI_POOL2}, {"b3c1", 250, 16, 128, 256, sedx::EPI_STORE},
-                     {"b3c2", 250, 16, 256, 256, sedx::EPI_POOL2}, {"b4c1", 125, 8, 256, 512, sedx::EPI_STORE},
-                     {"b4c2", 125, 8, 512, 512, sedx::EPI_FMEAN}};
+  const Layer LM[] = {{"b1c2", 1001, 64, 64, 64, sedx::EPI_POOL2},  {"b2c1", 500, 32, 64, 128, sedx::EPI_STORE},
+                      {"b2c2", 500, 32, 128, 128, sedx::EPI_POOL2}, {"b3c1", 250, 16, 128, 256, sedx::EPI_STORE},
+                      {"b3c2", 250, 16, 256, 256, sedx::EPI_POOL2}, {"b4c1", 125, 8, 256, 512, sedx::EPI_STORE},
+                      {"b4c2", 125, 8, 512, 512, sedx::EPI_FMEAN}};
+  // CB_SWEEP=1: K-length sweep at one shape (F=32, Cout 128, pooled), equal
+  // FLOPs per layer (T scaled by 1/Cin): time per FLOP vs chunks per tile
+  const Layer LS[] = {{"cin64", 1000, 32, 64, 128, sedx::EPI_POOL2},  {"cin128", 500, 32, 128, 128, sedx::EPI_POOL2},
+                      {"cin256", 250, 32, 256, 128, sedx::EPI_POOL2}, {"cin512", 125, 32, 512, 128, sedx::EPI_POOL2},
+                      {"s_cin64", 1000, 32, 64, 128, sedx::EPI_STORE}, {"s_cin256", 250, 32, 256, 128, sedx::EPI_STORE}};
+  const bool sweep = getenv("CB_SWEEP") != nullptr;
+  const Layer* L = sweep ? LS : LM;
+  const int NL = sweep ? 6 : 7;
   size_t max_in = 0, max_w = 0;
-  for (const Layer& l : L) {
+  for (int li = 0; li < NL; ++li) {
+    const Layer& l = L[li];
     max_in = std::max(max_in, (size_t)B * l.T * l.F * std::max(l.cin, l.cout));
     max_w = std::max(max_w, (size_t)l.cin * l.cout * 36);
   }
@@ -44,7 +53,8 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   hipEventCreate(&e0); hipEventCreate(&e1);
   double tot_ms = 0, tot_f = 0;
-  for (const Layer& l : L) {
+  for (int li = 0; li < NL; ++li) {
+    const Layer& l = L[li];
     hipMemsetAsync(sched, 0, 256 * 4, 0);
     sedx::launch_conv3x3_x3(in, B, l.T, l.F, l.cin, l.cout, w, bias, out, l.epi, sched, 0);
     hipDeviceSynchronize();

@@ -9,6 +9,8 @@
 //       and 16 MFMAs whose A side [hiA t|hiA t+1] is built by v_permlane32_swap
 //   V2  32x32x16, 4 waves (one per SIMD), 128x64 wave tile: per tap 8 A + 4 B
 //       reads, 24 MFMAs
+//   V3  32x32x16, 4 waves, 128x128 wave tile, half the tap count per launch
+//       (equal MACs): per tap 8 A + 8 B reads, 48 MFMAs
 // Prints TF/s (useful x3 MACs: 1/3 of the bf16 MFMA work) and the in-kernel
 // clock (s_memtime / s_memrealtime).  Random operands: the clock the chip
 // holds depends on data (MI355X_MICROARCH.md, DVFS notes).
@@ -35,10 +37,10 @@ __device__ __forceinline__ uint4 swap_lo(uint4 x, uint4 y) {   // [x lanes 0-31 
 constexpr int LDS_U4 = 8192;   // 128 KB: one workgroup per CU
 
 template <int V>
-__global__ __launch_bounds__(V == 2 ? 256 : 512) void body(const uint4* __restrict__ src, float* out,
+__global__ __launch_bounds__(V >= 2 ? 256 : 512) void body(const uint4* __restrict__ src, float* out,
                                                            int iters) {
   __shared__ uint4 lds[LDS_U4];
-  constexpr int NT = V == 2 ? 256 : 512;
+  constexpr int NT = V >= 2 ? 256 : 512;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   for (int i = tid; i < LDS_U4; i += NT) lds[i] = src[(blockIdx.x * 977 + i) & (LDS_U4 * 4 - 1)];
   __syncthreads();
@@ -108,6 +110,32 @@ __global__ __launch_bounds__(V == 2 ? 256 : 512) void body(const uint4* __restri
     for (int m = 0; m < 4; ++m)
       for (int q = 0; q < 4; ++q)
         for (int r = 0; r < 4; ++r) sink += acc[m][q][r];
+  } else if constexpr (V == 3) {
+    f32x16 acc[4][4] = {};
+    uint4 fa[2][8], fb[2][8];
+#pragma unroll
+    for (int f = 0; f < 8; ++f) { fa[0][f] = rd(0, f); fb[0][f] = rd(0, 8 + f); }
+    for (int it = 0; it < iters / 2; ++it) {
+#pragma unroll
+      for (int t = 0; t < 6; ++t) {
+        const int c = t & 1, n = c ^ 1, tt = it * 6 + t + 1;
+#pragma unroll
+        for (int f = 0; f < 8; ++f) { fa[n][f] = rd(tt, f); fb[n][f] = rd(tt, 8 + f); }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            acc[m][q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf(fa[c][2 * m]), bf(fb[c][2 * q]), acc[m][q], 0, 0, 0);
+            acc[m][q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf(fa[c][2 * m]), bf(fb[c][2 * q + 1]), acc[m][q], 0, 0, 0);
+            acc[m][q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf(fa[c][2 * m + 1]), bf(fb[c][2 * q]), acc[m][q], 0, 0, 0);
+          }
+        if (t % 3 == 2) __syncthreads();
+      }
+    }
+    for (int m = 0; m < 4; ++m)
+      for (int q = 0; q < 4; ++q)
+        for (int r = 0; r < 16; ++r) sink += acc[m][q][r];
   } else {
     f32x16 acc[4][2] = {};
     uint4 fa[2][8], fb[2][4];
@@ -148,7 +176,7 @@ __global__ __launch_bounds__(V == 2 ? 256 : 512) void body(const uint4* __restri
 
 template <int V>
 static void run(const uint4* src, float* out, int ncu, int iters, int reps) {
-  const int nt = V == 2 ? 256 : 512;
+  const int nt = V >= 2 ? 256 : 512;
   hipLaunchKernelGGL(body<V>, dim3(ncu), dim3(nt), 0, 0, src, out, iters);   // warm
   (void)hipDeviceSynchronize();
   unsigned long long z[2] = {0, 0};
@@ -186,6 +214,7 @@ int main(int argc, char** argv) {
     run<0>(src, out, ncu, iters, reps);
     run<1>(src, out, ncu, iters, reps);
     run<2>(src, out, ncu, iters, reps);
+    run<3>(src, out, ncu, iters, reps);
   }
   return 0;
 }
