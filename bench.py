@@ -61,23 +61,57 @@ def build_model(name, device):
     return m.to(device).eval()
 
 
-def cpu_baseline(name, seconds):
+def cpu_baseline(name, seconds, model=None, dev=None):
     """Oracle (CPU restatement, torch fp32, reference op sequence) on a bounded
-    sample: B=4 clips of 10 s per iteration, repeated for ~``seconds``."""
+    sample: B=4 clips of 10 s per iteration, repeated for ~``seconds``.  With
+    ``model`` the same 4 clips also go through the GPU path and the oracle's
+    output is the checker: max |d framewise| is reported beside the rate."""
     from oracle import sed_oracle as O
     sd = O.full_state(synth.make_state_dict(name, seed=0), '16k')
     wave = synth.make_waveforms(4, seconds=10.0, sample_rate=16000, seed=7)
     O.forward(sd, name, wave=wave[:1])  # warm-up
     n, t0 = 0, time.perf_counter()
     while True:
-        O.forward(sd, name, wave=wave)
+        ref = O.forward(sd, name, wave=wave)
         n += 4
         el = time.perf_counter() - t0
         if el >= seconds or n >= 400:
             break
-    return {'value': n / el, 'unit': 'clips/s', 'cores': torch.get_num_threads(), 'kind': 'port',
-            'sample': '%d x 10 s clips (B=4 per iteration, %.1f s) through oracle/sed_oracle.py '
-                      'forward on the host CPU' % (n, el)}
+    out = {'value': n / el, 'unit': 'clips/s', 'cores': torch.get_num_threads(), 'kind': 'port',
+           'sample': '%d x 10 s clips (B=4 per iteration, %.1f s) through oracle/sed_oracle.py '
+                     'forward on the host CPU' % (n, el)}
+    if model is not None:
+        with torch.no_grad():
+            fw = model(torch.from_numpy(wave).to(dev))['framewise_output'].cpu().numpy()
+        out['parity_max_abs_framewise'] = float(np.max(np.abs(fw - ref['framewise_output'].numpy())))
+        out['parity_tolerance'] = 1e-3
+    return out
+
+
+def latency_b1(model, dev, reps=20):
+    """End-to-end latency of ONE 10 s clip: clip mode and
+    window mode (its 6 windows in one launch), input already on the device;
+    and clip mode from a host buffer to the framewise output back on the
+    host (PCIe-inclusive)."""
+    w1 = torch.from_numpy(synth.make_waveforms(1, seconds=10.0, sample_rate=16000, seed=11))
+    wd = w1.to(dev)
+    out = {}
+    for key, fn in (('clip', lambda: model(wd)['framewise_output']),
+                    ('window', lambda: inference.predict_windows(model, wd, 5, 1)),
+                    ('clip_host_to_host', lambda: model(w1.to(dev))['framewise_output'].cpu())):
+        with torch.no_grad():
+            for _ in range(3):
+                fn()
+            torch.cuda.synchronize()
+            ts = []
+            for _ in range(reps):
+                a = time.perf_counter()
+                fn()
+                torch.cuda.synchronize()
+                ts.append((time.perf_counter() - a) * 1e3)
+        out[key] = round(statistics.median(ts), 4)
+    out['unit'] = 'ms p50'
+    return out
 
 
 def measure(model, wave, args, world, rank, dev):
@@ -301,10 +335,11 @@ def main():
     extra = {}
     if args.mode == 'clip' and rank == 0 and not args.no_side:
         extra = side_measurements(model, wave, args, dev, stage_ms)
+        extra['latency_b1'] = latency_b1(model, dev)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(name, args.cpu_seconds)
+        cpu = cpu_baseline(name, args.cpu_seconds, model, dev)
 
     if rank == 0:
         line = {
