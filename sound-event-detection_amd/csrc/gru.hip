@@ -208,13 +208,21 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
 #pragma unroll
         for (int k2 = 0; k2 < 2; ++k2) {
           const int it = min(tid + 768 * k2, 32 * 32 - 1);
-          const unsigned long long* q =
-              reinterpret_cast<const unsigned long long*>(src + (it >> 5) * 256 + 8 * (it & 31));
+          // a partial group moves only its nc clips (nc/32 of the 32 KB; rows
+          // of absent clips are zero and never read back); a full group keeps
+          // the straight-line loads (nc is uniform: no divergence)
+          if (nc == 32 || (it >> 5) < nc) {
+            const unsigned long long* q =
+                reinterpret_cast<const unsigned long long*>(src + (it >> 5) * 256 + 8 * (it & 31));
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const unsigned long long w = __hip_atomic_load(q + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            vv[k2][2 * e] = __uint_as_float((uint32_t)w);
-            vv[k2][2 * e + 1] = __uint_as_float((uint32_t)(w >> 32));
+            for (int e = 0; e < 4; ++e) {
+              const unsigned long long w = __hip_atomic_load(q + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              vv[k2][2 * e] = __uint_as_float((uint32_t)w);
+              vv[k2][2 * e + 1] = __uint_as_float((uint32_t)(w >> 32));
+            }
+          } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) vv[k2][e] = 0.f;
           }
         }
 #pragma unroll
@@ -274,11 +282,14 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
             hvs[i] = n + z * (hprev[c][u] - n);
           }
           float* xp = dst + c * 256 + 32 * p + u;
-          if (fast)
+          if (c >= nc) {
+            // absent clip: nothing to publish
+          } else if (fast) {
             *xp = hvs[i];
-          else
+          } else {
             __hip_atomic_store(reinterpret_cast<unsigned*>(xp), __float_as_uint(hvs[i]),
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
         }
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
