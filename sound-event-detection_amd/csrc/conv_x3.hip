@@ -26,6 +26,10 @@
 //     the current stage keep the matrix pipes busy;
 //   * A/B fragments of tap t+1 are read from LDS (two register sets) while
 //     tap t's 12 MFMAs issue, across stage, chunk and tile boundaries.
+//   * all layers but the fused block 1 stream the weights by LDS-DMA
+//     instead (global_load_lds_dwordx4 straight into the slot freed by the
+//     barrier, one stage ahead; counted vmcnt + raw s_barrier): no weight
+//     VGPRs or ds_writes, ~40 fewer VGPRs, 1-2 % faster per layer.
 // The MFMA row -> pixel map is chosen per epilogue so that 2x2 pooling (and
 // the 8-bin freq mean) is an in-lane register sum.
 #include <algorithm>
@@ -58,6 +62,19 @@ __device__ __forceinline__ void split8(const float4 a, const float4 b, uint4& hi
 }
 
 __device__ __forceinline__ bf16x8 as_bf16x8(uint4 v) { return __builtin_bit_cast(bf16x8, v); }
+
+// LDS-DMA of 16 B per lane: LDS[m0 + lane * 16] = *src.  Inline asm, so the
+// compiler neither counts it nor guards LDS reads against it: the caller
+// orders it with counted vmcnt waits before its barriers (its own waits for
+// ordinary loads only get more conservative, never less).
+__device__ __forceinline__ void sedx_glds16(const void* src, uint32_t m0) {
+  // m0 is reserved to the compiler, which uses it nowhere else in this file
+  // (checked in the ISA); the clobber keeps it from caching a value there
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(m0) : "memory", "m0");
+#pragma clang diagnostic pop
+}
 
 // 4x4 transpose across the 4 lanes of a quad (j = lane & 3): on entry lane j
 // holds column j of a 4x4 block in v[0..3] (v[k] = row k), on exit row j
@@ -194,12 +211,25 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
   constexpr int A_ITEMS = FUSE ? RT * CS : 4 * RT * CS;
   constexpr int NA = (A_ITEMS + 511) / 512;
   constexpr int NW = (WS_U4 + 511) / 512;
+#ifndef SEDX_NO_GLDS_W
+  // weight stages go global -> LDS by LDS-DMA (global_load_lds_dwordx4): the
+  // host-prepared image is copied lane-linearly, no VGPR round trip, no
+  // ds_write pass.  A DMA issued after a stage barrier must land before the
+  // next one (2-slot ring), so each barrier waits on a counted vmcnt.
+  // (not FUSE: block 1 measured 2 % slower with it — its conv1 VALU work
+  // and conditional halo loads force vmcnt(0) at every barrier)
+  constexpr bool GW = !FUSE;
+#else
+  constexpr bool GW = false;
+#endif
 
-  // W ring first so every fragment read is (lane base VGPR) + immediate
-  __shared__ uint4 lds[2 * WS_U4 + 2 * A_U4];
+  // one LDS object per W slot and one for the halo images: every fragment
+  // read is (lane base VGPR) + immediate, and the compiler's alias scopes
+  // tell a DMA into one W slot apart from reads of the other slot / halo
+  __shared__ uint4 lds_w0[WS_U4], lds_w1[WS_U4], lds_a[2 * A_U4];
   __shared__ int s_tiles[4];              // claimed tile of the workgroup's k-th tile, at k & 3
-  uint4* const Wbuf = lds;
-  uint4* const Abuf = lds + 2 * WS_U4;
+  uint4* const Abuf = lds_a;
+#define SEDX_WSLOT(slot) ((slot) ? lds_w1 : lds_w0)
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -266,7 +296,7 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
   for (int mt = 0; mt < MT; ++mt) {
     int tl, f;
     rowmap<F, EPI>(wm * WM + mt * 32 + (lane & 31), tl, f);
-    const int p = 2 * WS_U4 + (tl * CSP + f) * 5 + h;
+    const int p = (tl * CSP + f) * 5 + h;
     abase[0][mt] = p;
     abase[1][mt] = p + A_U4;
     asm volatile("" : "+v"(abase[0][mt]));
@@ -395,11 +425,30 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
   }
 #define SEDX_STORE_W(rs, slot)                                                          \
   {                                                                                     \
-    uint4* dst_ = Wbuf + (slot) * WS_U4;                                                \
+    uint4* dst_ = SEDX_WSLOT(slot);                                                \
     _Pragma("unroll") for (int i = 0; i < NW; ++i)                                      \
       dst_[min(tid + i * 512, WS_U4 - 1)] = ((rs) == 0) ? rw0[i] : rw1[i];              \
     asm volatile("" ::: "memory"); /* before the refill loads are issued */             \
   }
+
+  // GW: W stage ky_ of unit c_ -> LDS slot `slot` (wave-uniform LDS base, lane x 16 B)
+  const int wv_ = __builtin_amdgcn_readfirstlane(wave);
+#define SEDX_DMA_W(c_, ky_, slot)                                                       \
+  {                                                                                     \
+    const uint4* src_ = wsp + (((int64_t)(c_).nb * nchunks + (c_).chunk) * 3 + (ky_)) * WS_U4 + tid; \
+    _Pragma("unroll") for (int i = 0; i < NW; ++i) {                                    \
+      if (WS_U4 % 512 == 0 || i * 512 + (wv_ << 6) < WS_U4) {                           \
+        const uint32_t m0_ = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(        \
+            (__attribute__((address_space(3))) uint4*)(SEDX_WSLOT(slot) + i * 512 + (wv_ << 6)))); \
+        sedx_glds16(src_ + i * 512, m0_);                                               \
+      }                                                                                 \
+    }                                                                                   \
+    asm volatile("" ::: "memory");                                                      \
+  }
+  // stage barrier under GW: this wave's DMAs older than its n_ youngest VMEM
+  // ops have landed, its LDS writes are done, then the workgroup barrier
+#define SEDX_BAR_VM(n_)                                                                 \
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(n_) : "memory")
 
   bf16x8 fa[2][2 * MT], fb[2][2 * NT];
   // fragments of tap a (0..8) of a unit whose halo is in A buffer `abuf`
@@ -407,14 +456,14 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
 #define SEDX_READ_FRAGS(set, abuf, wslot, tap_)                                         \
   {                                                                                     \
     constexpr int aoff_ = (((tap_) / 3) * CSP + ((tap_) % 3)) * 5;                      \
-    constexpr int woff_ = (wslot) * WS_U4 + ((tap_) % 3) * W_U4;                        \
+    constexpr int woff_ = ((tap_) % 3) * W_U4;                        \
     _Pragma("unroll") for (int mt = 0; mt < MT; ++mt) {                                 \
-      fa[set][2 * mt] = as_bf16x8(lds[abase[abuf][mt] + aoff_]);                        \
-      fa[set][2 * mt + 1] = as_bf16x8(lds[abase[abuf][mt] + aoff_ + 2]);                \
+      fa[set][2 * mt] = as_bf16x8(lds_a[abase[abuf][mt] + aoff_]);                        \
+      fa[set][2 * mt + 1] = as_bf16x8(lds_a[abase[abuf][mt] + aoff_ + 2]);                \
     }                                                                                   \
     _Pragma("unroll") for (int nt = 0; nt < NT; ++nt) {                                 \
-      fb[set][2 * nt] = as_bf16x8(lds[wbase[nt][0] + woff_]);                           \
-      fb[set][2 * nt + 1] = as_bf16x8(lds[wbase[nt][1] + woff_]);                       \
+      fb[set][2 * nt] = as_bf16x8(SEDX_WSLOT(wslot)[wbase[nt][0] + woff_]);                           \
+      fb[set][2 * nt + 1] = as_bf16x8(SEDX_WSLOT(wslot)[wbase[nt][1] + woff_]);                       \
     }                                                                                   \
     __builtin_amdgcn_sched_barrier(0);                                                  \
   }
@@ -532,6 +581,13 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
   // W(cur, row 2), W(n1, row 0) and halo(n1)
   load_bias(cur);
   SEDX_LOAD_A(cur);
+  if constexpr (GW) {
+    SEDX_DMA_W(cur, 0, 0);
+    SEDX_DMA_W(cur, 1, 1);
+    SEDX_STORE_A(0, cur);
+    SEDX_LOAD_A(n1);
+    SEDX_BAR_VM(NA);
+  } else {
   SEDX_LOAD_W(0, cur, 0);
   SEDX_LOAD_W(1, cur, 1);
   SEDX_STORE_A(0, cur);
@@ -549,6 +605,7 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
     SEDX_LOAD_W(1, n1, 0);
   }
   __syncthreads();
+  }
   SEDX_READ_FRAGS(0, 0, 0, 0);
 
   // One stage = taps 3KY..3KY+2 of the current unit (parity U: halo in A
@@ -606,7 +663,28 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
 // U^1 was last read by unit U-1 before its stage-2 barrier, and n1's inputs
 // were loaded two stages earlier.
 #define SEDX_STAGE_POST(U, KY, set)                                                     \
-  {                                                                                     \
+  if constexpr (GW) {                                                                   \
+    /* halo(n1) first (its loads are older than this stage's DMA), then the */          \
+    /* DMA of the stage after next into the slot just freed, then halo(n2)   */          \
+    SEDX_MFMA_PIECE(set, 0, 0);                                                         \
+    if ((KY) == 0) {                                                                    \
+      SEDX_ABL_STORE_A((U) ^ 1, n1);                                                    \
+    }                                                                                   \
+    SEDX_MFMA_PIECE(set, 0, 1);                                                         \
+    if ((KY) == 0) {                                                                    \
+      SEDX_DMA_W(cur, 2, U);                                                            \
+    } else if ((KY) == 1) {                                                             \
+      SEDX_DMA_W(n1, 0, ((U) + 1) & 1);                                                 \
+    } else {                                                                            \
+      if (tid == 0) claim_land();                                                       \
+      SEDX_DMA_W(n1, 1, U);                                                             \
+    }                                                                                   \
+    SEDX_MFMA_PIECE(set, 1, 0);                                                         \
+    if ((KY) == 0) {                                                                    \
+      SEDX_ABL_LOAD_A(n2);                                                              \
+    }                                                                                   \
+    SEDX_MFMA_REST(set);                                                                \
+  } else {                                                                              \
     SEDX_MFMA_PIECE(set, 0, 0);                                                         \
     if ((KY) == 0) {                                                                    \
       SEDX_ABL_STORE_W((U) & 1, U);                                                     \
@@ -651,7 +729,12 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
     SEDX_READ_FRAGS(((U) + 3 * (KY) + 2) & 1, U, ((U) + (KY)) & 1, 3 * (KY) + 2);       \
     SEDX_MFMAS(((U) + 3 * (KY) + 1) & 1);                                               \
     SEDX_ST_BEGIN();                                                                    \
-    SEDX_ABL_SYNC();                                                                    \
+    if constexpr (GW) {                                                                 \
+      /* KY 1: the halo loads of n2, issued after KY 0's DMA, stay in flight */          \
+      if ((KY) == 1) SEDX_BAR_VM(NA); else SEDX_BAR_VM(0);                              \
+    } else {                                                                            \
+      SEDX_ABL_SYNC();                                                                  \
+    }                                                                                   \
     SEDX_ST_END(st_bar);                                                                \
     SEDX_ST_VMWAIT();                                                                   \
     SEDX_STAGE_POST(U, KY, ((U) + 3 * (KY) + 2) & 1);                                   \
@@ -693,6 +776,9 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
 #undef SEDX_READ_FRAGS
 #undef SEDX_MFMAS
 #undef SEDX_LOAD_W
+#undef SEDX_DMA_W
+#undef SEDX_WSLOT
+#undef SEDX_BAR_VM
 #undef SEDX_STORE_W
 #undef SEDX_LOAD_A
 #undef SEDX_STORE_A
