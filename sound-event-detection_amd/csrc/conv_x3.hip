@@ -211,6 +211,8 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
   constexpr int A_ITEMS = FUSE ? RT * CS : 4 * RT * CS;
   constexpr int NA = (A_ITEMS + 511) / 512;
   constexpr int NW = (WS_U4 + 511) / 512;
+  // store instructions one epilogue issues per wave (all of them issue)
+  constexpr int EPI_NST = (EPI == EPI_FMEAN) ? 2 * MT * 2 : 4 * MT * 2;
 #ifndef SEDX_NO_GLDS_W
   // weight stages go global -> LDS by LDS-DMA (global_load_lds_dwordx4): the
   // host-prepared image is copied lane-linearly, no VGPR round trip, no
@@ -467,14 +469,21 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
     }                                                                                   \
     __builtin_amdgcn_sched_barrier(0);                                                  \
   }
+#ifdef SEDX_SETPRIO
+#define SEDX_PRIO(p) __builtin_amdgcn_s_setprio(p)
+#else
+#define SEDX_PRIO(p)
+#endif
 #define SEDX_MFMAS(set)                                                                 \
   {                                                                                     \
+    SEDX_PRIO(1);                                                                       \
     _Pragma("unroll") for (int mt = 0; mt < MT; ++mt)                                   \
     _Pragma("unroll") for (int nt = 0; nt < NT; ++nt) {                                 \
       acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[set][2 * mt], fb[set][2 * nt], acc[mt][nt], 0, 0, 0);     \
       acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[set][2 * mt], fb[set][2 * nt + 1], acc[mt][nt], 0, 0, 0); \
       acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[set][2 * mt + 1], fb[set][2 * nt], acc[mt][nt], 0, 0, 0); \
     }                                                                                   \
+    SEDX_PRIO(0);                                                                       \
   }
 
   // bias of the current tile's columns, loaded when the tile starts (a load
@@ -491,6 +500,16 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
     asm volatile("" : "+v"(lane_));
     const int h = lane_ >> 5;
     const int n0 = c.nb * BN;
+    // stores go through a buffer resource over this clip's output: every
+    // store instruction issues (rows past the end get an out-of-range offset,
+    // which the range check drops), so their count is static and the next
+    // stage barrier can leave them in flight (SEDX_EPI_VM)
+    const int64_t clip_floats = (EPI == EPI_POOL2)   ? (int64_t)(T / 2) * (F / 2) * Cout
+                                : (EPI == EPI_FMEAN) ? (int64_t)T * Cout
+                                                     : (int64_t)T * F * Cout;
+    const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
+        out + (int64_t)c.b * clip_floats, (short)0, (int)(clip_floats * 4), 0x00020000);
+    constexpr uint32_t OOB = 0x80000000u;
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
       const int n = n0 + wn * 64 + nt * 32 + (lane_ & 31);
@@ -523,7 +542,6 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
           // channels of one pixel: 4 dwordx4 stores instead of 16 dword stores,
           // same bytes, the same 128-B lines per group of stores
           const int j = lane_ & 3;
-          float* ob = out + ((int64_t)c.b * T + c.t0) * F * Cout + (n - j);
           const int tlim = T - c.t0;
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
@@ -531,8 +549,10 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
             quad_transpose4(v, j);
             int tl, f;
             rowmap<F, EPI>(Rbase + 8 * g + 4 * h + j, tl, f);
-            if (live && tl < tlim)
-              *reinterpret_cast<float4*>(ob + (tl * F + f) * Cout) = make_float4(v[0], v[1], v[2], v[3]);
+            const uint32_t off = (live && tl < tlim) ? (uint32_t)((((c.t0 + tl) * F + f) * Cout + n - j) * 4) : OOB;
+            typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+            const u32x4 w = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
+            __builtin_amdgcn_raw_buffer_store_b128(w, ors, off, 0, 0);
             __builtin_amdgcn_sched_barrier(0);
           }
 #endif
@@ -545,15 +565,18 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
             const int tp = q / FO, fp = q % FO;
             const int to = c.t0 / 2 + tp;
             const float v = (((r[4 * g] + r[4 * g + 1]) + r[4 * g + 2]) + r[4 * g + 3]) * 0.25f;
-            if (live && to < To) out[(((int64_t)c.b * To + to) * FO + fp) * Cout + n] = v;
+            const uint32_t off = (live && to < To) ? (uint32_t)(((to * FO + fp) * Cout + n) * 4) : OOB;
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), ors, off, 0, 0);
           }
         } else {  // EPI_FMEAN, F == 8: regs {0-3,12-15} and {4-11} are one t each (rowmap)
           const float sa = (((r[0] + r[1]) + (r[2] + r[3])) + ((r[12] + r[13]) + (r[14] + r[15])));
           const float sb = (((r[4] + r[5]) + (r[6] + r[7])) + ((r[8] + r[9]) + (r[10] + r[11])));
           const int tb = c.t0 + 4 * (Rbase >> 5);
           const int ta = tb + (h ? 3 : 0), tb2 = tb + (h ? 2 : 1);
-          if (live && ta < T) out[((int64_t)c.b * T + ta) * Cout + n] = sa * 0.125f;
-          if (live && tb2 < T) out[((int64_t)c.b * T + tb2) * Cout + n] = sb * 0.125f;
+          const uint32_t offa = (live && ta < T) ? (uint32_t)((ta * Cout + n) * 4) : OOB;
+          const uint32_t offb = (live && tb2 < T) ? (uint32_t)((tb2 * Cout + n) * 4) : OOB;
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(sa * 0.125f), ors, offa, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(sb * 0.125f), ors, offb, 0, 0);
         }
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc[mt][nt][i] = 0.0f;
@@ -731,7 +754,10 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
     SEDX_ST_BEGIN();                                                                    \
     if constexpr (GW) {                                                                 \
       /* KY 1: the halo loads of n2, issued after KY 0's DMA, stay in flight */          \
-      if ((KY) == 1) SEDX_BAR_VM(NA); else SEDX_BAR_VM(0);                              \
+      /* KY 0 after a tile's epilogue: its stores, issued after KY 2's DMA, too */ \
+      if ((KY) == 1) SEDX_BAR_VM(NA);                                                   \
+      else if ((KY) == 0 && epi_prev) SEDX_BAR_VM(EPI_NST);                            \
+      else SEDX_BAR_VM(0);                              \
     } else {                                                                            \
       SEDX_ABL_SYNC();                                                                  \
     }                                                                                   \
@@ -755,6 +781,7 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
       epilogue(cur);                                                                    \
       SEDX_ST_END(st_epi);                                                              \
     }                                                                                   \
+    epi_prev = cur.chunk == nchunks - 1;                                                \
     cur = n1;                                                                           \
     n1 = n2;                                                                            \
     advance(n2);                                                                        \
@@ -762,6 +789,7 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
     if (cur.chunk == 0) load_bias(cur);                                                 \
   }
 
+  bool epi_prev = false;
   while (true) {
     SEDX_UNIT(0);
     SEDX_UNIT(1);
