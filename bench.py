@@ -144,6 +144,11 @@ def measure(model, wave, args, world, rank, dev):
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
+    # per-stage HIP events over the timed region: libsedx records them on the
+    # stream each forward's kernels are launched on, one event set per
+    # forward (accumulate mode), averaged by sedx_stage_times afterwards
+    nat, L = model.native(dev), _lib.lib()
+    _lib.check(L.sedx_set_profiling(nat.h, 2), nat.h, 'set_profiling')
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -152,6 +157,11 @@ def measure(model, wave, args, world, rank, dev):
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    ms = (ctypes.c_float * len(_lib.STAGES))()
+    n = ctypes.c_int32()
+    _lib.check(L.sedx_stage_times(nat.h, ms, len(_lib.STAGES), ctypes.byref(n)), nat.h, 'stage_times')
+    _lib.check(L.sedx_set_profiling(nat.h, 0), nat.h, 'set_profiling')
+    timed_stage_ms = {s_: round(float(v), 4) for s_, v in zip(_lib.STAGES, ms[:])}
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -166,7 +176,7 @@ def measure(model, wave, args, world, rank, dev):
         torch.cuda.synchronize()
         lat.append((time.perf_counter() - a) * 1e3 / B)
     lat.sort()
-    return value, elapsed, statistics.median(lat), lat[min(len(lat) - 1, int(0.99 * len(lat)))]
+    return value, elapsed, statistics.median(lat), lat[min(len(lat) - 1, int(0.99 * len(lat)))], timed_stage_ms
 
 
 def stage_times(model, wave, dev, reps):
@@ -243,7 +253,8 @@ def roofline(stage_ms, B, precision):
             'flops_per_launch': flops, 'avg_launch_ms': conv[dom],
             'avg_launch_ms_rocprof': rocprof_ms,
             'mfma_busy_frac_pmc': mfma_util, 'clock_ghz_pmc': clock,
-            'timing': 'avg_launch_ms: HIP events on the launch stream (one batch at a time); '
+            'timing': 'avg_launch_ms: HIP events on the launch stream over the timed region '
+                      '(one event set per forward, all steps averaged); '
                       'avg_launch_ms_rocprof: rocprofv3 --kernel-trace --stats of this bench '
                       '(--streams 1 --no-side), committed summary',
             'conv_stack_tflops': round(total / (sum(conv.values()) * 1e-3) / 1e12, 2)}
@@ -318,23 +329,23 @@ def main():
     B = args.batch
     wave = torch.from_numpy(synth.make_waveforms(B, 10.0, 16000, seed=1234 + rank)).to(dev)
 
-    value, elapsed, p50, p99 = measure(model, wave, args, world, rank, dev)
-    stage_ms = roof = None
+    value, elapsed, p50, p99, stage_ms = measure(model, wave, args, world, rank, dev)
+    roof = stage_iso = None
     if args.mode == 'clip':
-        stage_ms = stage_times(model, wave, dev, max(3, min(args.steps, 10)))
         roof = roofline(stage_ms, B, args.precision)
+        stage_iso = stage_times(model, wave, dev, max(3, min(args.steps, 10)))
     exact = None
     if not args.no_exact and args.precision != 'exact':
         model.set_precision('exact')
-        ev, _, ep50, _ = measure(model, wave, args, world, rank, dev)
+        ev, _, ep50, _, est = measure(model, wave, args, world, rank, dev)
         exact = {'value': round(ev, 2), 'ms_per_clip_p50': round(ep50, 4)}
         if args.mode == 'clip':
-            exact['roofline'] = roofline(stage_times(model, wave, dev, 3), B, 'exact')
+            exact['roofline'] = roofline(est, B, 'exact')
         model.set_precision(args.precision)
 
     extra = {}
     if args.mode == 'clip' and rank == 0 and not args.no_side:
-        extra = side_measurements(model, wave, args, dev, stage_ms)
+        extra = side_measurements(model, wave, args, dev, stage_iso)
         extra['latency_b1'] = latency_b1(model, dev)
 
     cpu = None
@@ -358,6 +369,7 @@ def main():
                        'pipelined': args.streams > 1 and not args.no_pipeline},
             'ms_per_clip_p99': round(p99, 4),
             'roofline': roof, 'cpu_baseline': cpu, 'stage_ms': stage_ms,
+            'stage_ms_isolated': stage_iso,
             'value_exact_fp32': exact,
         }
         line.update(extra)

@@ -181,7 +181,11 @@ sedx_status sedx_set_pipelined(sedx_handle* h, int32_t on);
  * on its stream at the stage boundaries; sedx_stage_times waits for them and
  * returns milliseconds for: 0 frontend, 1 conv1 of block 1, 2..8 the seven
  * implicit-GEMM convs (b1c2, b2c1, b2c2, b3c1, b3c2, b4c1, b4c2), 9 GRU / MHA
- * incl. projections, 10 AttBlock head. */
+ * incl. projections, 10 AttBlock head.  on = 1: the last forward's times;
+ * on = 2 (accumulate): every forward records into its own event set (so
+ * forwards in flight on several streams time independently) and
+ * sedx_stage_times returns per-stage averages over all forwards since the
+ * previous call (or since profiling was switched on), then resets them. */
 #define SEDX_N_STAGES 11
 sedx_status sedx_set_profiling(sedx_handle* h, int32_t on);
 sedx_status sedx_stage_times(sedx_handle* h, float* ms, int32_t capacity, int32_t* n_stages);

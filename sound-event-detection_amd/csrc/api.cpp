@@ -83,7 +83,7 @@ struct sedx_handle {
   int precision = SEDX_PRECISION_X3;   // conv stack arithmetic (sedx_set_precision)
   bool gru_simple = getenv("SEDX_GRU_SIMPLE") != nullptr;   // A/B: per-(clip,dir) recurrence
   bool debug_x0 = getenv("SEDX_DEBUG_X0") != nullptr;      // diagnostic: X0 snapshot after the frontend
-  bool profiling = false;
+  int profiling = 0;          // 0 off, 1 last forward, 2 accumulate
   // sedx_set_pipelined: conv stacks of successive forwards run in issue order
   // (each waits for the previous one's conv-done event), whatever streams
   // they are issued on, so the sequence + head of batch i overlap the conv
@@ -93,12 +93,59 @@ struct sedx_handle {
   hipEvent_t conv_done = nullptr;
   hipEvent_t ev[SEDX_N_STAGES + 1] = {};
   bool ev_recorded[SEDX_N_STAGES + 1] = {};
+  // profiling mode 2 (accumulate): every forward takes its own event set from
+  // this pool, so forwards in flight on different streams time independently;
+  // sedx_stage_times folds the used sets into per-stage sums and averages
+  struct EvSet {
+    hipEvent_t ev[SEDX_N_STAGES + 1] = {};
+    bool rec[SEDX_N_STAGES + 1] = {};
+  };
+  std::vector<EvSet> ev_pool;
+  size_t ev_used = 0;
+  EvSet* ev_cur = nullptr;
+  double acc_ms[SEDX_N_STAGES] = {};
+  int64_t acc_n[SEDX_N_STAGES] = {};
 };
 
 
 namespace {
+// mode 2: sums the elapsed times of every used event set, frees the pool
+void fold_ev_pool(sedx_handle* h) {
+  for (size_t k = 0; k < h->ev_used; ++k) {
+    auto& e = h->ev_pool[k];
+    for (int i = 0; i < SEDX_N_STAGES; ++i) {
+      if (!e.rec[i] || !e.rec[i + 1]) continue;
+      float v = 0.f;
+      if (hipEventSynchronize(e.ev[i + 1]) == hipSuccess && hipEventElapsedTime(&v, e.ev[i], e.ev[i + 1]) == hipSuccess) {
+        h->acc_ms[i] += v;
+        ++h->acc_n[i];
+      }
+    }
+  }
+  h->ev_used = 0;
+  h->ev_cur = nullptr;
+}
+
 inline void mark(sedx_handle* h, int i, hipStream_t s) {
-  if (h->profiling && h->ev[i]) {
+  if (!h->profiling) return;
+  if (h->profiling == 2) {
+    if (i == 0) {                       // a forward starts: next event set
+      if (h->ev_used == 4096) fold_ev_pool(h);
+      if (h->ev_used == h->ev_pool.size()) {
+        h->ev_pool.emplace_back();
+        for (auto& e : h->ev_pool.back().ev)
+          if (hipEventCreate(&e) != hipSuccess) e = nullptr;
+      }
+      h->ev_cur = &h->ev_pool[h->ev_used++];
+      for (auto& r : h->ev_cur->rec) r = false;
+    }
+    if (h->ev_cur && h->ev_cur->ev[i]) {
+      (void)hipEventRecord(h->ev_cur->ev[i], s);
+      h->ev_cur->rec[i] = true;
+    }
+    return;
+  }
+  if (h->ev[i]) {
     (void)hipEventRecord(h->ev[i], s);
     h->ev_recorded[i] = true;
   }
@@ -442,6 +489,9 @@ void sedx_destroy(sedx_handle* h) {
     DeviceGuard g(h->device);
     for (auto& e : h->ev)
       if (e) (void)hipEventDestroy(e);
+    for (auto& set : h->ev_pool)
+      for (auto& e : set.ev)
+        if (e) (void)hipEventDestroy(e);
     if (h->conv_done) (void)hipEventDestroy(h->conv_done);
     if (h->blob) (void)hipFree(h->blob);
     if (h->ws) (void)hipFree(h->ws);
@@ -822,8 +872,16 @@ sedx_status sedx_set_profiling(sedx_handle* h, int32_t on) {
   DeviceGuard dg(h->device);
   if (on && !h->ev[0])
     for (auto& e : h->ev) HIP_TRY(h, hipEventCreate(&e));
-  h->profiling = on != 0;
+  if (on < 0 || on > 2) return fail(h, SEDX_EINVAL, "profiling mode %d (0 off, 1 last forward, 2 accumulate)", (int)on);
+  if (h->profiling == 2) fold_ev_pool(h);
+  h->profiling = on;
   for (auto& r : h->ev_recorded) r = false;
+  h->ev_used = 0;
+  h->ev_cur = nullptr;
+  for (int i = 0; i < SEDX_N_STAGES; ++i) {
+    h->acc_ms[i] = 0.0;
+    h->acc_n[i] = 0;
+  }
   return SEDX_OK;
 }
 
@@ -841,6 +899,15 @@ sedx_status sedx_stage_times(sedx_handle* h, float* ms, int32_t capacity, int32_
   *n_stages = SEDX_N_STAGES;
   if (!h->profiling) return fail(h, SEDX_ESTATE, "profiling is off");
   DeviceGuard dg(h->device);
+  if (h->profiling == 2) {
+    fold_ev_pool(h);
+    for (int i = 0; i < SEDX_N_STAGES; ++i) {
+      if (i < capacity) ms[i] = h->acc_n[i] ? (float)(h->acc_ms[i] / (double)h->acc_n[i]) : 0.f;
+      h->acc_ms[i] = 0.0;
+      h->acc_n[i] = 0;
+    }
+    return SEDX_OK;
+  }
   for (int i = 0; i < SEDX_N_STAGES && i < capacity; ++i) {
     float v = 0.f;
     if (h->ev_recorded[i] && h->ev_recorded[i + 1]) {

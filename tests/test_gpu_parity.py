@@ -260,3 +260,40 @@ def test_int16_waveform_input(mt):
         b = m(torch.from_numpy(q).cuda())
     for k in ('framewise_output', 'clipwise_output', 'embedding'):
         assert np.array_equal(a[k], b[k].cpu().numpy()), k
+
+
+def test_stage_times_accumulate():
+    """sedx_set_profiling(h, 2): one event set per forward, so forwards in
+    flight on two streams time independently; sedx_stage_times averages them
+    and resets.  Mode 1 still reports the last forward; bad modes fail."""
+    import ctypes
+    from sedx import _lib
+    m = build(GRU)
+    nat, L = m.native(torch.device('cuda', 0)), _lib.lib()
+    w = torch.from_numpy(synth.make_waveforms(4, seconds=2.0, sample_rate=16000, seed=3)).cuda()
+    ms = (ctypes.c_float * len(_lib.STAGES))()
+    n = ctypes.c_int32()
+    assert L.sedx_set_profiling(nat.h, 3) != 0
+    assert L.sedx_set_profiling(nat.h, 2) == 0
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    with torch.no_grad():
+        outs = []
+        for i in range(6):
+            with torch.cuda.stream(streams[i % 2]):
+                outs.append(m(w)['framewise_output'])
+    torch.cuda.synchronize()
+    assert L.sedx_stage_times(nat.h, ms, len(_lib.STAGES), ctypes.byref(n)) == 0
+    assert n.value == len(_lib.STAGES)
+    acc = list(ms[:])
+    assert all(v > 0 for v in acc), acc
+    # reset after the read: nothing recorded since
+    assert L.sedx_stage_times(nat.h, ms, len(_lib.STAGES), ctypes.byref(n)) == 0
+    assert all(v == 0 for v in ms[:])
+    assert L.sedx_set_profiling(nat.h, 1) == 0
+    with torch.no_grad():
+        m(w)
+    assert L.sedx_stage_times(nat.h, ms, len(_lib.STAGES), ctypes.byref(n)) == 0
+    assert all(v > 0 for v in ms[:])
+    assert L.sedx_set_profiling(nat.h, 0) == 0
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0])
