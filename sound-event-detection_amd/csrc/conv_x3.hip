@@ -469,6 +469,10 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
     }                                                                                   \
     __builtin_amdgcn_sched_barrier(0);                                                  \
   }
+// cache policy of the epilogue stores (A/B builds: -DSEDX_EPI_AUX=2 is nt)
+#ifndef SEDX_EPI_AUX
+#define SEDX_EPI_AUX 0
+#endif
 #ifdef SEDX_SETPRIO
 #define SEDX_PRIO(p) __builtin_amdgcn_s_setprio(p)
 #else
@@ -552,7 +556,7 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
             const uint32_t off = (live && tl < tlim) ? (uint32_t)((((c.t0 + tl) * F + f) * Cout + n - j) * 4) : OOB;
             typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
             const u32x4 w = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
-            __builtin_amdgcn_raw_buffer_store_b128(w, ors, off, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(w, ors, off, 0, SEDX_EPI_AUX);
             __builtin_amdgcn_sched_barrier(0);
           }
 #endif
@@ -566,7 +570,7 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
             const int to = c.t0 / 2 + tp;
             const float v = (((r[4 * g] + r[4 * g + 1]) + r[4 * g + 2]) + r[4 * g + 3]) * 0.25f;
             const uint32_t off = (live && to < To) ? (uint32_t)(((to * FO + fp) * Cout + n) * 4) : OOB;
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), ors, off, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), ors, off, 0, SEDX_EPI_AUX);
           }
         } else {  // EPI_FMEAN, F == 8: regs {0-3,12-15} and {4-11} are one t each (rowmap)
           const float sa = (((r[0] + r[1]) + (r[2] + r[3])) + ((r[12] + r[13]) + (r[14] + r[15])));
@@ -575,8 +579,8 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
           const int ta = tb + (h ? 3 : 0), tb2 = tb + (h ? 2 : 1);
           const uint32_t offa = (live && ta < T) ? (uint32_t)((ta * Cout + n) * 4) : OOB;
           const uint32_t offb = (live && tb2 < T) ? (uint32_t)((tb2 * Cout + n) * 4) : OOB;
-          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(sa * 0.125f), ors, offa, 0, 0);
-          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(sb * 0.125f), ors, offb, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(sa * 0.125f), ors, offa, 0, SEDX_EPI_AUX);
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(sb * 0.125f), ors, offb, 0, SEDX_EPI_AUX);
         }
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc[mt][nt][i] = 0.0f;
