@@ -504,15 +504,20 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
     asm volatile("" : "+v"(lane_));
     const int h = lane_ >> 5;
     const int n0 = c.nb * BN;
-    // stores go through a buffer resource over this clip's output: every
-    // store instruction issues (rows past the end get an out-of-range offset,
-    // which the range check drops), so their count is static and the next
-    // stage barrier can leave them in flight (SEDX_EPI_VM)
-    const int64_t clip_floats = (EPI == EPI_POOL2)   ? (int64_t)(T / 2) * (F / 2) * Cout
-                                : (EPI == EPI_FMEAN) ? (int64_t)T * Cout
-                                                     : (int64_t)T * F * Cout;
+    // stores go through a buffer resource over the clip's output from the
+    // tile's first row on: every store instruction issues (rows past the
+    // clip's end get an out-of-range offset, which the range check drops), so
+    // their count is static and the next stage barrier can leave them in
+    // flight (EPI_NST).  Offsets stay below one tile's rows (< 1 MB) and the
+    // record count is clamped to 2^31 - 1, so any clip length is safe.
+    constexpr int ROW = (EPI == EPI_POOL2) ? (F / 2) * 1 : (EPI == EPI_FMEAN) ? 1 : F;
+    const int T_out = (EPI == EPI_POOL2) ? T / 2 : T;
+    const int row0 = (EPI == EPI_POOL2) ? c.t0 / 2 : c.t0;
+    const int64_t clip_floats = (int64_t)T_out * ROW * Cout;
+    const int64_t rest_bytes = ((int64_t)(T_out - row0) * ROW * Cout) * 4;
     const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
-        out + (int64_t)c.b * clip_floats, (short)0, (int)(clip_floats * 4), 0x00020000);
+        out + (int64_t)c.b * clip_floats + (int64_t)row0 * ROW * Cout, (short)0,
+        (int)(rest_bytes < 0x7fffffff ? rest_bytes : 0x7fffffff), 0x00020000);
     constexpr uint32_t OOB = 0x80000000u;
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
@@ -553,7 +558,7 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
             quad_transpose4(v, j);
             int tl, f;
             rowmap<F, EPI>(Rbase + 8 * g + 4 * h + j, tl, f);
-            const uint32_t off = (live && tl < tlim) ? (uint32_t)((((c.t0 + tl) * F + f) * Cout + n - j) * 4) : OOB;
+            const uint32_t off = (live && tl < tlim) ? (uint32_t)(((tl * F + f) * Cout + n - j) * 4) : OOB;
             typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
             const u32x4 w = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
             __builtin_amdgcn_raw_buffer_store_b128(w, ors, off, 0, SEDX_EPI_AUX);
@@ -569,7 +574,7 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
             const int tp = q / FO, fp = q % FO;
             const int to = c.t0 / 2 + tp;
             const float v = (((r[4 * g] + r[4 * g + 1]) + r[4 * g + 2]) + r[4 * g + 3]) * 0.25f;
-            const uint32_t off = (live && to < To) ? (uint32_t)(((to * FO + fp) * Cout + n) * 4) : OOB;
+            const uint32_t off = (live && to < To) ? (uint32_t)(((tp * FO + fp) * Cout + n) * 4) : OOB;
             __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), ors, off, 0, SEDX_EPI_AUX);
           }
         } else {  // EPI_FMEAN, F == 8: regs {0-3,12-15} and {4-11} are one t each (rowmap)
@@ -577,8 +582,8 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
           const float sb = (((r[4] + r[5]) + (r[6] + r[7])) + ((r[8] + r[9]) + (r[10] + r[11])));
           const int tb = c.t0 + 4 * (Rbase >> 5);
           const int ta = tb + (h ? 3 : 0), tb2 = tb + (h ? 2 : 1);
-          const uint32_t offa = (live && ta < T) ? (uint32_t)((ta * Cout + n) * 4) : OOB;
-          const uint32_t offb = (live && tb2 < T) ? (uint32_t)((tb2 * Cout + n) * 4) : OOB;
+          const uint32_t offa = (live && ta < T) ? (uint32_t)(((ta - c.t0) * Cout + n) * 4) : OOB;
+          const uint32_t offb = (live && tb2 < T) ? (uint32_t)(((tb2 - c.t0) * Cout + n) * 4) : OOB;
           __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(sa * 0.125f), ors, offa, 0, SEDX_EPI_AUX);
           __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(sb * 0.125f), ors, offb, 0, SEDX_EPI_AUX);
         }
