@@ -201,7 +201,7 @@ def stage_times(model, wave, dev, reps):
 # command (tools/profile_round.sh -> tools/pmc_summary.py; FETCH_SIZE x2 per
 # the gfx950 correction + WRITE_SIZE), committed under profiles/.
 PROFILE_SUMMARY = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles',
-                               'r01i_kernel_summary.json')
+                               'r01j_kernel_summary.json')
 STAGE_KERNEL = {'b1c2': '<64, 64, 1', 'b2c1': '<32, 128, 0', 'b2c2': '<32, 128, 1',
                 'b3c1': '<16, 128, 0', 'b3c2': '<16, 128, 1', 'b4c1': '<8, 128, 0',
                 'b4c2': '<8, 128, 2'}
