@@ -94,6 +94,24 @@ def test_batch32_vs_oracle(model):
         assert e <= TOL * scale
 
 
+@pytest.mark.parametrize('seconds', [61.3])
+def test_long_clip_vs_oracle(model, seconds):
+    """A long, ragged clip (6131 frames: many t-tiles per clip, the last one
+    partial in every layer, odd frame counts before each pooling) against
+    the CPU oracle: the epilogues' per-tile store ranges and the
+    range-checked stores past a clip's end."""
+    mt, m = model
+    wave = synth.make_waveforms(2, seconds=seconds, sample_rate=16000, seed=77)
+    out = run(m, wave)
+    ref = O.forward(O.full_state(synth.make_state_dict(mt, seed=SEEDS[mt])), mt, wave=wave)
+    for k in ('framewise_output', 'clipwise_output'):
+        scale = max(1.0, float(ref[k].abs().max()))
+        e = err(out[k], ref[k].numpy())
+        print(mt, 'long', k, out[k].shape, 'max|d| =', e)
+        assert out[k].shape == tuple(ref[k].shape)
+        assert e <= TOL * scale
+
+
 def test_batch_invariance(model):
     """A clip's output does not depend on the batch it runs in."""
     mt, m = model
