@@ -874,6 +874,12 @@ sedx_status sedx_set_profiling(sedx_handle* h, int32_t on) {
     for (auto& e : h->ev) HIP_TRY(h, hipEventCreate(&e));
   if (on < 0 || on > 2) return fail(h, SEDX_EINVAL, "profiling mode %d (0 off, 1 last forward, 2 accumulate)", (int)on);
   if (h->profiling == 2) fold_ev_pool(h);
+  // mode 2: event sets for the first 64 forwards up front, so a timed loop
+  // does not create events on the host while it issues work
+  while (on == 2 && h->ev_pool.size() < 64) {
+    h->ev_pool.emplace_back();
+    for (auto& e : h->ev_pool.back().ev) HIP_TRY(h, hipEventCreate(&e));
+  }
   h->profiling = on;
   for (auto& r : h->ev_recorded) r = false;
   h->ev_used = 0;
