@@ -1,0 +1,43 @@
+"""bench.py host logic (no GPU): the algorithmic FLOP counts behind
+roofline.achieved (26.03 GFLOP of conv per 10 s clip) and
+the roofline record built from per-stage times."""
+import importlib.util
+import os
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope='module')
+def bench():
+    spec = importlib.util.spec_from_file_location('bench_mod', os.path.join(REPO, 'bench.py'))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_conv_flops_per_clip(bench):
+    T = 160000 // 160 + 1
+    per_clip = sum(bench.conv_flops(s, 1, T) for s in bench.CONV_STAGES)
+    # the seven implicit-GEMM convs; SURVEY §8(a) a7's 26.03 GF also holds
+    # block 1's conv1 (Cin 1, 0.07 GF), hence the 1 % band
+    assert abs(bench.conv_flops('b2c2', 1, T) - 2 * 500 * 32 * 128 * 9 * 128) < 1
+    assert abs(bench.conv_flops('b4c2', 1, T) - 2 * 125 * 8 * 512 * 9 * 512) < 1
+    assert abs(per_clip - 26.03e9) / 26.03e9 < 0.01
+
+
+def test_roofline_record(bench):
+    stage = {s: 0.2 for s in bench.CONV_STAGES}
+    stage['b1c2'] = 0.4
+    r = bench.roofline(stage, 32, 'x3')
+    assert r['bound'] == 'mfma' and r['unit'] == 'TFLOP/s'
+    assert r['kernel'].endswith('(b1c2)')
+    T = 1001
+    flops = bench.conv_flops('b1c2', 32, T) + 2.0 * 32 * T * 64 * 64 * 9
+    assert r['flops_per_launch'] == flops
+    assert abs(r['achieved'] - flops / 0.4e-3 / 1e12) < 0.01
+    assert abs(r['frac'] - r['achieved'] / r['peak']) < 1e-3
+    assert r['peak'] == round(2500.0 / 3, 1)
+    e = bench.roofline(stage, 32, 'exact')
+    assert e['peak'] == 157.3 and 'fp32' in e['arith']
