@@ -1,18 +1,30 @@
 """Benchmark of the MI355X-native SED inference path (BASELINE.json metric).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--model gru|transformer]
-                    [--mode clip|window] [--batch 32] [--precision x3|exact]
-                    [--no-cpu-baseline] [--no-exact]
+                    [--mode clip|window] [--batch 32] [--precision exact|x3]
+                    [--no-cpu-baseline] [--no-side]
 
 One step = one forward of the hot path over one batch of synthetic 10 s @
 16 kHz clips per GPU (clip mode = main_strong inference_prob semantics, B=32
 per GPU: BASELINE.json configs[1]), inputs already resident in HBM, weights
-random-init with the reference architecture.  For N > 1 (launched by
-torch.distributed.run, one process per GPU) every rank runs its own shard of
-clips (weak scaling) and the framewise outputs are gathered to rank 0 over
-RCCL inside each step — the path's only collective.  Rank 0 prints ONE JSON
-line.  The headline uses the default conv arithmetic (3xbf16-split MFMA, fp32
-accumulate); the exact fp32-MFMA mode is timed beside it (value_exact_fp32).
+random-init with the reference architecture.  The headline runs the
+reference's arithmetic: fp32 operands and fp32 accumulation for every GEMM
+(conv stack on v_mfma_f32_32x32x2_f32, GRU recurrence on fp32 MFMA).  For
+N > 1 (launched by torch.distributed.run, one process per GPU) every rank
+runs its own shard of clips (weak scaling) and the framewise outputs are
+gathered to rank 0 over RCCL inside each step — the path's only collective.
+Rank 0 prints ONE JSON line.
+
+At N = 1 the line also carries, each with its own roofline:
+  value_x3            the same workload with the opt-in 3xbf16-split MFMA
+  configs.config3     Cnn_9layers_Transformer_FrameAtt logmel 16k, B=32
+  configs.config4     Cnn_9layers_Gru_FrameAtt gammatone 32k, B=32 (float64
+                      gammatone features from 32 kHz audio + the forward)
+  configs.window_mode predict.py semantics, 6 x 5 s windows per clip
+  cpu_baseline        the oracle (CPU restatement) at B=32 on the host cores,
+                      clip mode and predict.py's batch-1 window loop, with the
+                      parity of the same clips (framewise, event lists,
+                      threshold margin)
 """
 import argparse
 import ctypes
@@ -34,15 +46,21 @@ import torch.distributed as dist  # noqa: E402
 
 from sedx import _lib, distributed, inference, models, synth  # noqa: E402
 
-METRIC = '10s@16kHz clips/sec (whole node) + ms/clip p50, Cnn_9_Gru_FrameAtt logmel'
+MODEL_NAMES = {'gru': 'Cnn_9layers_Gru_FrameAtt', 'transformer': 'Cnn_9layers_Transformer_FrameAtt'}
+METRICS = {'gru': '10s@16kHz clips/sec (whole node) + ms/clip p50, Cnn_9_Gru_FrameAtt logmel',
+           'transformer': '10s@16kHz clips/sec (whole node) + ms/clip p50, Cnn_9_Transformer_FrameAtt logmel'}
 # MI355X_MICROARCH.md: FP32 matrix peak 157.3 TF; BF16 dense MFMA ~2.5 PF.  The
 # x3 scheme issues 3 bf16 MFMAs per useful MAC, so its arithmetic peak is 2.5/3 PF.
 PEAK_TF = {'exact': 157.3, 'x3': 2500.0 / 3}
-MODEL_NAMES = {'gru': 'Cnn_9layers_Gru_FrameAtt', 'transformer': 'Cnn_9layers_Transformer_FrameAtt'}
+PEAK_HBM_GBPS = 8000.0
+PEAK_FP64_TF = 78.6        # MI355X datasheet FP64 vector (not in MI355X_MICROARCH.md)
+DTYPE = {'exact': 'f32',
+         'x3': 'bf16x3-split (3 bf16 MFMAs per f32 MAC: hi*hi + hi*lo + lo*hi, f32 accumulate)'}
 # conv stages of sedx_stage_times: (F, Cin, Cout, number of 2x poolings before it)
 CONV_STAGES = {'b1c2': (64, 64, 64, 0), 'b2c1': (32, 64, 128, 1), 'b2c2': (32, 128, 128, 1),
                'b3c1': (16, 128, 256, 2), 'b3c2': (16, 256, 256, 2), 'b4c1': (8, 256, 512, 3),
                'b4c2': (8, 512, 512, 3)}
+FRONTEND_BYTES_PER_CLIP = 160000 * 4 + 1001 * 64 * 4   # waveform in + X0 out
 
 
 def conv_flops(stage, B, T):
@@ -52,8 +70,8 @@ def conv_flops(stage, B, T):
     return 2.0 * B * T * F * cout * 9 * cin
 
 
-def build_model(name, device):
-    m = getattr(models, name)(16000, 512, 160, 64, 25, 7000, 25, 'logmel')
+def build_model(name, device, preset=(16000, 512, 160, 64, 25, 7000), feature='logmel'):
+    m = getattr(models, name)(*preset, 25, feature)
     sd = m.state_dict()
     for k, v in synth.make_state_dict(name, seed=0).items():
         sd[k] = torch.from_numpy(v)
@@ -61,36 +79,186 @@ def build_model(name, device):
     return m.to(device).eval()
 
 
-def cpu_baseline(name, seconds, model=None, dev=None):
-    """Oracle (CPU restatement, torch fp32, reference op sequence) on a bounded
-    sample: B=4 clips of 10 s per iteration, repeated for ~``seconds``.  With
-    ``model`` the same 4 clips also go through the GPU path and the oracle's
-    output is the checker: max |d framewise| is reported beside the rate."""
+# ---------------------------------------------------------------------------
+# CPU baseline: the oracle (test infrastructure) on the host cores
+# ---------------------------------------------------------------------------
+def cpu_info():
+    model, logical, cores = None, os.cpu_count(), set()
+    try:
+        phys = core = None
+        with open('/proc/cpuinfo') as f:
+            for line in f:
+                k, _, v = line.partition(':')
+                k, v = k.strip(), v.strip()
+                if k == 'model name' and model is None:
+                    model = v
+                elif k == 'physical id':
+                    phys = v
+                elif k == 'core id':
+                    core = v
+                elif not k and phys is not None:
+                    cores.add((phys, core))
+                    phys = core = None
+    except OSError:
+        pass
+    return {'cpu_model': model, 'host_logical_cpus': logical,
+            'host_physical_cores': len(cores) or None}
+
+
+def cpu_baseline(name, model, dev, seconds, B=32):
+    """Clip mode: the oracle forward on B=32 clips per iteration (1 warm-up,
+    then timed iterations for ~``seconds``).  The same clips go through the
+    GPU path; the oracle is the checker: max |d framewise|, event lists
+    (frame_prediction_to_event_prediction_v2 on both sides) and the smallest
+    distance of any oracle value to a threshold."""
     from oracle import sed_oracle as O
     sd = O.full_state(synth.make_state_dict(name, seed=0), '16k')
-    wave = synth.make_waveforms(4, seconds=10.0, sample_rate=16000, seed=7)
-    O.forward(sd, name, wave=wave[:1])  # warm-up
-    n, t0 = 0, time.perf_counter()
+    wave = synth.make_waveforms(B, seconds=10.0, sample_rate=16000, seed=7)
+    O.forward(sd, name, wave=wave[:2])  # warm-up (allocator, threads)
+    ts, ref = [], None
+    t_all = time.perf_counter()
     while True:
+        a = time.perf_counter()
         ref = O.forward(sd, name, wave=wave)
-        n += 4
-        el = time.perf_counter() - t0
-        if el >= seconds or n >= 400:
+        ts.append(time.perf_counter() - a)
+        if time.perf_counter() - t_all >= seconds and len(ts) >= 2:
             break
-    out = {'value': n / el, 'unit': 'clips/s', 'cores': torch.get_num_threads(), 'kind': 'port',
-           'sample': '%d x 10 s clips (B=4 per iteration, %.1f s) through oracle/sed_oracle.py '
-                     'forward on the host CPU' % (n, el)}
-    if model is not None:
-        with torch.no_grad():
-            fw = model(torch.from_numpy(wave).to(dev))['framewise_output'].cpu().numpy()
-        out['parity_max_abs_framewise'] = float(np.max(np.abs(fw - ref['framewise_output'].numpy())))
-        out['parity_tolerance'] = 1e-3
+    rate = B * len(ts) / sum(ts)
+    out = {'value': round(rate, 3), 'unit': 'clips/s', 'cores': torch.get_num_threads(), 'kind': 'port',
+           'ms_per_clip_p50': round(statistics.median(ts) / B * 1e3, 2),
+           'sample': '%d iterations of B=%d x 10 s clips (clip mode, %.1f s) through oracle/sed_oracle.py '
+                     'forward (torch fp32, the reference op sequence) on %d host threads'
+                     % (len(ts), B, sum(ts), torch.get_num_threads())}
+    out.update(cpu_info())
+    with torch.no_grad():
+        fw = model(torch.from_numpy(wave).to(dev))['framewise_output']
+    gfw = fw.cpu().numpy()
+    rfw = ref['framewise_output'].numpy()
+    params = dict(inference.DEFAULT_PREDICT_PARAMS)
+    ev_gpu = inference.events_from_framewise(fw, params)
+    ev_ref = O.events_from_framewise(rfw, params)
+    thr = np.array([params['sed_high_threshold'], params['sed_low_threshold']], np.float64)
+    out['parity'] = {
+        'max_abs_framewise': float(np.max(np.abs(gfw - rfw))), 'tolerance': 1e-3,
+        'events_identical': ev_gpu == ev_ref, 'n_events': len(ev_ref),
+        'min_threshold_margin': float(np.min(np.abs(rfw.astype(np.float64)[..., None] - thr))),
+        'thresholds': {'high': params['sed_high_threshold'], 'low': params['sed_low_threshold']},
+        'sample': '%d clips, GPU (this precision) vs oracle' % B}
     return out
+
+
+def cpu_baseline_window(name, seconds, max_clips=16):
+    """predict.py's loop (pytorch/predict.py:297-349): every 10 s clip as six
+    batch-1 forwards of 5 s windows at 1 s stride, merged and averaged, then
+    thresholded — the oracle restatement of that loop, timed per clip."""
+    from oracle import sed_oracle as O
+    sd = O.full_state(synth.make_state_dict(name, seed=0), '16k')
+    audio = synth.make_waveforms(max_clips, seconds=10.0, sample_rate=16000, seed=9)
+    O.predict_windows(sd, name, audio[0], 16000)   # warm-up
+    ts = []
+    t_all = time.perf_counter()
+    for i in range(max_clips):
+        a = time.perf_counter()
+        merged = O.predict_windows(sd, name, audio[i], 16000, 5, 1)
+        O.events_from_framewise(merged, inference.DEFAULT_PREDICT_PARAMS)
+        ts.append(time.perf_counter() - a)
+        if time.perf_counter() - t_all >= seconds and len(ts) >= 3:
+            break
+    return {'value': round(len(ts) / sum(ts), 3), 'unit': 'clips/s', 'cores': torch.get_num_threads(),
+            'kind': 'port', 'ms_per_clip_p50': round(statistics.median(ts) * 1e3, 1),
+            'sample': '%d x 10 s clips through oracle predict_windows (6 batch-1 5 s windows, '
+                      'merge + avg_merge) + events, %.1f s' % (len(ts), sum(ts))}
+
+
+# ---------------------------------------------------------------------------
+# GPU measurement
+# ---------------------------------------------------------------------------
+def measure(step, args, world, dev, model=None, B=32):
+    """Throughput over K steps with ``args.streams`` batches in flight: step i
+    is issued on stream i % streams (a serving loop with that many concurrent
+    requests), so one batch's GRU / MHA + head overlap the next batch's conv
+    stack.  Every step is a complete forward of its own batch.  Returns
+    (clips/s over all ranks, elapsed s, per-stage ms over the timed region)."""
+    streams = [torch.cuda.Stream(dev) for _ in range(max(1, args.streams))]
+    if model is not None:
+        # conv stacks in issue order (sedx_set_pipelined): without it the
+        # batches in flight can fall into lockstep, two conv stacks splitting
+        # the chip and the GRUs running side by side on 32 CUs
+        model.set_pipelined(len(streams) > 1 and not args.no_pipeline)
+    torch.cuda.synchronize()
+    for i in range(args.warmup):
+        with torch.cuda.stream(streams[i % len(streams)]):
+            step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    nat = L = None
+    if model is not None:
+        # per-stage HIP events over the timed region: libsedx records them on
+        # the stream each forward's kernels are launched on, one event set per
+        # forward (accumulate mode), averaged by sedx_stage_times afterwards
+        nat, L = model.native(dev), _lib.lib()
+        _lib.check(L.sedx_set_profiling(nat.h, 2), nat.h, 'set_profiling')
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        with torch.cuda.stream(streams[i % len(streams)]):
+            step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    stage_ms = None
+    if model is not None:
+        ms = (ctypes.c_float * len(_lib.STAGES))()
+        n = ctypes.c_int32()
+        _lib.check(L.sedx_stage_times(nat.h, ms, len(_lib.STAGES), ctypes.byref(n)), nat.h, 'stage_times')
+        _lib.check(L.sedx_set_profiling(nat.h, 0), nat.h, 'set_profiling')
+        stage_ms = {s_: round(float(v), 4) for s_, v in zip(_lib.STAGES, ms[:])}
+        model.set_pipelined(False)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return world * B * args.steps / elapsed, elapsed, stage_ms
+
+
+def latency(step_fn, B, reps):
+    """p50 / p99 of (batch wall time / clips), one batch at a time."""
+    lat = []
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        a = time.perf_counter()
+        step_fn()
+        torch.cuda.synchronize()
+        lat.append((time.perf_counter() - a) * 1e3 / B)
+    lat.sort()
+    return statistics.median(lat), lat[min(len(lat) - 1, int(0.99 * len(lat)))]
+
+
+def host_to_host_step(model, host_wave, host_out, dev, world, rank):
+    """One batch from host-visible (pinned) input to the gathered framewise
+    output back in pinned host memory on rank 0 (SURVEY §8(d) p50 definition):
+    the H2D copy runs on a copy stream and the compute stream waits for it."""
+    copy = torch.cuda.Stream(dev)
+
+    def step():
+        with torch.cuda.stream(copy):
+            d = host_wave.to(dev, non_blocking=True)
+        torch.cuda.current_stream(dev).wait_stream(copy)
+        d.record_stream(torch.cuda.current_stream(dev))
+        with torch.no_grad():
+            fw = model(d)['framewise_output']
+        if world > 1:
+            fw = distributed.gather_to_rank0(fw, world, rank)
+        if rank == 0:
+            host_out.copy_(fw, non_blocking=True)
+    return step
 
 
 def latency_b1(model, dev, reps=20):
     """End-to-end latency of ONE 10 s clip: clip mode and
-    window mode (its 6 windows in one launch), input already on the device;
+    window mode (its 6 windows in one launch) with the input on the device,
     and clip mode from a host buffer to the framewise output back on the
     host (PCIe-inclusive)."""
     w1 = torch.from_numpy(synth.make_waveforms(1, seconds=10.0, sample_rate=16000, seed=11))
@@ -114,76 +282,9 @@ def latency_b1(model, dev, reps=20):
     return out
 
 
-def measure(model, wave, args, world, rank, dev):
-    """Throughput over K steps with ``args.streams`` batches in flight: step i
-    is issued on stream i % streams (a serving loop with that many concurrent
-    requests), so one batch's GRU recurrence — 16 CUs for ~0.5 ms — overlaps
-    the next batch's conv stack.  Every step is a complete forward of its own
-    batch.  Latency (p50/p99 ms per clip) is then taken one step at a time on
-    a single stream."""
-    B = wave.shape[0]
-    streams = [torch.cuda.Stream(dev) for _ in range(max(1, args.streams))]
-    # conv stacks in issue order (sedx_set_pipelined): without it the batches
-    # in flight can fall into lockstep, two conv stacks splitting the chip and
-    # the GRUs running side by side on 32 CUs (measured: ~10 % slower runs)
-    model.set_pipelined(len(streams) > 1 and not args.no_pipeline)
-
-    def step(st=None):
-        with torch.no_grad(), torch.cuda.stream(st or torch.cuda.current_stream(dev)):
-            if args.mode == 'clip':
-                fw = model(wave)['framewise_output']
-            else:
-                fw = inference.predict_windows(model, wave, 5, 1)
-            if world > 1:
-                distributed.gather_to_rank0(fw, world, rank)
-        return fw
-
-    torch.cuda.synchronize()
-    for i in range(args.warmup):
-        step(streams[i % len(streams)])
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    # per-stage HIP events over the timed region: libsedx records them on the
-    # stream each forward's kernels are launched on, one event set per
-    # forward (accumulate mode), averaged by sedx_stage_times afterwards
+def stage_times_isolated(model, wave, dev, reps):
+    """Per-stage device time one batch at a time (sedx_set_profiling mode 1)."""
     nat, L = model.native(dev), _lib.lib()
-    _lib.check(L.sedx_set_profiling(nat.h, 2), nat.h, 'set_profiling')
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(streams[i % len(streams)])
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    ms = (ctypes.c_float * len(_lib.STAGES))()
-    n = ctypes.c_int32()
-    _lib.check(L.sedx_stage_times(nat.h, ms, len(_lib.STAGES), ctypes.byref(n)), nat.h, 'stage_times')
-    _lib.check(L.sedx_set_profiling(nat.h, 0), nat.h, 'set_profiling')
-    timed_stage_ms = {s_: round(float(v), 4) for s_, v in zip(_lib.STAGES, ms[:])}
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    value = world * B * args.steps / elapsed
-    model.set_pipelined(False)
-    lat = []
-    for _ in range(max(5, min(args.steps, 20))):
-        torch.cuda.synchronize()
-        a = time.perf_counter()
-        step()
-        torch.cuda.synchronize()
-        lat.append((time.perf_counter() - a) * 1e3 / B)
-    lat.sort()
-    return value, elapsed, statistics.median(lat), lat[min(len(lat) - 1, int(0.99 * len(lat)))], timed_stage_ms
-
-
-def stage_times(model, wave, dev, reps):
-    """Per-stage device time: HIP events recorded by libsedx on the stream the
-    kernels are launched on (sedx_set_profiling / sedx_stage_times)."""
-    nat = model.native(dev)
-    L = _lib.lib()
     _lib.check(L.sedx_set_profiling(nat.h, 1), nat.h, 'set_profiling')
     acc = np.zeros(len(_lib.STAGES))
     for _ in range(reps):
@@ -197,80 +298,156 @@ def stage_times(model, wave, dev, reps):
     return {s: round(float(v), 4) for s, v in zip(_lib.STAGES, acc / reps)}
 
 
-# HBM traffic per launch comes from the rocprofv3 PMC passes of this bench
-# command (tools/profile_round.sh -> tools/pmc_summary.py; FETCH_SIZE x2 per
-# the gfx950 correction + WRITE_SIZE), committed under profiles/.
-PROFILE_SUMMARY = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles',
-                               'r01j_kernel_summary.json')
-STAGE_KERNEL = {'b1c2': '<64, 64, 1', 'b2c1': '<32, 128, 0', 'b2c2': '<32, 128, 1',
-                'b3c1': '<16, 128, 0', 'b3c2': '<16, 128, 1', 'b4c1': '<8, 128, 0',
-                'b4c2': '<8, 128, 2'}
-# x3 kernels carry a 4th template argument (FUSE: block 1's conv1 fused into b1c2)
-STAGE_FUSE = {'b1c2': 'true'}
+# ---------------------------------------------------------------------------
+# rooflines
+# ---------------------------------------------------------------------------
+# HBM traffic per launch, rocprof average duration, MFMA busy and clock come
+# from the rocprofv3 passes of this bench command (tools/profile_round.sh ->
+# tools/pmc_summary.py; FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE),
+# committed under profiles/.
+PROFILE_SUMMARY = os.path.join(REPO, 'profiles', 'r02_kernel_summary.json')
+
+
+# block 1's conv1 (Cin 1 -> 64) computed inside the b1c2 launch
+FUSED_BLOCK1 = {'x3': True, 'exact': False}
+
+
+def conv_kernel_name(stage, precision):
+    """rocprof kernel name of a conv stage's launch."""
+    F, cin, cout, _ = CONV_STAGES[stage]
+    epi = {'b1c2': 1, 'b2c1': 0, 'b2c2': 1, 'b3c1': 0, 'b3c2': 1, 'b4c1': 0, 'b4c2': 2}[stage]
+    bn = 64 if cout == 64 else 128
+    if precision == 'x3':
+        return 'sedx::conv3x3_x3_kernel<%d, %d, %d, %s>' % (F, bn, epi, 'true' if stage == 'b1c2' else 'false')
+    return 'sedx::conv3x3_kernel<%d, %d, %d>' % (F, bn, epi)
 
 
 def profiled(kernel):
-    """(HBM bytes per launch, rocprofv3 average duration in ms, MFMA busy
-    fraction, effective clock GHz) of ``kernel`` from the committed profile
-    summary (None where absent)."""
+    """(HBM bytes per launch, rocprofv3 average ms, MFMA busy fraction,
+    effective clock GHz) of ``kernel`` from the committed summary."""
     try:
         with open(PROFILE_SUMMARY) as f:
             v = json.load(f).get(kernel, {})
-        ns = v.get('avg_ns')
-        util, clk = v.get('mfma_util'), v.get('clock_ghz')
-        return (v.get('hbm_bytes_corrected'), (round(ns * 1e-6, 4) if ns else None),
-                round(util, 4) if util else None, round(clk, 3) if clk else None)
     except (OSError, ValueError):
         return None, None, None, None
+    ns = v.get('avg_ns')
+    util, clk = v.get('mfma_util'), v.get('clock_ghz')
+    return (v.get('hbm_bytes_corrected'), (round(ns * 1e-6, 4) if ns else None),
+            round(util, 4) if util else None, round(clk, 3) if clk else None)
 
 
-def roofline(stage_ms, B, precision):
-    T = 160000 // 160 + 1
+def roofline(stage_ms, B, precision, T=1001):
+    """MFMA roofline of the dominant conv launch: algorithmic FLOPs per launch
+    (2 B T F Cout 9 Cin, + the fused block-1 conv1 2 B T 64 64 9 for b1c2) over
+    its HIP-event launch time in the timed region.  Profile-derived fields
+    (traffic, rocprof time, MFMA busy) come from the committed summary of the
+    B=32, 10 s shapes only."""
     conv = {s: stage_ms[s] for s in CONV_STAGES}
     dom = max(conv, key=conv.get)
     flops = conv_flops(dom, B, T)
-    if precision == 'x3' and dom == 'b1c2':
-        # the fused block-1 launch also computes conv1 (Cin 1 -> 64, 9 taps) for
-        # every conv2 input pixel it stages: 2 * B * T * 64 * 64 * 9 flops
-        flops += 2.0 * B * T * 64 * 64 * 9
+    if dom == 'b1c2' and FUSED_BLOCK1[precision]:
+        flops += 2.0 * B * T * 64 * 64 * 9      # conv1 (Cin 1 -> 64) computed inside the launch
     achieved = flops / (conv[dom] * 1e-3) / 1e12
     peak = PEAK_TF[precision]
-    total = sum(conv_flops(s, B, T) for s in CONV_STAGES)
-    if precision == 'x3':
-        kname = 'sedx::conv3x3_x3_kernel%s, %s>' % (STAGE_KERNEL[dom], STAGE_FUSE.get(dom, 'false'))
-    else:
-        kname = 'sedx::conv3x3_kernel%s>' % STAGE_KERNEL[dom]
-    traffic, rocprof_ms, mfma_util, clock = profiled(kname) if B == 32 else (None, None, None, None)
-    return {'bound': 'mfma',
-            'kernel': 'conv3x3_%s (%s)' % ('x3_kernel' if precision == 'x3' else 'kernel', dom),
-            'arith': '3xbf16-split MFMA 32x32x16, fp32 acc (peak = bf16 dense 2.5 PF / 3)'
-                     if precision == 'x3' else 'fp32 MFMA 32x32x2',
+    total = sum(conv_flops(s, B, T) for s in CONV_STAGES) + 2.0 * B * T * 64 * 64 * 9
+    conv_ms = sum(conv.values()) + stage_ms.get('b1c1', 0.0)
+    kname = conv_kernel_name(dom, precision)
+    traffic, rocprof_ms, mfma_util, clock = profiled(kname) if (B, T) == (32, 1001) else (None,) * 4
+    return {'bound': 'mfma', 'kernel': '%s (%s)' % (kname, dom),
+            'arith': {'exact': 'fp32 MFMA v_mfma_f32_32x32x2_f32 (f32 in, f32 acc)',
+                      'x3': '3xbf16-split MFMA 32x32x16, f32 acc (peak = bf16 dense 2.5 PF / 3)'}[precision],
             'achieved': round(achieved, 2), 'peak': round(peak, 1), 'unit': 'TFLOP/s',
             'frac': round(achieved / peak, 4),
             'traffic': traffic, 'traffic_unit': 'bytes/launch (HBM, rocprofv3 PMC)',
-            'traffic_source': os.path.relpath(PROFILE_SUMMARY, os.path.dirname(os.path.abspath(__file__)))
-            if traffic is not None else None,
+            'traffic_source': os.path.relpath(PROFILE_SUMMARY, REPO) if traffic is not None else None,
             'flops_per_launch': flops, 'avg_launch_ms': conv[dom],
             'avg_launch_ms_rocprof': rocprof_ms,
             'mfma_busy_frac_pmc': mfma_util, 'clock_ghz_pmc': clock,
             'timing': 'avg_launch_ms: HIP events on the launch stream over the timed region '
-                      '(one event set per forward, all steps averaged); '
-                      'avg_launch_ms_rocprof: rocprofv3 --kernel-trace --stats of this bench '
-                      '(--streams 1 --no-side), committed summary',
-            'conv_stack_tflops': round(total / (sum(conv.values()) * 1e-3) / 1e12, 2)}
+                      '(one event set per forward, all steps averaged); avg_launch_ms_rocprof: '
+                      'rocprofv3 --kernel-trace --stats of this bench (--streams 1 --no-side), committed summary',
+            'conv_stack_tflops': round(total / (conv_ms * 1e-3) / 1e12, 2),
+            'conv_stack_frac': round(total / (conv_ms * 1e-3) / 1e12 / peak, 4)}
 
 
-FRONTEND_BYTES_PER_CLIP = 160000 * 4 + 1001 * 64 * 4   # SURVEY §8(d): waveform in + X0 out
-
-
-def side_measurements(model, wave, args, dev, stage_ms):
-    """Secondary numbers on rank 0 (not the headline): the frontend's achieved
-    HBM rate, GPU event extraction for the batch, and window mode (predict.py
-    semantics: 6 x 5 s windows per 10 s clip, merged + averaged)."""
+# ---------------------------------------------------------------------------
+# legs
+# ---------------------------------------------------------------------------
+def clip_leg(model, wave, args, world, rank, dev, precision):
+    model.set_precision(precision)
     B = wave.shape[0]
-    out = {}
-    if stage_ms and stage_ms.get('frontend'):
-        out['frontend_gbps'] = round(B * FRONTEND_BYTES_PER_CLIP / (stage_ms['frontend'] * 1e-3) / 1e9, 1)
+
+    def step():
+        with torch.no_grad():
+            fw = model(wave)['framewise_output']
+            if world > 1:
+                distributed.gather_to_rank0(fw, world, rank)
+
+    value, elapsed, stage_ms = measure(step, args, world, dev, model, B)
+    p50, p99 = latency(step, B, max(5, min(args.steps, 20)))
+    return value, elapsed, stage_ms, p50, p99
+
+
+def gamma_leg(args, dev, precision):
+    """BASELINE config 4: Cnn_9layers_Gru_FrameAtt gammatone 32k, B=32.  A
+    step = float64 gammatone features of 32 x 10 s @ 32 kHz clips (the
+    reference computes them on the CPU at HDF5-pack time, utils/features.py:
+    361-370) + the gamma-branch forward (models.py:636-688)."""
+    name = MODEL_NAMES['gru']
+    m = build_model(name, dev, (32000, 1024, 320, 64, 50, 14000), 'gamma').set_precision(precision)
+    B = args.batch
+    audio = torch.from_numpy(synth.make_waveforms(B, 10.0, 32000, seed=4321)).to(dev)
+
+    def step():
+        with torch.no_grad():
+            m(inference.gamma_features(m, audio))
+
+    value, elapsed, stage_ms = measure(step, args, 1, dev, m, B)
+    # gamma frontend alone, timed with torch events on the current stream (its
+    # kernels are launched on that stream)
+    for _ in range(2):
+        inference.gamma_features(m, audio)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 5
+    e0.record()
+    for _ in range(reps):
+        inference.gamma_features(m, audio)
+    e1.record()
+    torch.cuda.synchronize()
+    fe_ms = e0.elapsed_time(e1) / reps
+    T = 994
+    flops = B * (T * (5.0 * 1024 * 10 + 8.0 * 1025) + 2.0 * 64 * 1025 * T)   # FFT + unpack/|X| + ERB product
+    bytes_ = B * (320000 * 4 + 64 * T * 4)
+    return {'workload': 'Cnn_9layers_Gru_FrameAtt gammatone 32k, %d x 10 s @ 32 kHz clips per step '
+                        '(float64 gammatone features + forward)' % B,
+            'value': round(value, 2), 'unit': 'clips/s', 'dtype': DTYPE[precision] + '; gammatone frontend f64',
+            'ms_per_step': round(elapsed / args.steps * 1e3, 4),
+            'roofline': roofline(stage_ms, B, precision, T=T),
+            'gamma_frontend': {'ms_per_batch': round(fe_ms, 4), 'bound': 'fp64',
+                               'achieved': round(flops / (fe_ms * 1e-3) / 1e12, 3), 'peak': PEAK_FP64_TF,
+                               'unit': 'TFLOP/s (f64)', 'frac': round(flops / (fe_ms * 1e-3) / 1e12 / PEAK_FP64_TF, 4),
+                               'hbm_gbps_algorithmic': round(bytes_ / (fe_ms * 1e-3) / 1e9, 1),
+                               'note': 'algorithmic f64 FLOPs: 5 N log2 N complex FFT (N=1024) + unpack '
+                                       '+ 64 x 1025 ERB product per frame; bytes: audio in + features out'}}
+
+
+def window_leg(model, wave, args, dev, precision):
+    model.set_precision(precision)
+    B = wave.shape[0]
+
+    def step():
+        with torch.no_grad():
+            inference.predict_windows(model, wave, 5, 1)
+
+    value, elapsed, _ = measure(step, args, 1, dev, None, B)
+    return {'value': round(value, 2), 'unit': 'clips/s', 'windows_per_clip': 6,
+            'windows_per_s': round(6 * value, 1), 'ms_per_step': round(elapsed / args.steps * 1e3, 4),
+            'dtype': DTYPE[precision],
+            'note': '5 s windows, 1 s stride, all windows of the batch in one launch, merged + avg_merge '
+                    'on the GPU (predict.py:297-349)'}
+
+
+def events_side(model, wave):
     with torch.no_grad():
         fw = model(wave)['framewise_output']
     params = dict(inference.DEFAULT_PREDICT_PARAMS)
@@ -280,22 +457,7 @@ def side_measurements(model, wave, args, dev, stage_ms):
     t0 = time.perf_counter()
     for _ in range(reps):
         n_ev = len(inference.event_pairs(fw, params))
-    out['events_ms_per_batch'] = round((time.perf_counter() - t0) / reps * 1e3, 4)
-    out['events_per_batch'] = n_ev
-    with torch.no_grad():
-        for _ in range(2):
-            inference.predict_windows(model, wave, 5, 1)
-        torch.cuda.synchronize()
-        reps = max(3, min(args.steps, 10))
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            inference.predict_windows(model, wave, 5, 1)
-        torch.cuda.synchronize()
-    el = time.perf_counter() - t0
-    out['value_window_mode'] = {'value': round(B * reps / el, 2), 'unit': 'clips/s',
-                                'windows_per_clip': 6, 'note': '5 s windows, 1 s stride, merged + '
-                                                             'avg_merge on the GPU (predict.py:297-349)'}
-    return out
+    return {'events_ms_per_batch': round((time.perf_counter() - t0) / reps * 1e3, 4), 'events_per_batch': n_ev}
 
 
 def main():
@@ -310,12 +472,11 @@ def main():
                     help='streams > 1 without ordering the conv stacks (A/B of sedx_set_pipelined)')
     ap.add_argument('--model', choices=list(MODEL_NAMES), default='gru')
     ap.add_argument('--mode', choices=['clip', 'window'], default='clip')
-    ap.add_argument('--precision', choices=list(PEAK_TF), default='x3')
-    ap.add_argument('--no-exact', action='store_true', help='skip timing the exact fp32 mode')
+    ap.add_argument('--precision', choices=list(PEAK_TF), default='exact')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-side', action='store_true',
-                    help='skip the side measurements (events, window mode): profiling passes use it so '
-                         'that per-kernel rocprof averages cover only the headline launches')
+                    help='headline only (no x3 / config 3 / config 4 / window legs, no latency_b1): '
+                         'profiling passes use it so per-kernel rocprof averages cover only the headline')
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
     args = ap.parse_args()
 
@@ -325,40 +486,78 @@ def main():
     dev = torch.device('cuda', local)
     torch.cuda.set_device(dev)
     name = MODEL_NAMES[args.model]
-    model = build_model(name, dev).set_precision(args.precision)
+    model = build_model(name, dev)
     B = args.batch
     wave = torch.from_numpy(synth.make_waveforms(B, 10.0, 16000, seed=1234 + rank)).to(dev)
 
-    value, elapsed, p50, p99, stage_ms = measure(model, wave, args, world, rank, dev)
-    roof = stage_iso = None
     if args.mode == 'clip':
+        value, elapsed, stage_ms, p50_dev, p99_dev = clip_leg(model, wave, args, world, rank, dev, args.precision)
         roof = roofline(stage_ms, B, args.precision)
-        stage_iso = stage_times(model, wave, dev, max(3, min(args.steps, 10)))
-    exact = None
-    if not args.no_exact and args.precision != 'exact':
-        model.set_precision('exact')
-        ev, _, ep50, _, est = measure(model, wave, args, world, rank, dev)
-        exact = {'value': round(ev, 2), 'ms_per_clip_p50': round(ep50, 4)}
-        if args.mode == 'clip':
-            exact['roofline'] = roofline(est, B, 'exact')
+    else:
         model.set_precision(args.precision)
+        wl = window_leg(model, wave, args, dev, args.precision)
+        value, elapsed, stage_ms, roof = wl['value'], wl['ms_per_step'] * args.steps / 1e3, None, None
+        p50_dev = p99_dev = None
+    # p50 from host-visible input (pinned) to the framewise output on the host
+    host_wave = wave.cpu().pin_memory()
+    host_out = torch.empty((B * world, 1000, 25), dtype=torch.float32).pin_memory() if rank == 0 else None
+    h2h = host_to_host_step(model, host_wave, host_out, dev, world, rank)
+    for _ in range(3):
+        h2h()
+    p50, p99 = latency(h2h, B, max(5, min(args.steps, 20))) if args.mode == 'clip' else (None, None)
 
     extra = {}
-    if args.mode == 'clip' and rank == 0 and not args.no_side:
-        extra = side_measurements(model, wave, args, dev, stage_iso)
+    if world == 1 and rank == 0 and not args.no_side and args.mode == 'clip':
+        extra['stage_ms_isolated'] = stage_times_isolated(model, wave, dev, max(3, min(args.steps, 10)))
+        if extra['stage_ms_isolated'].get('frontend'):
+            fe = extra['stage_ms_isolated']['frontend']
+            extra['frontend_roofline'] = {
+                'bound': 'hbm', 'kernel': 'sedx::logmel_kernel<512, false>',
+                'achieved': round(B * FRONTEND_BYTES_PER_CLIP / (fe * 1e-3) / 1e9, 1), 'peak': PEAK_HBM_GBPS,
+                'unit': 'GB/s', 'frac': round(B * FRONTEND_BYTES_PER_CLIP / (fe * 1e-3) / 1e9 / PEAK_HBM_GBPS, 4),
+                'ms_per_batch': fe, 'bytes_per_clip': FRONTEND_BYTES_PER_CLIP}
+        extra.update(events_side(model, wave))
         extra['latency_b1'] = latency_b1(model, dev)
+        other = 'x3' if args.precision == 'exact' else 'exact'
+        v2, e2, st2, p2, _ = clip_leg(model, wave, args, 1, 0, dev, other)
+        extra['value_%s' % other] = {'value': round(v2, 2), 'unit': 'clips/s', 'dtype': DTYPE[other],
+                                     'ms_per_step': round(e2 / args.steps * 1e3, 4),
+                                     'ms_per_clip_p50_device': round(p2, 4),
+                                     'roofline': roofline(st2, B, other), 'stage_ms': st2,
+                                     'note': 'opt-in arithmetic, same workload' if other == 'x3' else
+                                             'the reference arithmetic, same workload'}
+        model.set_precision(args.precision)
+        cfgs = {}
+        if args.model == 'gru':
+            trf = build_model(MODEL_NAMES['transformer'], dev)
+            v3, e3, st3, p3, _ = clip_leg(trf, wave, args, 1, 0, dev, args.precision)
+            cfgs['config3'] = {'workload': 'Cnn_9layers_Transformer_FrameAtt logmel 16k, %d x 10 s clips '
+                                           'per step (clip mode)' % B,
+                               'metric': METRICS['transformer'],
+                               'value': round(v3, 2), 'unit': 'clips/s', 'dtype': DTYPE[args.precision],
+                               'ms_per_step': round(e3 / args.steps * 1e3, 4),
+                               'ms_per_clip_p50_device': round(p3, 4),
+                               'roofline': roofline(st3, B, args.precision), 'stage_ms': st3}
+            del trf
+        cfgs['config4'] = gamma_leg(args, dev, args.precision)
+        cfgs['window_mode'] = window_leg(model, wave, args, dev, args.precision)
+        model.set_precision(args.precision)
+        extra['configs'] = cfgs
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(name, args.cpu_seconds, model, dev)
+        cpu = cpu_baseline(name, model, dev, args.cpu_seconds, B)
+        if args.mode == 'clip' and not args.no_side:
+            cpu['window_mode'] = cpu_baseline_window(name, min(args.cpu_seconds, 10.0))
 
     if rank == 0:
         line = {
-            'metric': METRIC, 'value': round(value, 2), 'unit': 'clips/s', 'n_gpus': world,
+            'metric': METRICS[args.model], 'value': round(value, 2), 'unit': 'clips/s', 'n_gpus': world,
             'steps': args.steps, 'warmup': args.warmup,
-            'ms_per_step': round(elapsed / args.steps * 1e3, 4), 'ms_per_clip_p50': round(p50, 4),
+            'ms_per_step': round(elapsed / args.steps * 1e3, 4),
+            'ms_per_clip_p50': round(p50, 4) if p50 is not None else None,
             'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
-            'dtype': 'f32' if args.precision == 'exact' else 'f32 (conv: 3xbf16-split MFMA, f32 accumulate)',
+            'dtype': DTYPE[args.precision],
             'data': 'synthetic (seeded 0.1*N(0,1) + gated tones; random-init weights)',
             'config': {'workload': '%s logmel 16k, %d x 10 s clips per GPU per step (%s mode)'
                                    % (name, B, args.mode),
@@ -367,10 +566,12 @@ def main():
                        'parallelism': 'dp%d clip-sharded, RCCL gather of framewise' % world,
                        'streams': args.streams,
                        'pipelined': args.streams > 1 and not args.no_pipeline},
-            'ms_per_clip_p99': round(p99, 4),
+            'ms_per_clip_p99': round(p99, 4) if p99 is not None else None,
+            'ms_per_clip_p50_note': 'per batch, one at a time, from pinned host input (H2D on a copy '
+                                    'stream) to framewise in pinned host memory on rank 0',
+            'ms_per_clip_p50_device': round(p50_dev, 4) if p50_dev is not None else None,
+            'ms_per_clip_p99_device': round(p99_dev, 4) if p99_dev is not None else None,
             'roofline': roof, 'cpu_baseline': cpu, 'stage_ms': stage_ms,
-            'stage_ms_isolated': stage_iso,
-            'value_exact_fp32': exact,
         }
         line.update(extra)
         if cpu:

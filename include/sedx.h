@@ -19,8 +19,13 @@
  *    message (the Python shim raises RuntimeError with it), replacing the
  *    reference's Python exceptions (e.g. pytorch/models.py:139).
  *  - A handle is bound to one device and owns packed weights + a cached
- *    workspace; calls on one handle must be serialised by the caller (the
- *    reference's DataParallel uses one replica per device, one thread each).
+ *    workspace.  Host calls on one handle must be serialised by the caller
+ *    (the reference's DataParallel uses one replica per device, one thread
+ *    each); the device work they issue may run concurrently on different
+ *    streams when every such call passes its own d_workspace (the weights
+ *    are read-only after sedx_finalize_weights).  Handles share no mutable
+ *    state: calls on different handles (e.g. one per device, each from its
+ *    own thread) need no coordination.
  */
 #ifndef SEDX_H
 #define SEDX_H
@@ -121,10 +126,15 @@ sedx_status sedx_forward_features(sedx_handle* h, const float* d_feat, int64_t B
 /* Gammatone frontend (utils/gammatone/fftweight.py:126-168 + power_to_db
  * top_db=80 + float32_to_int16 / int16_to_float32, utils/features.py:361-370,
  * utils/utilities.py:73-79): d_audio [B, L] (already pad_truncated to 10 s)
- * -> d_feat [B, 64, T], T = 1 + floor((L - nfft) / hop). */
+ * -> d_feat [B, 64, T], T = 1 + floor((L - nfft) / hop).  Computed in float64
+ * like the reference's numpy (FFT, |X|, the ERB product, dB, top_db clamp and
+ * the int16 quantisation), so the int16 codes equal the reference's.
+ * d_feat == NULL: geometry query (T_out only).  Workspace:
+ * sedx_gamma_workspace_size (NULL d_workspace = handle-owned cache). */
 sedx_status sedx_gamma_features(sedx_handle* h, const float* d_audio, int64_t B, int64_t L,
                                 float* d_feat, int64_t* T_out, void* d_workspace,
                                 size_t workspace_bytes, void* stream);
+sedx_status sedx_gamma_workspace_size(const sedx_handle* h, int64_t B, int64_t L, size_t* bytes);
 
 /* Windowed driver (pytorch/predict.py:297-349; main_strong.py:790-833).
  * Slices every clip into windows of `sample_duration` s at stride
@@ -158,15 +168,35 @@ sedx_status sedx_forward_windows_vote(sedx_handle* h, const float* d_audio, int6
                                       int32_t pad_clip, const double* bin_thres, float* d_votes,
                                       void* d_workspace, size_t workspace_bytes, void* stream);
 
-/* Arithmetic of the 9-layer conv stack (96.8 % of the FLOPs).
- *  SEDX_PRECISION_X3    (default) bf16 MFMA with a 3-term hi/lo operand split
+/* Arithmetic of the GEMM-shaped work: the 9-layer conv stack (96.8 % of the
+ * FLOPs), the GRU input projection and recurrence, the MHA projections and
+ * the AttBlock projection.
+ *  SEDX_PRECISION_EXACT (default) fp32 operands, fp32 accumulation
+ *                       (v_mfma_f32_32x32x2_f32 / fp32 FMA): the reference's
+ *                       arithmetic (pytorch/models.py:614-615, :663-670).
+ *  SEDX_PRECISION_X3    opt-in: bf16 MFMA with a 3-term hi/lo operand split
  *                       (hi*hi + hi*lo + lo*hi, fp32 accumulate): operands
  *                       carry 16 significant bits, products err ~2^-16 rel.
- *  SEDX_PRECISION_EXACT fp32-in / fp32-acc MFMA (v_mfma_f32_32x32x2_f32),
- *                       bit-for-bit an fma chain, 16/3 x slower.
- * Everything else (FFT frontend, GRU / MHA, head) is fp32 in both modes. */
+ * The frontend (FFT, mel, dB), the gates, softmax and the head's
+ * element-wise work are fp32 in both modes; the gammatone frontend float64. */
 typedef enum { SEDX_PRECISION_EXACT = 0, SEDX_PRECISION_X3 = 1 } sedx_precision;
 sedx_status sedx_set_precision(sedx_handle* h, int32_t mode);
+
+/* Implementation choices that leave the arithmetic's meaning unchanged (A/B
+ * measurement and tests; the defaults are the fastest measured):
+ *  SEDX_TUNE_GRU_KERNEL   SEDX_GRU_KERNEL_COOP (default): the cooperative
+ *                         recurrence, 8 workgroups per (32-clip group,
+ *                         direction) exchanging h slices every step;
+ *                         SEDX_GRU_KERNEL_SIMPLE: one workgroup per (clip,
+ *                         direction), W_hh streamed from L2 (fp32 FMA).
+ *  SEDX_TUNE_GRU_HANDOFF  SEDX_GRU_HANDOFF_AUTO (default): XCD-local hand-off
+ *                         when all 8 slices share an XCD, else global;
+ *                         SEDX_GRU_HANDOFF_GLOBAL: always the global protocol
+ *                         (same bytes, bit-identical results). */
+typedef enum { SEDX_TUNE_GRU_KERNEL = 0, SEDX_TUNE_GRU_HANDOFF = 1 } sedx_tuning_knob;
+enum { SEDX_GRU_KERNEL_COOP = 0, SEDX_GRU_KERNEL_SIMPLE = 1 };
+enum { SEDX_GRU_HANDOFF_AUTO = 0, SEDX_GRU_HANDOFF_GLOBAL = 1 };
+sedx_status sedx_set_tuning(sedx_handle* h, int32_t knob, int32_t value);
 
 /* Serving with several batches in flight (one stream per request): when on,
  * the conv stack of every forward on this handle starts only after the conv
@@ -187,6 +217,16 @@ sedx_status sedx_set_pipelined(sedx_handle* h, int32_t on);
  * sedx_stage_times returns per-stage averages over all forwards since the
  * previous call (or since profiling was switched on), then resets them. */
 #define SEDX_N_STAGES 11
+/* Stage capture (per-stage parity tests): every later forward copies the
+ * output of stage `stage` (numbering as above) into d_buf (at most `bytes`),
+ * on its stream, in the library's channels-last layout:
+ *   0  bn0 output X0                  [items][T][64]
+ *   2,4,6  block 1..3 output (pooled) [items][T/2^k][64/2^k][C_k]
+ *   3,5,7  conv1 of block 2..4        [items][T'][F'][C]
+ *   8  block 4 + freq mean            [items][T/8][512]
+ *   9  GRU / MHA output               [items][T/8][512]
+ * stage < 0 or d_buf == NULL switches capture off. */
+sedx_status sedx_set_capture(sedx_handle* h, int32_t stage, float* d_buf, size_t bytes);
 sedx_status sedx_set_profiling(sedx_handle* h, int32_t on);
 sedx_status sedx_stage_times(sedx_handle* h, float* ms, int32_t capacity, int32_t* n_stages);
 
@@ -204,7 +244,7 @@ sedx_status sedx_events(const float* h_framewise, int64_t n_clips, int64_t T, in
                         const int64_t* n_salt, int32_t* h_events, int64_t capacity,
                         int64_t* n_events);
 
-/* The same thresholding on the GPU, one thread per (clip, class) series, no
+/* The same thresholding on the GPU, one wavefront per (clip, class) series, no
  * host round trip (asynchronous on `stream`; the device that owns d_x must be
  * current).
  *   mode 0: activity_detection (utils/vad.py:11-45) of framewise

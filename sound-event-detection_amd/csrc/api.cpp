@@ -58,9 +58,9 @@ struct DevWeights {
   void* wfc_x3 = nullptr;
   void* wac_x3 = nullptr;
   // gamma
-  float2* g_twiddle = nullptr;
-  float* g_window = nullptr;
-  float* g_weightsT = nullptr;  // [nfft/2+1][64] / nfft
+  double2* g_twiddle = nullptr;
+  double* g_window = nullptr;
+  double* g_weightsT = nullptr;  // [gamma_kp(nfft)][64] ERB weights (fft_weights)
 };
 
 }  // namespace
@@ -80,9 +80,13 @@ struct sedx_handle {
   void* ws = nullptr;        // cached workspace
   size_t ws_bytes = 0;
   // optional per-stage timing (sedx_set_profiling): events at stage boundaries
-  int precision = SEDX_PRECISION_X3;   // conv stack arithmetic (sedx_set_precision)
-  bool gru_simple = getenv("SEDX_GRU_SIMPLE") != nullptr;   // A/B: per-(clip,dir) recurrence
-  bool debug_x0 = getenv("SEDX_DEBUG_X0") != nullptr;      // diagnostic: X0 snapshot after the frontend
+  int precision = SEDX_PRECISION_EXACT;   // GEMM arithmetic (sedx_set_precision)
+  int gru_kernel = SEDX_GRU_KERNEL_COOP;   // sedx_set_tuning
+  int gru_handoff = SEDX_GRU_HANDOFF_AUTO;
+  // sedx_set_capture: copy one stage's output of every later forward
+  int cap_stage = -1;
+  float* cap_buf = nullptr;
+  size_t cap_bytes = 0;
   int profiling = 0;          // 0 off, 1 last forward, 2 accumulate
   // sedx_set_pipelined: conv stacks of successive forwards run in issue order
   // (each waits for the previous one's conv-done event), whatever streams
@@ -171,6 +175,24 @@ sedx_status fail(sedx_handle* h, sedx_status st, const char* fmt, ...) {
       return fail(h, SEDX_EHIP, "%s failed: %s", #expr, hipGetErrorString(e_));         \
   } while (0)
 
+// errors of the launches just issued: preparation failures noted by
+// launch_info (sedx_internal.h) first, then the runtime's launch error
+// sedx_set_capture: stage `stage` just wrote `n` floats at `src`
+void capture(sedx_handle* h, int stage, const float* src, size_t n, hipStream_t s) {
+  if (h->cap_stage != stage || !h->cap_buf) return;
+  const size_t bytes = std::min(n * sizeof(float), h->cap_bytes);
+  if (hipMemcpyAsync(h->cap_buf, src, bytes, hipMemcpyDeviceToDevice, s) != hipSuccess)
+    note_launch_error(hipErrorInvalidValue);
+}
+
+sedx_status launch_status(sedx_handle* h) {
+  const hipError_t pe = take_launch_error();
+  if (pe != hipSuccess) return fail(h, SEDX_EHIP, "kernel launch preparation failed: %s", hipGetErrorString(pe));
+  const hipError_t le = hipGetLastError();
+  if (le != hipSuccess) return fail(h, SEDX_EHIP, "kernel launch failed: %s", hipGetErrorString(le));
+  return SEDX_OK;
+}
+
 struct DeviceGuard {
   int prev = -1;
   explicit DeviceGuard(int dev) {
@@ -248,7 +270,7 @@ Geometry geometry_from_T(const sedx_handle* h, int64_t T) {
 
 // workspace layout (floats), 256-B aligned regions
 struct WsLayout {
-  size_t x0, bufA, bufB, sched, dbg, total_bytes;
+  size_t x0, bufA, bufB, sched, total_bytes;
 };
 
 size_t align_up(size_t x) { return (x + 63) & ~size_t(63); }
@@ -275,8 +297,6 @@ WsLayout ws_layout(const sedx_handle* h, int64_t B, const Geometry& g) {
   off += align_up(b);
   l.sched = off;                                  // 7 conv launches x CONV_SCHED_INTS claim counters
   off += align_up(7 * CONV_SCHED_INTS);
-  l.dbg = off;                                    // SEDX_DEBUG_X0: copy of X0 taken after the frontend
-  if (h->debug_x0) off += align_up((size_t)B * g.T * 64);
   l.total_bytes = off * sizeof(float);
   return l;
 }
@@ -307,8 +327,11 @@ sedx_status run_body(sedx_handle* h, int64_t B, const Geometry& g, float* ws, co
   float* A = ws + l.bufA;
   float* P = ws + l.bufB;
   const int iB = (int)B;
-  mark(h, 1, s);
+  // the cross-stream wait for the previous forward's conv stack comes before
+  // the b1c1 stage event, so stage 1 times only this forward's work
   if (h->pipelined && h->conv_done_recorded) HIP_TRY(h, hipStreamWaitEvent(s, h->conv_done, 0));
+  mark(h, 1, s);
+  capture(h, 0, X0, (size_t)B * g.T * 64, s);
   const bool x3 = h->precision == SEDX_PRECISION_X3;
   int* sched = reinterpret_cast<int*>(ws + l.sched);
   if (x3) {
@@ -342,6 +365,9 @@ sedx_status run_body(sedx_handle* h, int64_t B, const Geometry& g, float* ws, co
                         sched + i * CONV_SCHED_INTS, s);
     else
       launch_conv3x3(c.in, iB, c.T, c.F, c.cin, c.cout, w.wp[c.idx], w.cb[c.idx], c.out, c.epi, s);
+    const size_t px = c.epi == EPI_STORE ? (size_t)c.T * c.F : c.epi == EPI_POOL2 ? (size_t)(c.T / 2) * (c.F / 2)
+                                                                                   : (size_t)c.T;
+    capture(h, 2 + i, c.out, (size_t)B * px * c.cout, s);
   }
   mark(h, 9, s);
   if (h->pipelined) {
@@ -364,23 +390,24 @@ sedx_status run_body(sedx_handle* h, int64_t B, const Geometry& g, float* ws, co
   };
   if (is_gru(h)) {
     linear(S, w.w_ih, w.w_ih_x3, 1536, 128, w.b_ih, G, 0);
-    if (h->gru_simple)
+    if (h->gru_kernel == SEDX_GRU_KERNEL_SIMPLE)
       launch_gru(G, iB, (int)g.T3, w.whhT, w.bhh, Hs, s);
     else
-      launch_gru_coop(G, iB, (int)g.T3, w.whh, w.bhh, Hs, LG + align_up((size_t)M * h->nac), s);
+      launch_gru_coop(G, iB, (int)g.T3, w.whh, w.bhh, Hs, LG + align_up((size_t)M * h->nac), !x3,
+                      h->gru_handoff == SEDX_GRU_HANDOFF_AUTO, s);
   } else {
     linear(S, w.wqkv, w.wqkv_x3, 1536, 128, w.bqkv, G, 0);
     launch_mha(G, iB, (int)g.T3, O, s);
     linear(O, w.wfc, w.wfc_x3, 512, 128, w.bfc, Hs, 1);
   }
+  capture(h, 9, Hs, (size_t)M * 512, s);
   mark(h, 10, s);
   linear(Hs, w.wac, w.wac_x3, h->nac, 64, w.bac, LG, 0);
   launch_att_head(LG, iB, (int)g.T3, h->cfg.classes_num, h->nac, (int)g.out_frames, d_fw, d_clip,
                   is_gru(h) ? d_emb : nullptr, s);
   if (!is_gru(h) && d_emb) launch_transpose_btd(Hs, iB, (int)g.T3, 512, d_emb, s);
   mark(h, 11, s);
-  HIP_TRY(h, hipGetLastError());
-  return SEDX_OK;
+  return launch_status(h);
 }
 
 // -------- window geometry (predict.py:297-338 / main_strong.py:791-832) --------
@@ -462,6 +489,38 @@ sedx_status sedx_set_precision(sedx_handle* h, int32_t mode) {
 }
 
 const char* sedx_last_error(const sedx_handle* h) { return h ? h->err.c_str() : "null handle"; }
+
+sedx_status sedx_set_capture(sedx_handle* h, int32_t stage, float* d_buf, size_t bytes) {
+  if (!h) return SEDX_EINVAL;
+  if (stage < 0 || !d_buf) {
+    h->cap_stage = -1;
+    h->cap_buf = nullptr;
+    h->cap_bytes = 0;
+    return SEDX_OK;
+  }
+  if (stage == 1 || stage > 9) return fail(h, SEDX_EINVAL, "stage %d cannot be captured", (int)stage);
+  h->cap_stage = stage;
+  h->cap_buf = d_buf;
+  h->cap_bytes = bytes;
+  return SEDX_OK;
+}
+
+sedx_status sedx_set_tuning(sedx_handle* h, int32_t knob, int32_t value) {
+  if (!h) return SEDX_EINVAL;
+  switch (knob) {
+    case SEDX_TUNE_GRU_KERNEL:
+      if (value != SEDX_GRU_KERNEL_COOP && value != SEDX_GRU_KERNEL_SIMPLE) break;
+      h->gru_kernel = value;
+      return SEDX_OK;
+    case SEDX_TUNE_GRU_HANDOFF:
+      if (value != SEDX_GRU_HANDOFF_AUTO && value != SEDX_GRU_HANDOFF_GLOBAL) break;
+      h->gru_handoff = value;
+      return SEDX_OK;
+    default:
+      return fail(h, SEDX_EINVAL, "unknown tuning knob %d", (int)knob);
+  }
+  return fail(h, SEDX_EINVAL, "bad value %d for tuning knob %d", (int)value, (int)knob);
+}
 
 sedx_status sedx_create(const sedx_config* cfg, int device, sedx_handle** out) {
   if (!cfg || !out) return SEDX_EINVAL;
@@ -720,9 +779,10 @@ sedx_status sedx_finalize_weights(sedx_handle* h) {
     }
   }
 
-  // ---- gammatone weights (computed here: utils/gammatone/fftweight.py:63-123) ----
-  std::vector<float> g_tw, g_win, g_wT;
+  // ---- gammatone tables (float64, numpy operation order: gamma_weights.cpp) ----
+  std::vector<double> g_tw, g_win, g_wT;
   if (h->cfg.feature_type == SEDX_FEATURE_GAMMA) {
+    // fft_gtgram (fftweight.py:151-152) + gtgram_strides (gtgram.py:23-40)
     const double fs = h->cfg.sample_rate;
     const double win_t = (double)h->cfg.window_size / fs, hop_t = (double)h->cfg.hop_size / fs;
     const int nfft_g = (int)std::pow(2.0, std::ceil(std::log2(2 * win_t * fs)));
@@ -733,58 +793,7 @@ sedx_status sedx_finalize_weights(sedx_handle* h) {
     h->g_nfft = nfft_g;
     h->g_nwin = nwin;
     h->g_hop = nhop;
-    const int NB = nfft_g / 2 + 1, nf = 64;
-    const double fmin = h->cfg.fmin, fmax = fs / 2;
-    const double ear_q = 9.26449, min_bw = 24.7, T = 1.0 / fs;
-    std::vector<double> cf(nf);
-    for (int i = 0; i < nf; ++i) {
-      const double frac = (double)(i + 1) / nf;
-      cf[nf - 1 - i] = -ear_q * min_bw + std::exp(frac * (-std::log(fmax + ear_q * min_bw) +
-                                                          std::log(fmin + ear_q * min_bw))) *
-                                             (fmax + ear_q * min_bw);
-    }
-    g_wT.assign((size_t)NB * nf, 0.f);
-    typedef std::complex<double> cd;
-    for (int i = 0; i < nf; ++i) {
-      const double erb = cf[i] / ear_q + min_bw;
-      const double Bw = 1.019 * 2 * M_PI * erb;
-      const double arg = 2 * cf[i] * M_PI * T;
-      const cd vec = std::exp(cd(0, 2 * arg));
-      const double rt_pos = std::sqrt(3 + std::pow(2.0, 1.5)), rt_neg = std::sqrt(3 - std::pow(2.0, 1.5));
-      const double common = -T * std::exp(-(Bw * T));
-      const double k11 = std::cos(arg) + rt_pos * std::sin(arg), k12 = std::cos(arg) - rt_pos * std::sin(arg);
-      const double k13 = std::cos(arg) + rt_neg * std::sin(arg), k14 = std::cos(arg) - rt_neg * std::sin(arg);
-      const double A11 = common * k11, A12 = common * k12, A13 = common * k13, A14 = common * k14;
-      const cd gain_arg = std::exp(cd(-Bw * T, arg));
-      const cd den = -1.0 / std::exp(Bw * T) + 1.0 + vec * (1.0 - std::exp(Bw * T));
-      const cd q = T * std::exp(Bw * T) / den;
-      const double gain = std::abs((vec - gain_arg * k11) * (vec - gain_arg * k12) *
-                                   (vec - gain_arg * k13) * (vec - gain_arg * k14) * (q * q * q * q));
-      const double B2 = std::exp(-2 * Bw * T);
-      const double r = std::sqrt(B2), theta = 2 * M_PI * cf[i] / fs;
-      const cd pole = r * std::exp(cd(0, theta));
-      for (int k = 0; k < NB; ++k) {
-        const cd uc = std::exp(cd(0, 2 * M_PI * k / nfft_g));
-        const double v = std::abs(uc + A11 * fs) * std::abs(uc + A12 * fs) * std::abs(uc + A13 * fs) *
-                         std::abs(uc + A14 * fs) *
-                         std::pow(std::abs(fs * (pole - uc) * (std::conj(pole) - uc)), -4.0) / gain;
-        g_wT[(size_t)k * nf + i] = (float)(v / nfft_g);
-      }
-    }
-    g_tw.resize(2 * nfft_g);
-    for (int m = 0; m < nfft_g; ++m) {
-      g_tw[2 * m] = (float)std::cos(-2.0 * M_PI * m / nfft_g);
-      g_tw[2 * m + 1] = (float)std::sin(-2.0 * M_PI * m / nfft_g);
-    }
-    // specgram_window: centred Hann of width nwin in nfft (fftweight.py:15-30)
-    g_win.assign(nfft_g, 0.f);
-    const int halflen = nwin / 2, halff = nfft_g / 2;
-    const int act = std::min(halff, halflen);
-    for (int i = 0; i < act; ++i) {
-      const double v = 0.5 * (1 + std::cos(M_PI * i / halflen));
-      g_win[halff + i] = (float)v;
-      g_win[halff - i] = (float)v;
-    }
+    gamma_tables(fs, nfft_g, nwin, 64, h->cfg.fmin, g_wT, gamma_kp(nfft_g), g_tw, g_win);
   }
 
   // ---- upload: one blob ----
@@ -843,9 +852,9 @@ sedx_status sedx_finalize_weights(sedx_handle* h) {
   wac_x3 = pack_linear_x3(wac, h->nac, 512, 64);
   add(&W.wac_x3, wac_x3.data(), wac_x3.size() * 2);
   if (!g_wT.empty()) {
-    add((void**)&W.g_twiddle, g_tw.data(), g_tw.size() * 4);
-    add((void**)&W.g_window, g_win.data(), g_win.size() * 4);
-    add((void**)&W.g_weightsT, g_wT.data(), g_wT.size() * 4);
+    add((void**)&W.g_twiddle, g_tw.data(), g_tw.size() * 8);
+    add((void**)&W.g_window, g_win.data(), g_win.size() * 8);
+    add((void**)&W.g_weightsT, g_wT.data(), g_wT.size() * 8);
   }
   size_t total = 0;
   for (auto& it : items) total += (it.bytes + 255) & ~size_t(255);
@@ -986,9 +995,6 @@ static sedx_status forward_wave(sedx_handle* h, const float* d_wave, const int16
   p.out = ws + l.x0;
   mark(h, 0, s);
   launch_logmel(p, h->cfg.window_size, s);
-  if (h->debug_x0)
-    HIP_TRY(h, hipMemcpyAsync(ws + l.dbg, ws + l.x0, (size_t)B * g.T * 64 * sizeof(float),
-                              hipMemcpyDeviceToDevice, s));
   return run_body(h, B, g, ws, l, d_framewise, d_clipwise, d_embedding, s);
 }
 
@@ -1041,13 +1047,16 @@ sedx_status sedx_gamma_features(sedx_handle* h, const float* d_audio, int64_t B,
   if (T_out) *T_out = T;
   if (!d_feat) return SEDX_OK;   // geometry query
   if (!d_audio || B <= 0) return fail(h, SEDX_EINVAL, "null pointer or empty batch");
+  if (B > INT32_MAX / 64 || B * T > INT32_MAX / 64) return fail(h, SEDX_EINVAL, "batch too large");
   const int64_t fill = (L - h->g_nfft + h->g_hop - 1) / h->g_hop;   // len(range(0, s-n, h))
   DeviceGuard dg(h->device);
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const size_t need = ((size_t)B * 64 * T + 256 + 2 * (size_t)B) * sizeof(float);
+  const size_t need = gamma_workspace_bytes(B, T, h->g_nfft);
   float* ws = nullptr;
   sedx_status st = get_ws(h, need, d_workspace, workspace_bytes, &ws);
   if (st != SEDX_OK) return st;
+  auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
+  char* base = reinterpret_cast<char*>(ws);
   GammaParams p{};
   p.audio = d_audio;
   p.L = L;
@@ -1056,14 +1065,24 @@ sedx_status sedx_gamma_features(sedx_handle* h, const float* d_audio, int64_t B,
   p.T_fill = (int32_t)std::min<int64_t>(fill, T);
   p.hop = h->g_hop;
   p.nfft = h->g_nfft;
+  p.kp = gamma_kp(h->g_nfft);
   p.twiddle = h->w.g_twiddle;
   p.window = h->w.g_window;
-  p.weights = h->w.g_weightsT;
-  p.gt = ws;
-  p.maxbuf = ws + (((size_t)B * 64 * T + 63) & ~size_t(63));
+  p.weightsT = h->w.g_weightsT;
+  p.mag = reinterpret_cast<double*>(base);
+  base += al((size_t)B * T * p.kp * sizeof(double));
+  p.db = reinterpret_cast<double*>(base);
+  base += al((size_t)B * 64 * T * sizeof(double));
+  p.mm = reinterpret_cast<unsigned long long*>(base);
   p.out = d_feat;
   launch_gamma(p, s);
-  HIP_TRY(h, hipGetLastError());
+  return launch_status(h);
+}
+
+sedx_status sedx_gamma_workspace_size(const sedx_handle* h, int64_t B, int64_t L, size_t* bytes) {
+  if (!h || !bytes || B <= 0) return SEDX_EINVAL;
+  if (h->cfg.feature_type != SEDX_FEATURE_GAMMA || !h->finalized || L < h->g_nfft) return SEDX_EINVAL;
+  *bytes = gamma_workspace_bytes(B, 1 + (L - h->g_nfft) / h->g_hop, h->g_nfft);
   return SEDX_OK;
 }
 
@@ -1104,6 +1123,9 @@ static sedx_status forward_windows_impl(sedx_handle* h, const float* d_audio, in
   if (st != SEDX_OK) return st;
   if (wg.win_samples <= h->cfg.window_size / 2)
     return fail(h, SEDX_EINVAL, "window too short for reflect padding");
+  // the frontend and conv launches index items with 32-bit sizes (as forward_wave)
+  if (n_clips > INT32_MAX / wg.n_win || n_clips * wg.n_win * wg.g.T > INT32_MAX / 64)
+    return fail(h, SEDX_EINVAL, "batch too large: %lld clips x %d windows", (long long)n_clips, wg.n_win);
   DeviceGuard dg(h->device);
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int64_t items = n_clips * wg.n_win;
@@ -1141,8 +1163,7 @@ static sedx_status forward_windows_impl(sedx_handle* h, const float* d_audio, in
   if (st != SEDX_OK) return st;
   launch_merge(fw, (int)n_clips, wg.n_win, (int)wg.Tw, C, wg.step, (int)wg.N, wg.interval, wg.sd,
                h_vote_thres ? vthr : nullptr, d_merged, s);
-  HIP_TRY(h, hipGetLastError());
-  return SEDX_OK;
+  return launch_status(h);
 }
 
 sedx_status sedx_window_workspace_size(const sedx_handle* h, int64_t n_clips, int64_t L_clip,
@@ -1220,6 +1241,7 @@ sedx_status sedx_events_device(const float* d_x, int64_t n_clips, int64_t T, int
               step, (int64_t)sample_duration, counts, slots, events_slot_cap(T), d_info, d_events,
               capacity};
   launch_events(a, mode, s);
+  if (take_launch_error() != hipSuccess) return SEDX_EHIP;
   return hipGetLastError() == hipSuccess ? SEDX_OK : SEDX_EHIP;
 }
 

@@ -284,17 +284,11 @@ static void launch_f_bn(const float* in, int B, int T, int Cin, int Cout, const 
   constexpr int TT = 128 / F;
   dim3 grid(B * ((T + TT - 1) / TT), Cout / BN);
   if (epi == EPI_STORE)
-    hipLaunchKernelGGL((conv3x3_kernel<F, BN, EPI_STORE>), grid, dim3(256),
-                       mfma_cu_exclusive_lds(reinterpret_cast<const void*>(conv3x3_kernel<F, BN, EPI_STORE>), 256), s,
-                       in, T, Cin, Cout, wp, bias, out);
+    launch_excl(conv3x3_kernel<F, BN, EPI_STORE>, grid, 256, s, in, T, Cin, Cout, wp, bias, out);
   else if (epi == EPI_POOL2)
-    hipLaunchKernelGGL((conv3x3_kernel<F, BN, EPI_POOL2>), grid, dim3(256),
-                       mfma_cu_exclusive_lds(reinterpret_cast<const void*>(conv3x3_kernel<F, BN, EPI_POOL2>), 256), s,
-                       in, T, Cin, Cout, wp, bias, out);
+    launch_excl(conv3x3_kernel<F, BN, EPI_POOL2>, grid, 256, s, in, T, Cin, Cout, wp, bias, out);
   else
-    hipLaunchKernelGGL((conv3x3_kernel<F, BN, EPI_FMEAN>), grid, dim3(256),
-                       mfma_cu_exclusive_lds(reinterpret_cast<const void*>(conv3x3_kernel<F, BN, EPI_FMEAN>), 256), s,
-                       in, T, Cin, Cout, wp, bias, out);
+    launch_excl(conv3x3_kernel<F, BN, EPI_FMEAN>, grid, 256, s, in, T, Cin, Cout, wp, bias, out);
 }
 
 void launch_conv3x3(const float* in, int B, int T, int F, int Cin, int Cout, const float* wp,

@@ -827,15 +827,12 @@ static void launch_x3_epi(const float* in, int B, int T, int Cin, int Cout, cons
                           const float* bias, float* out, int* sched, hipStream_t s,
                           const float* w1 = nullptr, const float* b1 = nullptr) {
   constexpr int TT = ConvGeom<F, BN>::TT;
-  static int resident = 0;           // workgroups resident on the whole device
-  if (!resident) {
-    int dev = 0, ncu = 0, per_cu = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, conv3x3_x3_kernel<F, BN, EPI, FUSE>, 512, 0);
-    resident = (ncu > 0 ? ncu : 256) * (per_cu > 0 ? per_cu : 1);
-  }
-  const size_t pad = mfma_cu_exclusive_lds(reinterpret_cast<const void*>(conv3x3_x3_kernel<F, BN, EPI, FUSE>), 512);
+  // workgroups resident on the whole device + the CU-exclusive LDS pad (per device)
+  const LaunchInfo li =
+      launch_info(reinterpret_cast<const void*>(conv3x3_x3_kernel<F, BN, EPI, FUSE>), 512, 0, true);
+  if (!li.ok) return;
+  const int resident = li.ncu * li.per_cu;
+  const size_t pad = li.dyn;
   const int ntiles = B * ((T + TT - 1) / TT) * (Cout / BN);
   const int per_xcd = (ntiles + 7) / 8;
   int grid = resident & ~7;

@@ -297,14 +297,10 @@ void launch_events(const EventArgs& a, int mode, hipStream_t s) {
   int wpb = (int)std::min<int64_t>(EV_WAVES, std::max<int64_t>(1, EV_LDS_BYTES / (16 * std::max<int64_t>(W, 1))));
   const unsigned blocks = (unsigned)((n + wpb - 1) / wpb);
   const size_t lds = (size_t)wpb * 2 * W * 8;
-  static bool attr = false;                      // > 64 KB of dynamic LDS must be opted into
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(events_series_kernel<0>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)EV_LDS_BYTES);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(events_series_kernel<1>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)EV_LDS_BYTES);
-    attr = true;
-  }
+  // > 64 KB of dynamic LDS must be opted into (per device: launch_info)
+  if (!launch_info(reinterpret_cast<const void*>(events_series_kernel<0>), 64, EV_LDS_BYTES, false).ok ||
+      !launch_info(reinterpret_cast<const void*>(events_series_kernel<1>), 64, EV_LDS_BYTES, false).ok)
+    return;
   if (mode == 0)
     hipLaunchKernelGGL(events_series_kernel<0>, dim3(blocks), dim3(64 * wpb), lds, s, a, W, wpb);
   else

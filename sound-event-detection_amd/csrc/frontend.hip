@@ -113,7 +113,6 @@ __device__ __forceinline__ float2 real_bin(const float2* Z, const float2* tw, in
 // CU-exclusive, 0 of 64.  MFMA kernels are padded the same way
 // (mfma_cu_exclusive_lds).
 constexpr int FE_WAVES = 16;
-constexpr int LDS_PER_CU = 160 * 1024;
 
 template <int NFFT, bool I16>
 __global__ __launch_bounds__(64 * FE_WAVES) void logmel_kernel(FrontendParams p) {
@@ -221,27 +220,20 @@ __global__ __launch_bounds__(64 * FE_WAVES) void logmel_kernel(FrontendParams p)
 
 // one CU-exclusive workgroup per CU; every wave walks several frames, so the
 // register prefetch of the next frame overlaps the current FFT
+// (launch facts per device: launch_info)
+constexpr size_t FE_MEL_LDS = 16 * 1024;   // room for the packed mel weights (<= 2 (n_fft/2+1) floats)
+
 template <int NFFT, bool I16>
 static void launch_logmel_t(const FrontendParams& p0, int64_t total, hipStream_t s) {
-  static size_t dyn = 0;
-  static int ncu = 0;
-  if (!ncu) {
-    hipFuncAttributes fa{};
-    (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(logmel_kernel<NFFT, I16>));
-    dyn = (LDS_PER_CU - fa.sharedSizeBytes) & ~size_t(511);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(logmel_kernel<NFFT, I16>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    if (ncu <= 0) ncu = 256;
-  }
+  const LaunchInfo li =
+      launch_info(reinterpret_cast<const void*>(logmel_kernel<NFFT, I16>), 64 * FE_WAVES, FE_MEL_LDS, true);
+  if (!li.ok) return;
   FrontendParams p = p0;
-  p.mel_lds_floats = (int32_t)(dyn / 4);
+  p.mel_lds_floats = (int32_t)(li.dyn / 4);
   int64_t blocks = (total + FE_WAVES - 1) / FE_WAVES;
-  if (blocks > ncu) blocks = ncu;
+  blocks = std::min<int64_t>(blocks, (int64_t)li.ncu * li.per_cu);
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL((logmel_kernel<NFFT, I16>), dim3((unsigned)blocks), dim3(64 * FE_WAVES), dyn, s, p);
+  hipLaunchKernelGGL((logmel_kernel<NFFT, I16>), dim3((unsigned)blocks), dim3(64 * FE_WAVES), li.dyn, s, p);
 }
 
 void launch_logmel(const FrontendParams& p, int n_fft, hipStream_t s) {
@@ -292,130 +284,264 @@ void launch_features_bn0(const float* feat, int B, int T, const float* bn_scale,
 }
 
 // ---------------------------------------------------------------------------
-// Gammatone frontend (nfft = 2048 at 32 kHz, 1024 at 16 kHz)
+// Gammatone frontend (nfft = 2048 at 32 kHz, 1024 at 16 kHz, 512 at 8 kHz),
+// float64 throughout like the reference's numpy path:
+//   specgram (fftweight.py:33-60): frames b in range(0, s - n, h), un-centred,
+//     u = win * x[b:b+n] (float64 window x float32 samples), t = fft(u)[:n/2+1]
+//   fft_gtgram (:126-168): W . |specgram| / nfft
+//   power_to_db (features.py:363, ref 1.0, amin 1e-10, top_db 80)
+//   float32_to_int16 / int16_to_float32 (utilities.py:73-79)
+// Three launches: gamma_spec_kernel (one 256-thread workgroup per frame:
+// Stockham FFT in LDS, |X| rows to HBM), gamma_erb_kernel (the dense
+// 64 x (nfft/2+1) ERB product as a float64 GEMM over 64-frame tiles, dB and
+// the per-clip max / min in its epilogue), gamma_quant_kernel.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ unsigned int f2ord(float f) {
-  const unsigned int u = __float_as_uint(f);
-  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+__device__ __forceinline__ double2 zmul(double2 a, double2 b) {
+  return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
 }
-__device__ __forceinline__ float ord2f(unsigned int u) {
-  return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
-}
+__device__ __forceinline__ double2 zadd(double2 a, double2 b) { return make_double2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ double2 zsub(double2 a, double2 b) { return make_double2(a.x - b.x, a.y - b.y); }
 
-template <int NFFT>
-__global__ __launch_bounds__(256) void gamma_frames_kernel(GammaParams p, unsigned int* mm) {
-  constexpr int N2 = NFFT / 2;
-  constexpr int NB = N2 + 1;
-  __shared__ float2 s_tw[NFFT];
-  __shared__ float2 s_buf[2][2][N2];
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;   // 0..3 ; waves 0,1 do FFTs, all 4 help in the ERB sum
-  for (int i = threadIdx.x; i < NFFT; i += 256) s_tw[i] = p.twiddle[i];
-  __syncthreads();
-  const int64_t total = (int64_t)p.B * p.T;
-  for (int64_t f0 = (int64_t)blockIdx.x * 2; f0 < total; f0 += (int64_t)gridDim.x * 2) {
-    const int sub = wave & 1;
-    const int64_t fr = f0 + sub;
-    const bool valid = fr < total;
-    float2* X = s_buf[sub][0];
-    float2* Y = s_buf[sub][1];
-    int64_t b = 0;
-    int t = 0;
-    if (valid) {
-      b = fr / p.T;
-      t = (int)(fr - b * p.T);
-    }
-    if (valid && wave < 2) {
-      const float* src = p.audio + b * p.L + (int64_t)t * p.hop;
-      for (int m = lane; m < N2; m += 64)
-        X[m] = make_float2(src[2 * m] * p.window[2 * m], src[2 * m + 1] * p.window[2 * m + 1]);
-    }
-    __syncthreads();
-    // both FFT waves run the transform; waves 2,3 follow the barriers only
-    float2* Z;
-    {
-      float2* XX = X;
-      float2* YY = Y;
-      if (wave >= 2) { XX = s_buf[sub][0]; YY = s_buf[sub][1]; }
-      // waves 2/3 must not write: give them an empty loop by lane >= 64 trick
-      const int l = (wave < 2) ? lane : 1 << 20;
-      stockham_fft<N2>(XX, YY, s_tw, l, &Z);
-    }
-    float* Mg = reinterpret_cast<float*>(Z == X ? Y : X);
-    if (valid && wave < 2) {
-      for (int k = lane; k < NB; k += 64) {
-        const float2 Xk = real_bin<N2>(Z, s_tw, k);
-        Mg[k] = sqrtf(Xk.x * Xk.x + Xk.y * Xk.y);
+// Stockham FFT of N2 complex points by P threads of the block (block barriers).
+template <int N2, int Ns, int P>
+__device__ __forceinline__ double2* zstockham(double2* X, double2* Y, const double2* tw, int tid) {
+  if constexpr (Ns >= N2) {
+    return X;
+  } else {
+    constexpr int NFFT = 2 * N2;
+    constexpr int R = ((N2 / Ns) % 4 == 0) ? 4 : 2;
+    constexpr int nb = N2 / R;
+    constexpr int step = NFFT / (Ns * R);
+    for (int j = tid; j < nb; j += P) {
+      const int k = j & (Ns - 1);
+      const int base = (j - k) * R + k;
+      if constexpr (R == 4) {
+        double2 v0 = X[j], v1 = X[j + nb], v2 = X[j + 2 * nb], v3 = X[j + 3 * nb];
+        if constexpr (Ns > 1) {
+          v1 = zmul(v1, tw[k * step]);
+          v2 = zmul(v2, tw[2 * k * step]);
+          v3 = zmul(v3, tw[3 * k * step]);
+        }
+        const double2 a0 = zadd(v0, v2), a1 = zsub(v0, v2);
+        const double2 b0 = zadd(v1, v3), b1 = zsub(v1, v3);
+        const double2 mib1 = make_double2(b1.y, -b1.x);
+        Y[base] = zadd(a0, b0);
+        Y[base + Ns] = zadd(a1, mib1);
+        Y[base + 2 * Ns] = zsub(a0, b0);
+        Y[base + 3 * Ns] = zsub(a1, mib1);
+      } else {
+        double2 v0 = X[j], v1 = X[j + nb];
+        if constexpr (Ns > 1) v1 = zmul(v1, tw[k * step]);
+        Y[base] = zadd(v0, v1);
+        Y[base + Ns] = zsub(v0, v1);
       }
     }
     __syncthreads();
-    // ERB reduction: 64 channels x 2 frames = 128 outputs; 4 waves -> each
-    // (wave&1) frame, half of the bins per wave pair, combined via LDS.
-    __shared__ float s_part[2][2][64];
-    if (valid) {
-      const int half = wave >> 1;
-      const int kb = half ? NB / 2 : 0, ke = half ? NB : NB / 2;
-      const float* w = p.weights;  // transposed: [NB][64]
-      float acc = 0.0f;
-      for (int k = kb; k < ke; ++k) acc = fmaf(w[(int64_t)k * 64 + lane], Mg[k], acc);
-      s_part[sub][half][lane] = acc;
-    }
-    __syncthreads();
-    if (valid && wave < 2) {
-      const float g = (t < p.T_fill) ? s_part[sub][0][lane] + s_part[sub][1][lane] : 0.0f;
-      const float db = 10.0f * log10f(fmaxf(g, 1e-10f));
-      p.gt[(b * 64 + lane) * p.T + t] = db;
-      // per-clip max / min of dB (ordered-int atomics)
-      atomicMax(&mm[2 * b], f2ord(db));
-      atomicMin(&mm[2 * b + 1], f2ord(db));
-    }
-    __syncthreads();
+    return zstockham<N2, Ns * R, P>(Y, X, tw, tid);
   }
 }
 
-__global__ void gamma_init_kernel(unsigned int* mm, int B) {
+// Real-input spectrum bin k (0..N2) from the N2-point complex FFT Z of the
+// packed sequence z[m] = x[2m] + i x[2m+1].
+template <int N2>
+__device__ __forceinline__ double2 zreal_bin(const double2* Z, const double2* tw, int k) {
+  const double2 A = Z[k & (N2 - 1)];
+  const double2 Bz = Z[(N2 - k) & (N2 - 1)];
+  const double2 E = make_double2(0.5 * (A.x + Bz.x), 0.5 * (A.y - Bz.y));
+  const double2 O = make_double2(0.5 * (A.y + Bz.y), -0.5 * (A.x - Bz.x));
+  return zadd(E, zmul(tw[k], O));
+}
+
+constexpr int GAMMA_SPEC_THREADS = 256;
+
+template <int NFFT>
+constexpr size_t gamma_spec_lds() {   // twiddles + window + two FFT buffers
+  return (size_t)NFFT * sizeof(double2) + (size_t)NFFT * sizeof(double) + (size_t)NFFT * sizeof(double2);
+}
+
+template <int NFFT>
+__global__ __launch_bounds__(GAMMA_SPEC_THREADS) void gamma_spec_kernel(GammaParams p) {
+  constexpr int N2 = NFFT / 2;
+  constexpr int NB = N2 + 1;
+  extern __shared__ double2 s_gdyn[];
+  double2* s_tw = s_gdyn;                                      // [NFFT]
+  double2* X = s_gdyn + NFFT;                                  // [N2]
+  double2* Y = X + N2;                                         // [N2]
+  double* s_win = reinterpret_cast<double*>(Y + N2);           // [NFFT]
+  const int tid = threadIdx.x;
+  for (int i = tid; i < NFFT; i += GAMMA_SPEC_THREADS) {
+    s_tw[i] = p.twiddle[i];
+    s_win[i] = p.window[i];
+  }
+  __syncthreads();
+  const int64_t total = (int64_t)p.B * p.T;
+  for (int64_t fr = blockIdx.x; fr < total; fr += gridDim.x) {
+    const int64_t b = fr / p.T;
+    const int t = (int)(fr - b * p.T);
+    double* row = p.mag + fr * p.kp;
+    if (t >= p.T_fill) {        // column never written by specgram's loop: zeros
+      for (int k = tid; k < p.kp; k += GAMMA_SPEC_THREADS) row[k] = 0.0;
+      continue;
+    }
+    const float* src = p.audio + b * p.L + (int64_t)t * p.hop;
+    for (int m = tid; m < N2; m += GAMMA_SPEC_THREADS)
+      X[m] = make_double2(s_win[2 * m] * (double)src[2 * m], s_win[2 * m + 1] * (double)src[2 * m + 1]);
+    __syncthreads();
+    const double2* Z = zstockham<N2, 1, GAMMA_SPEC_THREADS>(X, Y, s_tw, tid);
+    for (int k = tid; k < p.kp; k += GAMMA_SPEC_THREADS) {
+      double v = 0.0;
+      if (k < NB) {
+        const double2 Xk = zreal_bin<N2>(Z, s_tw, k);
+        v = hypot(Xk.x, Xk.y);    // numpy abs(complex)
+      }
+      row[k] = v;
+    }
+    __syncthreads();            // Z read before the next frame's writes
+  }
+}
+
+__device__ __forceinline__ unsigned long long d2ord(double d) {
+  const unsigned long long u = (unsigned long long)__double_as_longlong(d);
+  return (u & 0x8000000000000000ull) ? ~u : (u | 0x8000000000000000ull);
+}
+__device__ __forceinline__ double ord2d(unsigned long long u) {
+  return __longlong_as_double((long long)((u & 0x8000000000000000ull) ? (u & 0x7fffffffffffffffull) : ~u));
+}
+
+// db[b][ch][t] = 10 log10(max(1e-10, sum_k W[ch][k] |X_t[k]| / nfft)) over a
+// tile of 64 frames of one clip x 64 channels; 256 threads, 4 x 4 outputs
+// each, K staged through LDS 32 bins at a time.
+__global__ __launch_bounds__(256) void gamma_erb_kernel(GammaParams p) {
+  __shared__ double As[32][64];   // [k][frame]
+  __shared__ double Ws[32][64];   // [k][channel]
+  __shared__ double s_red[2][4];
+  const int tid = threadIdx.x;
+  const int64_t b = blockIdx.y;
+  const int t0 = blockIdx.x * 64;
+  const int tf = tid >> 4, tc = tid & 15;
+  double acc[4][4] = {};
+  const double* M = p.mag + b * (int64_t)p.T * p.kp;
+  const int lf = tid >> 2, lk = (tid & 3) * 8;
+  const bool frame_ok = t0 + lf < p.T;
+  const double* arow = M + (int64_t)(frame_ok ? t0 + lf : 0) * p.kp + lk;
+  for (int k0 = 0; k0 < p.kp; k0 += 32) {
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+      double2 v = frame_ok ? *reinterpret_cast<const double2*>(arow + k0 + j) : make_double2(0.0, 0.0);
+      As[lk + j][lf] = v.x;
+      As[lk + j + 1][lf] = v.y;
+    }
+    const double* wsrc = p.weightsT + (int64_t)k0 * 64;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) (&Ws[0][0])[tid + 256 * j] = wsrc[tid + 256 * j];
+    __syncthreads();
+#pragma unroll 4
+    for (int kk = 0; kk < 32; ++kk) {
+      const double2 a01 = *reinterpret_cast<const double2*>(&As[kk][tf * 4]);
+      const double2 a23 = *reinterpret_cast<const double2*>(&As[kk][tf * 4 + 2]);
+      const double2 w01 = *reinterpret_cast<const double2*>(&Ws[kk][tc * 4]);
+      const double2 w23 = *reinterpret_cast<const double2*>(&Ws[kk][tc * 4 + 2]);
+      const double a[4] = {a01.x, a01.y, a23.x, a23.y};
+      const double w[4] = {w01.x, w01.y, w23.x, w23.y};
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[i][c] = fma(a[i], w[c], acc[i][c]);
+    }
+    __syncthreads();
+  }
+  double mx = -INFINITY, mn = INFINITY;
+  const double nfft = (double)p.nfft;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int t = t0 + tf * 4 + i;
+    if (t >= p.T) continue;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const double g = acc[i][c] / nfft;
+      const double db = 10.0 * log10(fmax(1e-10, g));   // - 10 log10(max(amin, ref=1)) == 0
+      p.db[(b * 64 + tc * 4 + c) * p.T + t] = db;
+      mx = fmax(mx, db);
+      mn = fmin(mn, db);
+    }
+  }
+  // block max / min -> one atomic each per tile (every tile lies in one clip)
+  for (int o = 32; o > 0; o >>= 1) {
+    mx = fmax(mx, __shfl_xor(mx, o));
+    mn = fmin(mn, __shfl_xor(mn, o));
+  }
+  if ((tid & 63) == 0) {
+    s_red[0][tid >> 6] = mx;
+    s_red[1][tid >> 6] = mn;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    mx = fmax(fmax(s_red[0][0], s_red[0][1]), fmax(s_red[0][2], s_red[0][3]));
+    mn = fmin(fmin(s_red[1][0], s_red[1][1]), fmin(s_red[1][2], s_red[1][3]));
+    atomicMax(&p.mm[2 * b], d2ord(mx));
+    atomicMin(&p.mm[2 * b + 1], d2ord(mn));
+  }
+}
+
+__global__ void gamma_init_kernel(unsigned long long* mm, int B) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < B) {
-    mm[2 * i] = 0u;
-    mm[2 * i + 1] = 0xffffffffu;
+    mm[2 * i] = 0ull;
+    mm[2 * i + 1] = ~0ull;
   }
 }
 
-__global__ __launch_bounds__(256) void gamma_quant_kernel(GammaParams p, const unsigned int* mm) {
+// power_to_db's top_db clamp, float32_to_int16 (per-clip max |x| scaling,
+// x 32767, truncation toward zero by astype(int16)), int16_to_float32 —
+// all on the float64 dB values.
+__global__ __launch_bounds__(256) void gamma_quant_kernel(GammaParams p) {
   const int64_t n = (int64_t)p.B * 64 * p.T;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
     const int64_t b = i / (64 * (int64_t)p.T);
-    const double mx = (double)ord2f(mm[2 * b]);
-    const double mn = (double)ord2f(mm[2 * b + 1]);
-    const double floor_db = mx - 80.0;                 // power_to_db top_db
-    const double lo = mn > floor_db ? mn : floor_db;
-    const double maxabs = fmax(fabs(mx), fabs(lo));
-    double x = (double)p.gt[i];
-    if (x < floor_db) x = floor_db;
-    if (maxabs > 1.0) x /= maxabs;                     // float32_to_int16
-    const double q = trunc(x * 32767.0);               // astype(int16): toward zero
-    p.out[i] = (float)(q / 32767.0);                   // int16_to_float32
+    const double mx = ord2d(p.mm[2 * b]);
+    const double mn = ord2d(p.mm[2 * b + 1]);
+    const double floor_db = mx - 80.0;                 // log_spec.max() - top_db
+    const double lo = fmax(mn, floor_db);
+    const double maxabs = fmax(fabs(mx), fabs(lo));    // np.max(np.abs(x)) after the clamp
+    double x = fmax(p.db[i], floor_db);
+    if (maxabs > 1.0) x = x / maxabs;
+    const double q = trunc(x * 32767.0);
+    p.out[i] = (float)(q / 32767.0);
   }
 }
 
-void launch_gamma(const GammaParams& p, hipStream_t s) {
-  unsigned int* mm = reinterpret_cast<unsigned int*>(p.maxbuf);
-  hipLaunchKernelGGL(gamma_init_kernel, dim3((p.B + 255) / 256), dim3(256), 0, s, mm, p.B);
+int gamma_kp(int nfft) { return ((nfft / 2 + 1) + 31) / 32 * 32; }
+
+size_t gamma_workspace_bytes(int64_t B, int64_t T, int nfft) {
+  auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
+  return al((size_t)B * T * gamma_kp(nfft) * sizeof(double)) + al((size_t)B * 64 * T * sizeof(double)) +
+         al((size_t)B * 2 * sizeof(unsigned long long));
+}
+
+template <int NFFT>
+static void launch_gamma_spec(const GammaParams& p, hipStream_t s) {
+  const void* k = reinterpret_cast<const void*>(gamma_spec_kernel<NFFT>);
+  // the in-LDS FFT owns its CUs (CU-exclusive LDS footprint, see logmel)
+  const LaunchInfo li = launch_info(k, GAMMA_SPEC_THREADS, gamma_spec_lds<NFFT>(), true);
+  if (!li.ok) return;
   const int64_t total = (int64_t)p.B * p.T;
-  int64_t blocks = (total + 1) / 2;
-  if (blocks > 4096) blocks = 4096;
-  // the same in-LDS FFT as the logmel frontend: CU-exclusive LDS footprint
-  // (mfma_cu_exclusive_lds keeps the kernel's own workgroups per CU)
-  auto go = [&](const void* k, auto kern) {
-    hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), mfma_cu_exclusive_lds(k, 256), s, p, mm);
-  };
+  int64_t blocks = std::min<int64_t>(total, (int64_t)li.ncu * li.per_cu * 4);
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(gamma_spec_kernel<NFFT>, dim3((unsigned)blocks), dim3(GAMMA_SPEC_THREADS), li.dyn, s, p);
+}
+
+void launch_gamma(const GammaParams& p, hipStream_t s) {
+  hipLaunchKernelGGL(gamma_init_kernel, dim3((p.B + 255) / 256), dim3(256), 0, s, p.mm, p.B);
   if (p.nfft == 2048)
-    go(reinterpret_cast<const void*>(gamma_frames_kernel<2048>), gamma_frames_kernel<2048>);
+    launch_gamma_spec<2048>(p, s);
   else if (p.nfft == 1024)
-    go(reinterpret_cast<const void*>(gamma_frames_kernel<1024>), gamma_frames_kernel<1024>);
+    launch_gamma_spec<1024>(p, s);
   else if (p.nfft == 512)
-    go(reinterpret_cast<const void*>(gamma_frames_kernel<512>), gamma_frames_kernel<512>);
-  hipLaunchKernelGGL(gamma_quant_kernel, dim3(2048), dim3(256), 0, s, p, mm);
+    launch_gamma_spec<512>(p, s);
+  else
+    return note_launch_error(hipErrorInvalidValue);
+  hipLaunchKernelGGL(gamma_erb_kernel, dim3((p.T + 63) / 64, p.B), dim3(256), 0, s, p);
+  hipLaunchKernelGGL(gamma_quant_kernel, dim3(2048), dim3(256), 0, s, p);
 }
 
 }  // namespace sedx

@@ -22,12 +22,20 @@
 //    storing wave, barrier, one agent-scope atomic add per slice; sc1 poll of
 //    the counter, barrier, sc1 loads of the payload.
 // Results are identical in both modes (same arithmetic; only the transport
-// differs).  The exchange buffer is double-buffered by step parity (a slice
+// differs).
+//
+// Arithmetic (template EXACT): false = the bf16 hi/lo x3 split above;
+// true = fp32 operands on v_mfma_f32_32x32x2_f32 (the reference's fp32
+// nn.GRU): each wave keeps its 32 gate rows x 64-K quarter of W_hh as 32 fp32
+// B-fragments (lane: row lane&31, k = 2 st + (lane>>5)) and reads h_{s-1}
+// from an fp32 [k][clip] LDS image whose rows are XOR-swizzled by (k>>3)&31
+// (conflict-free for both the gather's writes and the fragment reads).  The exchange buffer is double-buffered by step parity (a slice
 // publishes step gs only after it has gathered step gs-1 from every slice,
 // i.e. after all slices finished reading step gs-2's buffer; at group
 // boundaries the wait still runs although h is reset).  Flags, counters and
 // the id table are zeroed by hipMemsetAsync before every launch; every spin is
-// bounded and reports through *err.
+// bounded: a timeout sets sync->err and turns every later H value of that
+// workgroup into NaN, so it surfaces in framewise / clipwise output.
 #include "sedx_internal.h"
 
 namespace sedx {
@@ -83,6 +91,7 @@ struct GruSync {                      // zeroed every launch
 #define GRU_STAMP(i)
 #endif
 
+template <bool EXACT>
 __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__ G, int B, int T,
                                                        const float* __restrict__ whh,
                                                        const float* __restrict__ bhh,
@@ -92,6 +101,7 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
   __shared__ float part[4][3][32][33];         // K-quarter partial gate pre-activations
   __shared__ float hprev[32][33];              // own-slice h_{s-1}
   __shared__ int s_fast;
+  __shared__ int s_err;                        // a bounded spin timed out: outputs become NaN
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int pair = blockIdx.x & 7;             // dispatch residue -> one XCD (observed)
   const int p = blockIdx.x >> 3;               // slice 0..7
@@ -102,6 +112,7 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
 
   // ---- placement check (global protocol) ----
   if (tid == 0) {
+    s_err = 0;
     unsigned xid;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xid));
     __hip_atomic_store(&sync->xcc[pair][p], (xid & 0xffu) + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -112,6 +123,7 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
       __builtin_amdgcn_s_sleep(1);
       if (++spins > GRU_SPIN) {
         atomicOr(&sync->err, 1u);
+        s_err = 1;
         break;
       }
     }
@@ -130,19 +142,26 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
 
   // W_hh slice -> B fragments: B[k][n] = W_hh[gate row n][k]
   bf16x8_g Bhi[4], Blo[4];
+  float Bf[EXACT ? 32 : 1];
   {
     const float* wrow = whh + ((int64_t)dir * 768 + nt * 256 + 32 * p + (lane & 31)) * 256;
+    if constexpr (EXACT) {
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      const float4* q = reinterpret_cast<const float4*>(wrow + 16 * (4 * kq + ks) + 8 * h);
-      const float4 a = q[0], b = q[1];
-      const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-      uint4 hi, lo;
-      g_split8(v, hi, lo);
-      Bhi[ks] = __builtin_bit_cast(bf16x8_g, hi);
-      Blo[ks] = __builtin_bit_cast(bf16x8_g, lo);
+      for (int st = 0; st < 32; ++st) Bf[st] = wrow[64 * kq + 2 * st + h];
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const float4* q = reinterpret_cast<const float4*>(wrow + 16 * (4 * kq + ks) + 8 * h);
+        const float4 a = q[0], b = q[1];
+        const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        uint4 hi, lo;
+        g_split8(v, hi, lo);
+        Bhi[ks] = __builtin_bit_cast(bf16x8_g, hi);
+        Blo[ks] = __builtin_bit_cast(bf16x8_g, lo);
+      }
     }
   }
+  float* Af = reinterpret_cast<float*>(Aimg);  // EXACT: h_{s-1} [256 k][32 clips], swizzled
   const int u = tid & 31;                      // gate-phase unit (768 % 32 == 0)
   const float br = bhh[dir * 768 + 32 * p + u];
   const float bz = bhh[dir * 768 + 256 + 32 * p + u];
@@ -179,6 +198,7 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
             while (g_ld(Fl + tid * 16) < (unsigned)gs) {
               if (++spins > GRU_SPIN) {
                 atomicOr(&sync->err, 2u);
+                s_err = 1;
                 break;
               }
             }
@@ -190,6 +210,7 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
             __builtin_amdgcn_s_sleep(1);
             if (++spins > GRU_SPIN) {
               atomicOr(&sync->err, 1u);
+              s_err = 1;
               break;
             }
           }
@@ -231,11 +252,19 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
           if (it >= 32 * 32) break;
           const int c = it >> 5, oct = it & 31;
           const float* v = vv[k2];
-          uint4 hi, lo;
-          g_split8(v, hi, lo);
-          const int ks = oct >> 1, hh = oct & 1, sw = (c >> 2) & 3;
-          Aimg[(ks * 32 + c) * 4 + (hh ^ sw)] = hi;
-          Aimg[(ks * 32 + c) * 4 + ((2 + hh) ^ sw)] = lo;
+          if constexpr (EXACT) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const int k = 8 * oct + e;
+              Af[k * 32 + (c ^ ((k >> 3) & 31))] = v[e];
+            }
+          } else {
+            uint4 hi, lo;
+            g_split8(v, hi, lo);
+            const int ks = oct >> 1, hh = oct & 1, sw = (c >> 2) & 3;
+            Aimg[(ks * 32 + c) * 4 + (hh ^ sw)] = hi;
+            Aimg[(ks * 32 + c) * 4 + ((2 + hh) ^ sw)] = lo;
+          }
           if ((oct >> 2) == p) {
 #pragma unroll
             for (int e = 0; e < 8; ++e) hprev[c][8 * (oct & 3) + e] = v[e];
@@ -247,7 +276,15 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
       f32x16_g acc;
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-      {
+      if constexpr (EXACT) {
+        const int c = lane & 31;
+#pragma unroll
+        for (int st = 0; st < 32; ++st) {
+          const int k = 64 * kq + 2 * st + h;
+          const float a = Af[k * 32 + (c ^ ((k >> 3) & 31))];
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, Bf[st], acc, 0, 0, 0);
+        }
+      } else {
         const int c = lane & 31, sw = (c >> 2) & 3;
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
@@ -279,7 +316,7 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
             const float r = g_sigmoid(gi[i][0] + ghr);
             const float z = g_sigmoid(gi[i][1] + ghz);
             const float n = g_tanh(gi[i][2] + r * ghn);
-            hvs[i] = n + z * (hprev[c][u] - n);
+            hvs[i] = s_err ? __builtin_nanf("") : n + z * (hprev[c][u] - n);   // NaN propagates to every slice
           }
           float* xp = dst + c * 256 + 32 * p + u;
           if (c >= nc) {
@@ -306,7 +343,8 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
       for (int i = 0; i < 2; ++i) {
         const int pr = tid + 768 * i;
         const int c = pr >> 5;
-        if (pr < 1024 && c < nc) H[((int64_t)(c0 + c) * T + t) * 512 + dir * 256 + 32 * p + u] = hvs[i];
+        if (pr < 1024 && c < nc)
+          H[((int64_t)(c0 + c) * T + t) * 512 + dir * 256 + 32 * p + u] = hvs[i];
       }
     }
   }
@@ -322,17 +360,18 @@ size_t gru_coop_workspace_bytes(int B) {
 }
 
 void launch_gru_coop(const float* G, int B, int T, const float* whh, const float* bhh, float* H,
-                     void* ws, hipStream_t s) {
+                     void* ws, bool exact, bool allow_fast, hipStream_t s) {
   const int ngroups = (B + 31) / 32;
   const int nslots = ngroups < GRU_MAX_SLOTS ? ngroups : GRU_MAX_SLOTS;
   GruSync* sync = static_cast<GruSync*>(ws);
   float* X = reinterpret_cast<float*>(static_cast<char*>(ws) + ((sizeof(GruSync) + 255) & ~size_t(255)));
-  const int allow_fast = getenv("SEDX_GRU_GLOBAL_ONLY") ? 0 : 1;   // A/B switch
   (void)hipMemsetAsync(sync, 0, sizeof(GruSync), s);
-  hipLaunchKernelGGL(gru_coop_kernel, dim3(64), dim3(768),
-                     mfma_cu_exclusive_lds(reinterpret_cast<const void*>(gru_coop_kernel), 768), s, G, B, T,
-                     whh, bhh, H, X, sync,
-                     nslots, allow_fast);
+  if (exact)
+    launch_excl(gru_coop_kernel<true>, dim3(64), 768, s, G, B, T, whh, bhh, H, X, sync, nslots,
+                allow_fast ? 1 : 0);
+  else
+    launch_excl(gru_coop_kernel<false>, dim3(64), 768, s, G, B, T, whh, bhh, H, X, sync, nslots,
+                allow_fast ? 1 : 0);
 }
 
 }  // namespace sedx

@@ -164,22 +164,14 @@ void launch_linear_x3(const float* A, int M, int K, const void* Wp, int N, int B
   const dim3 grid((M + 127) / 128, N / BN);
   if (BN == 128) {
     if (act)
-      hipLaunchKernelGGL((linear_x3_kernel<128, 1>), grid, dim3(256),
-                         mfma_cu_exclusive_lds(reinterpret_cast<const void*>(linear_x3_kernel<128, 1>), 256), s,
-                         A, M, K, w, N, bias, C);
+      launch_excl(linear_x3_kernel<128, 1>, grid, 256, s, A, M, K, w, N, bias, C);
     else
-      hipLaunchKernelGGL((linear_x3_kernel<128, 0>), grid, dim3(256),
-                         mfma_cu_exclusive_lds(reinterpret_cast<const void*>(linear_x3_kernel<128, 0>), 256), s,
-                         A, M, K, w, N, bias, C);
+      launch_excl(linear_x3_kernel<128, 0>, grid, 256, s, A, M, K, w, N, bias, C);
   } else {
     if (act)
-      hipLaunchKernelGGL((linear_x3_kernel<64, 1>), grid, dim3(256),
-                         mfma_cu_exclusive_lds(reinterpret_cast<const void*>(linear_x3_kernel<64, 1>), 256), s,
-                         A, M, K, w, N, bias, C);
+      launch_excl(linear_x3_kernel<64, 1>, grid, 256, s, A, M, K, w, N, bias, C);
     else
-      hipLaunchKernelGGL((linear_x3_kernel<64, 0>), grid, dim3(256),
-                         mfma_cu_exclusive_lds(reinterpret_cast<const void*>(linear_x3_kernel<64, 0>), 256), s,
-                         A, M, K, w, N, bias, C);
+      launch_excl(linear_x3_kernel<64, 0>, grid, 256, s, A, M, K, w, N, bias, C);
   }
 }
 

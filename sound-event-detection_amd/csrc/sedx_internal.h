@@ -13,6 +13,10 @@
 #include <mutex>
 #include <stdint.h>
 
+#include <algorithm>
+#include <utility>
+#include <vector>
+
 namespace sedx {
 
 // ---- frontend -------------------------------------------------------------
@@ -45,18 +49,28 @@ void launch_features_bn0(const float* feat, int B, int T, const float* bn_scale,
                          const float* bn_mean, const float* bn_bias, float* out,
                          hipStream_t s);
 
+// Gammatone frontend, float64 end to end like the reference's numpy
+// (utils/gammatone/fftweight.py:126-168 computes in float64; power_to_db and
+// float32_to_int16 run on that float64 array, utils/features.py:361-370).
 struct GammaParams {
-  const float* audio;     // [B][L]
+  const float* audio;      // [B][L] (float32 samples, as librosa.load returns)
   int64_t L;
   int32_t B, T, hop, nfft;
   int32_t T_fill;          // frames actually filled by specgram's range(0, s-n, h)
-  const float2* twiddle;  // [nfft]
-  const float* window;    // [nfft] centred hann (specgram_window)
-  const float* weights;   // [64][nfft/2+1] ERB weights / nfft
-  float* gt;              // [B][64][T] workspace (linear magnitude)
-  float* maxbuf;          // [B] workspace
-  float* out;             // [B][64][T] dequantised features
+  int32_t kp;              // padded bin count (row stride of mag / rows of weightsT)
+  const double2* twiddle;  // [nfft] exp(-2 pi i m / nfft)
+  const double* window;    // [nfft] centred hann (specgram_window)
+  const double* weightsT;  // [kp][64] ERB weights (fft_weights), zero rows past nfft/2
+  double* mag;             // [B][T][kp] workspace: |FFT| (zero for unfilled frames)
+  double* db;              // [B][64][T] workspace: 10 log10(max(1e-10, W.|X| / nfft))
+  unsigned long long* mm;  // [B][2] workspace: ordered max / min of db per clip
+  float* out;              // [B][64][T] dequantised features
 };
+int gamma_kp(int nfft);
+// host: ERB weights [kp][nfilts] (zero rows past nfft/2), twiddles [2 nfft], window [nfft]
+void gamma_tables(double fs, int nfft, int nwin, int nfilts, double fmin, std::vector<double>& weightsT,
+                  int kp, std::vector<double>& twiddle, std::vector<double>& window);
+size_t gamma_workspace_bytes(int64_t B, int64_t T, int nfft);
 void launch_gamma(const GammaParams& p, hipStream_t s);
 
 // ---- conv stack -----------------------------------------------------------
@@ -82,28 +96,103 @@ void launch_conv3x3(const float* in, int B, int T, int F, int Cin, int Cout,
 // "Concurrent streams"): a frontend workgroup sharing a CU with MFMA waves of
 // another kernel (another stream) intermittently produced wrong FFT results;
 // with the pad, 0 of 128 runs differ.  Same-kernel sharing is unaffected.
-// Returns the pad in bytes (cached per kernel; thread-safe).
-inline size_t mfma_cu_exclusive_lds(const void* kernel, int block_threads) {
-  static std::mutex mu;
-  static std::map<const void*, size_t> cache;
-  std::lock_guard<std::mutex> lock(mu);
-  auto it = cache.find(kernel);
-  if (it != cache.end()) return it->second;
-  constexpr int lds_cu = 160 * 1024;   // gfx950 LDS per CU (the device attribute reports 64 KB)
+//
+// Launch failures that happen while preparing a launch (attribute queries /
+// hipFuncSetAttribute) are recorded per host thread and turned into
+// SEDX_EHIP by the C ABI entry point that issued the work
+// (take_launch_error); the launch is then skipped, never run with a
+// different LDS footprint.
+inline thread_local hipError_t t_launch_err = hipSuccess;
+inline void note_launch_error(hipError_t e) {
+  if (e != hipSuccess && t_launch_err == hipSuccess) t_launch_err = e;
+}
+inline hipError_t take_launch_error() {
+  const hipError_t e = t_launch_err;
+  t_launch_err = hipSuccess;
+  return e;
+}
+
+constexpr int LDS_PER_CU = 160 * 1024;   // gfx950 LDS per CU (the device attribute reports 64 KB)
+
+// Per (device, kernel) launch facts, computed once under a mutex: the CU
+// count, the kernel's workgroups per CU at its own LDS footprint, and the
+// dynamic LDS to launch with.  ok == false: the attribute calls failed (the
+// error was noted; callers skip the launch).
+struct LaunchInfo {
+  bool ok = false;
+  int ncu = 0;
   int per_cu = 0;
+  size_t dyn = 0;
+};
+// dyn_need: dynamic LDS the kernel itself uses.  exclusive: pad the dynamic
+// LDS so the kernel's workgroups fill the CU's LDS at its own occupancy.
+inline LaunchInfo launch_info(const void* kernel, int block_threads, size_t dyn_need, bool exclusive) {
+  static std::mutex mu;
+  static std::map<std::pair<int, const void*>, LaunchInfo> cache;
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) {
+    note_launch_error(e);
+    return LaunchInfo{};
+  }
+  std::lock_guard<std::mutex> lock(mu);
+  const auto key = std::make_pair(dev, kernel);
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  LaunchInfo li;
   hipFuncAttributes fa{};
-  (void)hipFuncGetAttributes(&fa, kernel);
-  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block_threads, 0);
-  if (per_cu < 1) per_cu = 1;
-  const size_t per_wg = ((size_t)lds_cu / (size_t)per_cu) & ~size_t(511);
-  size_t pad = per_wg > fa.sharedSizeBytes ? per_wg - fa.sharedSizeBytes : 0;
-  if (pad && hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pad) != hipSuccess)
-    pad = 0;
-  cache[kernel] = pad;
+  if ((e = hipFuncGetAttributes(&fa, kernel)) != hipSuccess ||
+      (e = hipDeviceGetAttribute(&li.ncu, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) {
+    note_launch_error(e);
+    return LaunchInfo{};
+  }
+  if (dyn_need && (e = hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)dyn_need)) != hipSuccess) {
+    note_launch_error(e);
+    return LaunchInfo{};
+  }
+  if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&li.per_cu, kernel, block_threads, dyn_need)) !=
+      hipSuccess) {
+    note_launch_error(e);
+    return LaunchInfo{};
+  }
+  if (li.per_cu < 1) li.per_cu = 1;
+  if (li.ncu < 1) li.ncu = 256;
+  li.dyn = dyn_need;
+  if (exclusive) {
+    const size_t per_wg = ((size_t)LDS_PER_CU / (size_t)li.per_cu) & ~size_t(511);
+    const size_t used = fa.sharedSizeBytes + dyn_need;
+    if (per_wg > used) {
+      li.dyn = dyn_need + (per_wg - used);
+      if ((e = hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)li.dyn)) !=
+          hipSuccess) {
+        note_launch_error(e);
+        return LaunchInfo{};
+      }
+    }
+  }
+  li.ok = true;
+  cache[key] = li;
   if (getenv("SEDX_DEBUG_LDS"))
-    fprintf(stderr, "sedx: kernel %p static LDS %zu B, %d workgroups/CU -> pad %zu B\n", kernel,
-            (size_t)fa.sharedSizeBytes, per_cu, pad);
-  return pad;
+    fprintf(stderr, "sedx: dev %d kernel %p static LDS %zu B, dyn %zu B, %d workgroups/CU\n", dev, kernel,
+            (size_t)fa.sharedSizeBytes, li.dyn, li.per_cu);
+  return li;
+}
+
+// MFMA kernels: the dynamic-LDS pad in bytes, or launch skipped (returns false).
+inline bool mfma_cu_exclusive_lds(const void* kernel, int block_threads, size_t* pad) {
+  const LaunchInfo li = launch_info(kernel, block_threads, 0, true);
+  *pad = li.dyn;
+  return li.ok;
+}
+
+// hipLaunchKernelGGL with the CU-exclusive LDS pad; skipped (error noted) if
+// the pad cannot be set
+template <typename... P, typename... A>
+inline void launch_excl(void (*kern)(P...), dim3 grid, int threads, hipStream_t s, A... args) {
+  size_t pad = 0;
+  if (!mfma_cu_exclusive_lds(reinterpret_cast<const void*>(kern), threads, &pad)) return;
+  hipLaunchKernelGGL(kern, grid, dim3(threads), pad, s, args...);
 }
 
 // sched: CONV_SCHED_INTS zeroed ints per launch (the 8 per-XCD tile-claim counters)
@@ -135,8 +224,10 @@ void launch_gru(const float* G, int B, int T, const float* whhT, const float* bh
 // exchanging h slices each step).  whh = W_hh [2][768][256] (natural layout);
 // ws >= gru_coop_workspace_bytes(B) bytes of device scratch (counters + exchange).
 size_t gru_coop_workspace_bytes(int B);
+// exact: fp32 MFMA (else the x3 bf16 split); allow_fast: XCD-local hand-off
+// when the placement allows it (else always the global protocol).
 void launch_gru_coop(const float* G, int B, int T, const float* whh, const float* bhh, float* H,
-                     void* ws, hipStream_t s);
+                     void* ws, bool exact, bool allow_fast, hipStream_t s);
 
 // MHA core: QKV [B][T][1536] (q|k|v, head h = cols 64h..64h+63) -> O [B][T][512]
 void launch_mha(const float* QKV, int B, int T, float* O, hipStream_t s);

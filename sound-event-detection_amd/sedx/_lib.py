@@ -22,7 +22,9 @@ EXPORTS = ['sedx_create', 'sedx_destroy', 'sedx_last_error', 'sedx_version', 'se
            'sedx_events', 'sedx_set_profiling', 'sedx_stage_times', 'sedx_set_precision', 'sedx_set_pipelined',
            'sedx_forward_windows_vote', 'sedx_events_workspace_size', 'sedx_events_device',
            'sedx_forward_i16', 'sedx_wav_parse', 'sedx_wav_decode_mono', 'sedx_resample_size',
-           'sedx_resample_workspace_size', 'sedx_resample']
+           'sedx_resample_workspace_size', 'sedx_resample', 'sedx_gamma_workspace_size',
+           'sedx_set_tuning', 'sedx_set_capture']
+TUNE_GRU_KERNEL, TUNE_GRU_HANDOFF = 0, 1
 PRECISION = {'exact': 0, 'x3': 1}
 STAGES = ['frontend', 'b1c1', 'b1c2', 'b2c1', 'b2c2', 'b3c1', 'b3c2', 'b4c1', 'b4c2', 'seq', 'head']
 
@@ -78,6 +80,9 @@ def lib():
         'sedx_forward_features': ([P, P, I64, I64, P, P, P, P, SZ, P], I32),
         'sedx_forward_i16': ([P, P, I64, I64, P, P, P, P, SZ, P], I32),
         'sedx_gamma_features': ([P, P, I64, I64, P, PI64, P, SZ, P], I32),
+        'sedx_gamma_workspace_size': ([P, I64, I64, PSZ], I32),
+        'sedx_set_tuning': ([P, I32, I32], I32),
+        'sedx_set_capture': ([P, I32, P, SZ], I32),
         'sedx_window_geometry': ([P, I64, F32, F32, I32, PI64, PI64, PI64], I32),
         'sedx_forward_windows': ([P, P, I64, I64, F32, F32, I32, P, P, SZ, P], I32),
         'sedx_window_workspace_size': ([P, I64, I64, F32, F32, I32, PSZ], I32),

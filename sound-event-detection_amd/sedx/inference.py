@@ -117,7 +117,9 @@ def gamma_features(model, audio):
                                      ctypes.byref(T), ctypes.c_void_p(0), 0, ctypes.c_void_p(0)),
                nat.h, 'gamma geometry')
     out = torch.empty((B, 64, T.value), dtype=torch.float32, device=x.device)
-    ws = torch.empty((B * 64 * T.value + 256 + 2 * B + 64) * 4, dtype=torch.uint8, device=x.device)
+    wsz = ctypes.c_size_t()
+    _lib.check(L.sedx_gamma_workspace_size(nat.h, B, n, ctypes.byref(wsz)), nat.h, 'gamma_workspace_size')
+    ws = torch.empty(wsz.value, dtype=torch.uint8, device=x.device)
     stream = ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
     _lib.check(L.sedx_gamma_features(nat.h, _ptr(x), B, n, _ptr(out), ctypes.byref(T), _ptr(ws),
                                      ws.numel(), stream), nat.h, 'gamma_features')
@@ -278,8 +280,9 @@ def inference_prob(model, waveforms, batch_size=32, device=None):
 
 
 def write_xml(audio_name, events, start=0, end=0):
-    """XML document of pytorch/predict.py:264-407 (SoundCaptionList)."""
-    s = ['<AudioDoc name="{}">\n'.format(audio_name), '\t<SoundCaptionList>\n']
+    """XML document of pytorch/predict.py:264-407 (SoundCaptionList); the
+    document is named after the file, not its path (predict.py:267)."""
+    s = ['<AudioDoc name="{}">\n'.format(audio_name.split('/')[-1]), '\t<SoundCaptionList>\n']
     if events:
         for e in events:
             s.append('\t\t<SoundSegment stime="{}" dur="{}" event="{}">{}</SoundSegment>\n'.format(

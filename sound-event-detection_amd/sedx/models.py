@@ -54,7 +54,9 @@ def init_bn(bn):
 
 def init_gru(rnn):
     """models.py:35-60: U(+-sqrt(3/fan_in)) per gate block, orthogonal n-gate
-    recurrent block, zero biases."""
+    recurrent block, zero biases -- of the forward-direction tensors only
+    (``weight_ih_l{i}`` etc.); the ``_reverse`` tensors keep nn.GRU's own
+    initialisation, as in the reference."""
     def _concat_init(tensor, init_funcs):
         length, fan_out = tensor.shape
         fan_in = length // len(init_funcs)
@@ -66,12 +68,11 @@ def init_gru(rnn):
         nn.init.uniform_(tensor, -math.sqrt(3 / fan_in), math.sqrt(3 / fan_in))
 
     for i in range(rnn.num_layers):
-        for sfx in ('', '_reverse') if rnn.bidirectional else ('',):
-            _concat_init(getattr(rnn, 'weight_ih_l%d%s' % (i, sfx)), [_inner_uniform] * 3)
-            nn.init.constant_(getattr(rnn, 'bias_ih_l%d%s' % (i, sfx)), 0)
-            _concat_init(getattr(rnn, 'weight_hh_l%d%s' % (i, sfx)),
-                         [_inner_uniform, _inner_uniform, nn.init.orthogonal_])
-            nn.init.constant_(getattr(rnn, 'bias_hh_l%d%s' % (i, sfx)), 0)
+        _concat_init(getattr(rnn, 'weight_ih_l%d' % i), [_inner_uniform] * 3)
+        nn.init.constant_(getattr(rnn, 'bias_ih_l%d' % i), 0)
+        _concat_init(getattr(rnn, 'weight_hh_l%d' % i),
+                     [_inner_uniform, _inner_uniform, nn.init.orthogonal_])
+        nn.init.constant_(getattr(rnn, 'bias_hh_l%d' % i), 0)
 
 
 def roundup(x):
@@ -167,7 +168,7 @@ class _Native(object):
         self.h = h
         self.device_index = device_index
         self.signature = None
-        self.precision = 'x3'   # the library default
+        self.precision = 'exact'   # the library default
 
     def load(self, state_dict):
         L = _lib.lib()
@@ -218,7 +219,7 @@ class _SedModel(nn.Module):
         self.conv_block3 = ConvBlock(128, 256)
         self.conv_block4 = ConvBlock(256, 512)
         self._natives = {}
-        self.precision = 'x3'
+        self.precision = 'exact'
         self.pipelined = False
 
     def _config(self):
@@ -264,8 +265,10 @@ class _SedModel(nn.Module):
         return nat
 
     def set_precision(self, mode):
-        """Conv-stack arithmetic: 'x3' (default; 3xbf16-split MFMA, fp32
-        accumulate, ~1e-6 from fp32) or 'exact' (fp32 MFMA)."""
+        """GEMM arithmetic (conv stack, GRU / MHA projections and recurrence,
+        AttBlock projection): 'exact' (default; fp32 operands and
+        accumulation, the reference's arithmetic) or 'x3' (opt-in;
+        3xbf16-split MFMA, fp32 accumulate, ~1e-6 from fp32)."""
         if mode not in _lib.PRECISION:
             raise ValueError('precision must be one of %s' % sorted(_lib.PRECISION))
         self.precision = mode

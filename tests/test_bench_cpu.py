@@ -41,3 +41,20 @@ def test_roofline_record(bench):
     assert r['peak'] == round(2500.0 / 3, 1)
     e = bench.roofline(stage, 32, 'exact')
     assert e['peak'] == 157.3 and 'fp32' in e['arith']
+
+
+def test_roofline_exact_unfused_and_names(bench):
+    stage = {s: 0.2 for s in bench.CONV_STAGES}
+    stage['b1c2'] = 1.0
+    e = bench.roofline(stage, 32, 'exact')
+    fused = bench.FUSED_BLOCK1['exact']
+    flops = bench.conv_flops('b1c2', 32, 1001) + (2.0 * 32 * 1001 * 64 * 64 * 9 if fused else 0.0)
+    assert e['flops_per_launch'] == flops
+    assert e['kernel'].startswith(bench.conv_kernel_name('b1c2', 'exact'))
+    assert bench.conv_kernel_name('b4c2', 'x3') == 'sedx::conv3x3_x3_kernel<8, 128, 2, false>'
+
+
+def test_cpu_info(bench):
+    info = bench.cpu_info()
+    assert info['host_logical_cpus'] >= 1
+    assert 'cpu_model' in info
