@@ -309,7 +309,7 @@ PROFILE_SUMMARY = os.path.join(REPO, 'profiles', 'r02_kernel_summary.json')
 
 
 # block 1's conv1 (Cin 1 -> 64) computed inside the b1c2 launch
-FUSED_BLOCK1 = {'x3': True, 'exact': False}
+FUSED_BLOCK1 = {'x3': True, 'exact': True}
 
 
 def conv_kernel_name(stage, precision):
@@ -319,7 +319,7 @@ def conv_kernel_name(stage, precision):
     bn = 64 if cout == 64 else 128
     if precision == 'x3':
         return 'sedx::conv3x3_x3_kernel<%d, %d, %d, %s>' % (F, bn, epi, 'true' if stage == 'b1c2' else 'false')
-    return 'sedx::conv3x3_kernel<%d, %d, %d>' % (F, bn, epi)
+    return 'sedx::conv3x3_kernel<%d, %d, %d, %s>' % (F, bn, epi, 'true' if stage == 'b1c2' else 'false')
 
 
 def profiled(kernel):
@@ -519,6 +519,9 @@ def main():
         extra.update(events_side(model, wave))
         extra['latency_b1'] = latency_b1(model, dev)
         other = 'x3' if args.precision == 'exact' else 'exact'
+        model.set_precision(other)
+        extra['latency_b1_%s' % other] = latency_b1(model, dev)
+        model.set_precision(args.precision)
         v2, e2, st2, p2, _ = clip_leg(model, wave, args, 1, 0, dev, other)
         extra['value_%s' % other] = {'value': round(v2, 2), 'unit': 'clips/s', 'dtype': DTYPE[other],
                                      'ms_per_step': round(e2 / args.steps * 1e3, 4),

@@ -38,6 +38,7 @@ struct DevWeights {
   float* c1_w = nullptr;
   float* c1_wt = nullptr;
   float* c1_b = nullptr;
+  float* zero = nullptr;   // 256 zero bytes (LDS-DMA source of out-of-clip halo pixels)
   float* wp[8] = {};    // packed conv weights: block k conv j -> index 2(k-1)+(j-1); [0] unused
   float* cb[8] = {};    // folded biases
   void* wx3[8] = {};    // split bf16 hi/lo packs for conv3x3_x3 (same indices)
@@ -280,7 +281,10 @@ WsLayout ws_layout(const sedx_handle* h, int64_t B, const Geometry& g) {
   size_t off = 0;
   l.x0 = off;
   off += align_up((size_t)B * g.T * 64);
-  size_t a = (size_t)B * g.T * 64 * 64;
+  // A: the zero-bordered bn0 output (block 1 is one fused launch in both
+  // modes: conv1's 64-channel activation never exists), then the conv1
+  // outputs of blocks 2-4, then the head scratch
+  size_t a = block1_pad_floats((int)B, (int)g.T);
   a = std::max(a, (size_t)B * g.T1 * 32 * 128);
   a = std::max(a, (size_t)B * g.T2 * 16 * 256);
   a = std::max(a, (size_t)B * g.T3 * 8 * 512);
@@ -334,14 +338,10 @@ sedx_status run_body(sedx_handle* h, int64_t B, const Geometry& g, float* ws, co
   capture(h, 0, X0, (size_t)B * g.T * 64, s);
   const bool x3 = h->precision == SEDX_PRECISION_X3;
   int* sched = reinterpret_cast<int*>(ws + l.sched);
-  if (x3) {
-    HIP_TRY(h, hipMemsetAsync(sched, 0, 7 * CONV_SCHED_INTS * sizeof(int), s));
-    // block 1 as one launch: conv1 computed inside conv2's halo staging (the
-    // b1c1 stage is then just the zero-bordered copy of the bn0 output)
-    launch_block1_fused_x3(X0, iB, (int)g.T, A, w.c1_wt, w.c1_b, w.wx3[1], w.cb[1], nullptr, nullptr, s);
-  } else {
-    launch_conv_c1(X0, iB, (int)g.T, w.c1_w, w.c1_b, A, s);
-  }
+  // block 1 as one launch in both modes: conv1 computed inside conv2's halo
+  // staging (the b1c1 stage is just the zero-bordered copy of the bn0 output)
+  if (x3) HIP_TRY(h, hipMemsetAsync(sched, 0, 7 * CONV_SCHED_INTS * sizeof(int), s));
+  launch_pad_x0(X0, iB, (int)g.T, A, s);
   struct L {
     const float* in;
     int T, F, cin, cout, idx, epi;
@@ -360,11 +360,13 @@ sedx_status run_body(sedx_handle* h, int64_t B, const Geometry& g, float* ws, co
     if (x3 && i == 0)
       launch_block1_fused_x3(nullptr, iB, c.T, A, w.c1_wt, w.c1_b, w.wx3[c.idx], w.cb[c.idx], c.out,
                              sched, s);
+    else if (i == 0)
+      launch_block1_exact(A, iB, c.T, w.c1_w, w.c1_b, w.wp[c.idx], w.cb[c.idx], c.out, w.zero, s);
     else if (x3)
       launch_conv3x3_x3(c.in, iB, c.T, c.F, c.cin, c.cout, w.wx3[c.idx], w.cb[c.idx], c.out, c.epi,
                         sched + i * CONV_SCHED_INTS, s);
     else
-      launch_conv3x3(c.in, iB, c.T, c.F, c.cin, c.cout, w.wp[c.idx], w.cb[c.idx], c.out, c.epi, s);
+      launch_conv3x3(c.in, iB, c.T, c.F, c.cin, c.cout, w.wp[c.idx], w.cb[c.idx], c.out, c.epi, w.zero, s);
     const size_t px = c.epi == EPI_STORE ? (size_t)c.T * c.F : c.epi == EPI_POOL2 ? (size_t)(c.T / 2) * (c.F / 2)
                                                                                    : (size_t)c.T;
     capture(h, 2 + i, c.out, (size_t)B * px * c.cout, s);
@@ -648,7 +650,9 @@ sedx_status sedx_finalize_weights(sedx_handle* h) {
   bn_fold("bn0", 64, s0, mu0, bi0);
   for (int i = 0; i < 64; ++i) sc0f[i] = (float)s0[i];
 
-  // ---- conv weights: fold BN, pack [Cin/8][9][8][Cout] ----
+  // ---- conv weights: fold BN, pack [Cin/4][9][khalf 2][Cout][ks 2] (exact:
+  // channel 2 ks + khalf of a 4-channel chunk; the MFMA B fragments of both
+  // k-steps are one 8-byte LDS read) ----
   const int ch[5] = {1, 64, 128, 256, 512};
   std::vector<float> packed[8], cbias[8], c1w(64 * 9), c1b(64);
   std::vector<uint16_t> packed_x3[8];
@@ -674,8 +678,8 @@ sedx_status sedx_finalize_weights(sedx_handle* h) {
       for (int o = 0; o < cout; ++o)
         for (int i = 0; i < cin; ++i)
           for (int t = 0; t < 9; ++t) {
-            const int chunk = i / 8, kc = i % 8;
-            pk[(((size_t)chunk * 9 + t) * 8 + kc) * cout + o] =
+            const int chunk = i / 4, kc = i % 4, ks = kc >> 1, kh = kc & 1;
+            pk[((((size_t)chunk * 9 + t) * 2 + kh) * cout + o) * 2 + ks] =
                 (float)(wt[((size_t)o * cin + i) * 9 + t] * sc[o]);
           }
       cbias[idx] = bias;
@@ -820,6 +824,8 @@ sedx_status sedx_finalize_weights(sedx_handle* h) {
     for (int t = 0; t < 9; ++t) c1wt[t * 64 + o] = c1w[o * 9 + t];
   add((void**)&W.c1_wt, c1wt.data(), c1wt.size() * 4);
   add((void**)&W.c1_b, c1b.data(), c1b.size() * 4);
+  std::vector<float> zeros(64, 0.f);
+  add((void**)&W.zero, zeros.data(), zeros.size() * 4);
   for (int i = 1; i < 8; ++i) {
     add((void**)&W.wp[i], packed[i].data(), packed[i].size() * 4);
     add((void**)&W.cb[i], cbias[i].data(), cbias[i].size() * 4);

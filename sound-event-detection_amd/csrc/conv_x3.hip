@@ -63,19 +63,6 @@ __device__ __forceinline__ void split8(const float4 a, const float4 b, uint4& hi
 
 __device__ __forceinline__ bf16x8 as_bf16x8(uint4 v) { return __builtin_bit_cast(bf16x8, v); }
 
-// LDS-DMA of 16 B per lane: LDS[m0 + lane * 16] = *src.  Inline asm, so the
-// compiler neither counts it nor guards LDS reads against it: the caller
-// orders it with counted vmcnt waits before its barriers (its own waits for
-// ordinary loads only get more conservative, never less).
-__device__ __forceinline__ void sedx_glds16(const void* src, uint32_t m0) {
-  // m0 is reserved to the compiler, which uses it nowhere else in this file
-  // (checked in the ISA); the clobber keeps it from caching a value there
-#pragma clang diagnostic push
-#pragma clang diagnostic ignored "-Winline-asm"
-  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(m0) : "memory", "m0");
-#pragma clang diagnostic pop
-}
-
 // 4x4 transpose across the 4 lanes of a quad (j = lane & 3): on entry lane j
 // holds column j of a 4x4 block in v[0..3] (v[k] = row k), on exit row j
 // (v[k] = column k).  Two butterfly stages (lane bit 0, lane bit 1), each a
@@ -899,13 +886,15 @@ __global__ __launch_bounds__(256) void pad_x0_kernel(const float* __restrict__ x
   }
 }
 
+void launch_pad_x0(const float* x0, int B, int T, float* xpad, hipStream_t s) {
+  const int64_t n = (int64_t)B * (T + 2) * 66;
+  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(pad_x0_kernel, dim3(blocks), dim3(256), 0, s, x0, B, T, xpad);
+}
+
 void launch_block1_fused_x3(const float* x0, int B, int T, float* xpad, const float* w1, const float* b1,
                             const void* wp, const float* bias, float* out, int* sched, hipStream_t s) {
-  if (x0) {
-    const int64_t n = (int64_t)B * (T + 2) * 66;
-    const int blocks = (int)std::min<int64_t>((n + 255) / 256, 4096);
-    hipLaunchKernelGGL(pad_x0_kernel, dim3(blocks), dim3(256), 0, s, x0, B, T, xpad);
-  }
+  if (x0) launch_pad_x0(x0, B, T, xpad, s);
   if (out)
     launch_x3_epi<64, 64, EPI_POOL2, true>(xpad, B, T, 64, 64, static_cast<const uint4*>(wp), bias, out,
                                            sched, s, w1, b1);

@@ -74,17 +74,24 @@ size_t gamma_workspace_bytes(int64_t B, int64_t T, int nfft);
 void launch_gamma(const GammaParams& p, hipStream_t s);
 
 // ---- conv stack -----------------------------------------------------------
-// block-1 conv1: Cin=1 -> 64, BN folded, ReLU.  X0 [B][T][64] -> A [B][T][64][64]
-void launch_conv_c1(const float* x0, int B, int T, const float* w /*[64][9]*/,
-                    const float* bias /*[64]*/, float* out, hipStream_t s);
+// bn0 output X0 [B][T][64] -> zero-bordered [B][T+2][66] (block1_pad_floats)
+void launch_pad_x0(const float* x0, int B, int T, float* xpad, hipStream_t s);
+// exact block 1 in one launch: conv1 (w1 [64][9], b1 [64], BN folded) computed
+// while conv2's halo is staged, conv2 + BN + ReLU + 2x2 avg-pool -> out
+// [B][T/2][32][64]
+void launch_block1_exact(const float* xpad, int B, int T, const float* w1, const float* b1, const float* wp,
+                         const float* bias, float* out, const float* zero16, hipStream_t s);
 
 enum ConvEpi { EPI_STORE = 0, EPI_POOL2 = 1, EPI_FMEAN = 2 };
 // 3x3 conv (pad 1) + folded BN + ReLU (+ epilogue), implicit GEMM on fp32 MFMA.
 //  in [B][T][F][Cin] -> EPI_STORE: [B][T][F][Cout], EPI_POOL2: [B][T/2][F/2][Cout],
-//  EPI_FMEAN: [B][T][Cout].  wp = packed [Cin/8][9][8][Cout], bias [Cout].
+//  EPI_FMEAN: [B][T][Cout].  wp = packed [Cin/4][9][2][Cout][2] (channel 2 ks + khalf), bias [Cout].
+//  F in {32, 16, 8}, Cout % 128 == 0 (block 1 runs launch_block1_exact).
+// zero16: >= 16 bytes of zeros in device memory (the halo DMA's source for
+// pixels outside the clip).
 void launch_conv3x3(const float* in, int B, int T, int F, int Cin, int Cout,
                     const float* wp, const float* bias, float* out, int epi,
-                    hipStream_t s);
+                    const float* zero16, hipStream_t s);
 
 // Same contract on bf16 MFMA with a 3-term hi/lo split (fp32-class accuracy).
 // wp = host-packed split weights [Cout/BN][Cin/16][9][BN][4 x 16 B] (BN = 64 if
@@ -184,6 +191,20 @@ inline bool mfma_cu_exclusive_lds(const void* kernel, int block_threads, size_t*
   const LaunchInfo li = launch_info(kernel, block_threads, 0, true);
   *pad = li.dyn;
   return li.ok;
+}
+
+// LDS-DMA of 16 B per lane: LDS[m0 + lane * 16] = *src.  Inline asm, so the
+// compiler neither counts it nor guards LDS reads against it: the caller
+// orders it with counted vmcnt waits before its barriers (its own waits for
+// ordinary loads only get more conservative, never less).
+__device__ __forceinline__ void sedx_glds16(const void* src, uint32_t m0) {
+  // m0 is reserved to the compiler, which uses it nowhere else in the kernels
+  // that call this (checked in their ISA); the clobber keeps it from caching
+  // a value there
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(m0) : "memory", "m0");
+#pragma clang diagnostic pop
 }
 
 // hipLaunchKernelGGL with the CU-exclusive LDS pad; skipped (error noted) if
