@@ -147,7 +147,7 @@ def cpu_baseline(name, model, dev, seconds, B=32):
     return out
 
 
-def cpu_baseline_window(name, seconds, max_clips=16):
+def cpu_baseline_window(name, seconds, max_clips=64):
     """predict.py's loop (pytorch/predict.py:297-349): every 10 s clip as six
     batch-1 forwards of 5 s windows at 1 s stride, merged and averaged, then
     thresholded — the oracle restatement of that loop, timed per clip."""
@@ -319,7 +319,8 @@ def conv_kernel_name(stage, precision):
     bn = 64 if cout == 64 else 128
     if precision == 'x3':
         return 'sedx::conv3x3_x3_kernel<%d, %d, %d, %s>' % (F, bn, epi, 'true' if stage == 'b1c2' else 'false')
-    return 'sedx::conv3x3_kernel<%d, %d, %d, %s>' % (F, bn, epi, 'true' if stage == 'b1c2' else 'false')
+    # exact: 8-wave tiles at the bench shapes (4-wave tiles only for small grids)
+    return 'sedx::conv3x3_kernel<%d, %d, %d, %s, 8>' % (F, bn, epi, 'true' if stage == 'b1c2' else 'false')
 
 
 def profiled(kernel):

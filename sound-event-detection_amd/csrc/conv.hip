@@ -333,11 +333,11 @@ static void launch_f_bn_w(const float* in, int B, int T, int Cin, int Cout, cons
   constexpr int NT = 64 * WAVES;
   dim3 grid(B * ((T + TT - 1) / TT), Cout / BN);
   if (epi == EPI_STORE)
-    launch_excl(conv3x3_kernel<F, BN, EPI_STORE, FUSE, WAVES>, grid, NT, s, in, T, Cin, Cout, wp, bias, out, w1, b1, zero16);
+    launch_kernel(conv3x3_kernel<F, BN, EPI_STORE, FUSE, WAVES>, grid, NT, s, in, T, Cin, Cout, wp, bias, out, w1, b1, zero16);
   else if (epi == EPI_POOL2)
-    launch_excl(conv3x3_kernel<F, BN, EPI_POOL2, FUSE, WAVES>, grid, NT, s, in, T, Cin, Cout, wp, bias, out, w1, b1, zero16);
+    launch_kernel(conv3x3_kernel<F, BN, EPI_POOL2, FUSE, WAVES>, grid, NT, s, in, T, Cin, Cout, wp, bias, out, w1, b1, zero16);
   else
-    launch_excl(conv3x3_kernel<F, BN, EPI_FMEAN, FUSE, WAVES>, grid, NT, s, in, T, Cin, Cout, wp, bias, out, w1, b1, zero16);
+    launch_kernel(conv3x3_kernel<F, BN, EPI_FMEAN, FUSE, WAVES>, grid, NT, s, in, T, Cin, Cout, wp, bias, out, w1, b1, zero16);
 }
 
 // 8-wave tiles when they make at least two workgroups per CU of the chip,

@@ -40,7 +40,6 @@ namespace sedx {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 
@@ -368,23 +367,18 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
       uint4 hi, lo;                                                                     \
       const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);                                 \
       if constexpr (FUSE) {                                                             \
-        /* the chunk's 16 conv1 channels, two per packed fma (w1 is [tap][64]:  */      \
-        /* wave-uniform scalar pairs); per channel the fma chain of conv_c1      */      \
+        /* the chunk's 16 conv1 channels (w1 is [tap][64]: wave-uniform scalars); */    \
+        /* per channel the fma chain of conv1, scalar v_fma_f32: no packed f32   */      \
+        /* VALU beside MFMAs (see sedx_internal.h "packed FP32")                  */      \
         const int ch0 = (c_).chunk * 16;                                                \
         _Pragma("unroll") for (int hh = 0; hh < 2; ++hh) {                              \
-          f32x2 a2[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};               \
-          _Pragma("unroll") for (int k = 0; k < 9; ++k) {                               \
-            const f32x2 xx = {xr[i][k], xr[i][k]};                                      \
-            _Pragma("unroll") for (int j = 0; j < 4; ++j)                               \
-              a2[j] = __builtin_elementwise_fma(                                        \
-                  *reinterpret_cast<const f32x2*>(w1 + k * 64 + ch0 + 8 * hh + 2 * j), xx, a2[j]); \
-          }                                                                             \
+          float a8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};                       \
+          _Pragma("unroll") for (int k = 0; k < 9; ++k)                                 \
+            _Pragma("unroll") for (int j = 0; j < 8; ++j)                               \
+              a8[j] = fmaf(w1[k * 64 + ch0 + 8 * hh + j], xr[i][k], a8[j]);             \
           float o[8];                                                                   \
-          _Pragma("unroll") for (int j = 0; j < 4; ++j) {                               \
-            const f32x2 bb = *reinterpret_cast<const f32x2*>(b1 + ch0 + 8 * hh + 2 * j); \
-            o[2 * j] = rok[i] ? fmaxf(a2[j].x + bb.x, 0.0f) : 0.0f;                     \
-            o[2 * j + 1] = rok[i] ? fmaxf(a2[j].y + bb.y, 0.0f) : 0.0f;                 \
-          }                                                                             \
+          _Pragma("unroll") for (int j = 0; j < 8; ++j)                                 \
+            o[j] = rok[i] ? fmaxf(a8[j] + b1[ch0 + 8 * hh + j], 0.0f) : 0.0f;           \
           split8(make_float4(o[0], o[1], o[2], o[3]), make_float4(o[4], o[5], o[6], o[7]), hi, lo); \
           dst_[a_rec[i] + hh] = hi;                                                     \
           dst_[a_rec[i] + 2 + hh] = lo;                                                 \
@@ -814,9 +808,9 @@ static void launch_x3_epi(const float* in, int B, int T, int Cin, int Cout, cons
                           const float* bias, float* out, int* sched, hipStream_t s,
                           const float* w1 = nullptr, const float* b1 = nullptr) {
   constexpr int TT = ConvGeom<F, BN>::TT;
-  // workgroups resident on the whole device + the CU-exclusive LDS pad (per device)
+  // workgroups resident on the whole device (per device)
   const LaunchInfo li =
-      launch_info(reinterpret_cast<const void*>(conv3x3_x3_kernel<F, BN, EPI, FUSE>), 512, 0, true);
+      launch_info(reinterpret_cast<const void*>(conv3x3_x3_kernel<F, BN, EPI, FUSE>), 512, 0, false);
   if (!li.ok) return;
   const int resident = li.ncu * li.per_cu;
   const size_t pad = li.dyn;

@@ -105,13 +105,10 @@ __device__ __forceinline__ float2 real_bin(const float2* Z, const float2* tw, in
 // sit in registers; the next frame's samples are loaded into registers while
 // the current frame is transformed.
 //
-// One 1024-thread workgroup per CU, and the workgroup claims the CU's whole
-// LDS (the dynamic part beyond the mel weights is padding): no workgroup of
-// another kernel can share its CU.  Measured on MI355X (tools/fe_race.cpp):
-// this FFT, sharing a CU with MFMA (or other heavy) waves of a kernel on
-// another stream, intermittently produced wrong spectra (11 of 32 launches);
-// CU-exclusive, 0 of 64.  MFMA kernels are padded the same way
-// (mfma_cu_exclusive_lds).
+// 1024-thread workgroups (16 waves), as many per CU as the LDS allows.
+// Built without packed FP32 VALU (Makefile): with v_pk_* arithmetic this FFT
+// returned wrong spectra while MFMA waves shared its CU (sedx_internal.h
+// "packed FP32").
 constexpr int FE_WAVES = 16;
 
 template <int NFFT, bool I16>
@@ -218,15 +215,15 @@ __global__ __launch_bounds__(64 * FE_WAVES) void logmel_kernel(FrontendParams p)
   }
 }
 
-// one CU-exclusive workgroup per CU; every wave walks several frames, so the
-// register prefetch of the next frame overlaps the current FFT
+// at most the resident workgroups of the chip; every wave walks several
+// frames, so the register prefetch of the next frame overlaps the current FFT
 // (launch facts per device: launch_info)
 constexpr size_t FE_MEL_LDS = 16 * 1024;   // room for the packed mel weights (<= 2 (n_fft/2+1) floats)
 
 template <int NFFT, bool I16>
 static void launch_logmel_t(const FrontendParams& p0, int64_t total, hipStream_t s) {
   const LaunchInfo li =
-      launch_info(reinterpret_cast<const void*>(logmel_kernel<NFFT, I16>), 64 * FE_WAVES, FE_MEL_LDS, true);
+      launch_info(reinterpret_cast<const void*>(logmel_kernel<NFFT, I16>), 64 * FE_WAVES, FE_MEL_LDS, false);
   if (!li.ok) return;
   FrontendParams p = p0;
   p.mel_lds_floats = (int32_t)(li.dyn / 4);
@@ -521,8 +518,7 @@ size_t gamma_workspace_bytes(int64_t B, int64_t T, int nfft) {
 template <int NFFT>
 static void launch_gamma_spec(const GammaParams& p, hipStream_t s) {
   const void* k = reinterpret_cast<const void*>(gamma_spec_kernel<NFFT>);
-  // the in-LDS FFT owns its CUs (CU-exclusive LDS footprint, see logmel)
-  const LaunchInfo li = launch_info(k, GAMMA_SPEC_THREADS, gamma_spec_lds<NFFT>(), true);
+  const LaunchInfo li = launch_info(k, GAMMA_SPEC_THREADS, gamma_spec_lds<NFFT>(), false);
   if (!li.ok) return;
   const int64_t total = (int64_t)p.B * p.T;
   int64_t blocks = std::min<int64_t>(total, (int64_t)li.ncu * li.per_cu * 4);

@@ -367,10 +367,10 @@ void launch_gru_coop(const float* G, int B, int T, const float* whh, const float
   float* X = reinterpret_cast<float*>(static_cast<char*>(ws) + ((sizeof(GruSync) + 255) & ~size_t(255)));
   (void)hipMemsetAsync(sync, 0, sizeof(GruSync), s);
   if (exact)
-    launch_excl(gru_coop_kernel<true>, dim3(64), 768, s, G, B, T, whh, bhh, H, X, sync, nslots,
+    launch_kernel(gru_coop_kernel<true>, dim3(64), 768, s, G, B, T, whh, bhh, H, X, sync, nslots,
                 allow_fast ? 1 : 0);
   else
-    launch_excl(gru_coop_kernel<false>, dim3(64), 768, s, G, B, T, whh, bhh, H, X, sync, nslots,
+    launch_kernel(gru_coop_kernel<false>, dim3(64), 768, s, G, B, T, whh, bhh, H, X, sync, nslots,
                 allow_fast ? 1 : 0);
 }
 

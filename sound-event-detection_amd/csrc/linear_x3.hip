@@ -164,14 +164,14 @@ void launch_linear_x3(const float* A, int M, int K, const void* Wp, int N, int B
   const dim3 grid((M + 127) / 128, N / BN);
   if (BN == 128) {
     if (act)
-      launch_excl(linear_x3_kernel<128, 1>, grid, 256, s, A, M, K, w, N, bias, C);
+      launch_kernel(linear_x3_kernel<128, 1>, grid, 256, s, A, M, K, w, N, bias, C);
     else
-      launch_excl(linear_x3_kernel<128, 0>, grid, 256, s, A, M, K, w, N, bias, C);
+      launch_kernel(linear_x3_kernel<128, 0>, grid, 256, s, A, M, K, w, N, bias, C);
   } else {
     if (act)
-      launch_excl(linear_x3_kernel<64, 1>, grid, 256, s, A, M, K, w, N, bias, C);
+      launch_kernel(linear_x3_kernel<64, 1>, grid, 256, s, A, M, K, w, N, bias, C);
     else
-      launch_excl(linear_x3_kernel<64, 0>, grid, 256, s, A, M, K, w, N, bias, C);
+      launch_kernel(linear_x3_kernel<64, 0>, grid, 256, s, A, M, K, w, N, bias, C);
   }
 }
 

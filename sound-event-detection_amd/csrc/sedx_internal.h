@@ -96,13 +96,20 @@ void launch_conv3x3(const float* in, int B, int T, int F, int Cin, int Cout,
 // Same contract on bf16 MFMA with a 3-term hi/lo split (fp32-class accuracy).
 // wp = host-packed split weights [Cout/BN][Cin/16][9][BN][4 x 16 B] (BN = 64 if
 // Cout == 64 else 128), slots XOR-swizzled by ((n >> 2) & 3).
-// MFMA kernels are launched with a dynamic-LDS pad that makes their
-// workgroups fill a CU's LDS (LDS per CU / the kernel's own workgroups per
-// CU): no workgroup of another kernel can then share a CU with MFMA waves.
-// Measured on MI355X (tools/fe_race.cpp, tools/mfma_corun.cpp, DESIGN.md
-// "Concurrent streams"): a frontend workgroup sharing a CU with MFMA waves of
-// another kernel (another stream) intermittently produced wrong FFT results;
-// with the pad, 0 of 128 runs differ.  Same-kernel sharing is unaffected.
+//
+// packed FP32: no kernel of this library contains packed FP32 VALU
+// instructions (v_pk_add_f32 / v_pk_mul_f32 / v_pk_fma_f32); the Makefile
+// compiles with -fno-slp-vectorize -fno-vectorize and `make isa-check`
+// (tests/test_host_cpu.py) verifies every kernel's ISA.  Measured on MI355X
+// (tools/fe_race.cpp, round 2): an FFT kernel whose float2 arithmetic the
+// compiler had packed into v_pk_* produced wrong values in 16-27 of 64
+// launches while an MFMA loop ran on the same CU from another stream (the
+// round-1 "co-residency corruption"); the identical kernel compiled without
+// packed FP32, 0 of 192.  The corruption needs only the two instruction kinds
+// on one SIMD — any kernel with MFMAs whose own VALU code was packed (the x3
+// fused block 1's conv1 chain, epilogues) was exposed to it through its own
+// partner waves — so the fix is the instruction ban, not CU-exclusive LDS
+// footprints (round 1's workaround, removed).
 //
 // Launch failures that happen while preparing a launch (attribute queries /
 // hipFuncSetAttribute) are recorded per host thread and turned into
@@ -186,13 +193,6 @@ inline LaunchInfo launch_info(const void* kernel, int block_threads, size_t dyn_
   return li;
 }
 
-// MFMA kernels: the dynamic-LDS pad in bytes, or launch skipped (returns false).
-inline bool mfma_cu_exclusive_lds(const void* kernel, int block_threads, size_t* pad) {
-  const LaunchInfo li = launch_info(kernel, block_threads, 0, true);
-  *pad = li.dyn;
-  return li.ok;
-}
-
 // LDS-DMA of 16 B per lane: LDS[m0 + lane * 16] = *src.  Inline asm, so the
 // compiler neither counts it nor guards LDS reads against it: the caller
 // orders it with counted vmcnt waits before its barriers (its own waits for
@@ -207,13 +207,12 @@ __device__ __forceinline__ void sedx_glds16(const void* src, uint32_t m0) {
 #pragma clang diagnostic pop
 }
 
-// hipLaunchKernelGGL with the CU-exclusive LDS pad; skipped (error noted) if
-// the pad cannot be set
+// hipLaunchKernelGGL after the per-device launch facts were established;
+// skipped (error noted) if they could not be
 template <typename... P, typename... A>
-inline void launch_excl(void (*kern)(P...), dim3 grid, int threads, hipStream_t s, A... args) {
-  size_t pad = 0;
-  if (!mfma_cu_exclusive_lds(reinterpret_cast<const void*>(kern), threads, &pad)) return;
-  hipLaunchKernelGGL(kern, grid, dim3(threads), pad, s, args...);
+inline void launch_kernel(void (*kern)(P...), dim3 grid, int threads, hipStream_t s, A... args) {
+  if (!launch_info(reinterpret_cast<const void*>(kern), threads, 0, false).ok) return;
+  hipLaunchKernelGGL(kern, grid, dim3(threads), 0, s, args...);
 }
 
 // sched: CONV_SCHED_INTS zeroed ints per launch (the 8 per-XCD tile-claim counters)

@@ -79,9 +79,9 @@ void launch_linear(const float* A, int M, int K, const float* W, int N, const fl
                    float* C, int act, hipStream_t s) {
   dim3 grid((M + 127) / 128, N / 64);
   if (act == 1)
-    launch_excl(linear_kernel<1>, grid, 256, s, A, M, K, W, N, bias, C);
+    launch_kernel(linear_kernel<1>, grid, 256, s, A, M, K, W, N, bias, C);
   else
-    launch_excl(linear_kernel<0>, grid, 256, s, A, M, K, W, N, bias, C);
+    launch_kernel(linear_kernel<0>, grid, 256, s, A, M, K, W, N, bias, C);
 }
 
 // ---------------------------------------------------------------------------

@@ -103,3 +103,19 @@ def test_window_geometry_host_rules():
     assert O.window_starts(10.0, 5, 1) == [0, 1, 2, 3, 4, 5]
     assert len(O.window_starts(10.0, 6, 0.5)) == 9
     assert O.window_starts(3.0, 5, 1) == [0]
+
+
+def test_no_packed_fp32_in_any_kernel():
+    """Every kernel's gfx950 ISA is free of packed FP32 VALU (v_pk_add/mul/
+    fma_f32): measured on MI355X, packed FP32 beside MFMA waves on the same
+    SIMD returns wrong values (tools/fe_race.cpp; sedx_internal.h "packed
+    FP32").  `make isa-check` compiles each .hip with the library's flags
+    (-fno-slp-vectorize -fno-vectorize) and greps the assembly."""
+    import shutil
+    import subprocess
+    if shutil.which('/opt/rocm/bin/hipcc') is None:
+        pytest.skip('needs hipcc')
+    pkg = os.path.join(REPO, 'sound-event-detection_amd')
+    r = subprocess.run(['make', '-s', '-C', pkg, '-j8', 'isa-check'], capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert 'no packed FP32 VALU' in r.stdout

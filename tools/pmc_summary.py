@@ -8,7 +8,8 @@ the bytes of a wide (16 B/lane) coalesced read, so hbm_read = 2 * FETCH_SIZE
 * 1024 (both raw and corrected values are kept); WRITE_SIZE is exact for
 16-B stores.
 
-usage: python tools/pmc_summary.py gpurun_out/prof r01
+usage: python tools/pmc_summary.py gpurun_out/prof/exact r02_exact
+       python tools/pmc_summary.py merge r02 r02_exact r02_x3
 """
 import csv
 import json
@@ -76,5 +77,19 @@ def main(src, tag):
     print('\n'.join(lines))
 
 
+def merge(tags, out_tag):
+    """profiles/<out_tag>_kernel_summary.json = the union of several runs'
+    summaries (earlier tags win for kernels present in more than one)."""
+    out = {}
+    for t in reversed(tags):
+        with open(os.path.join('profiles', '%s_kernel_summary.json' % t)) as f:
+            out.update(json.load(f))
+    with open(os.path.join('profiles', '%s_kernel_summary.json' % out_tag), 'w') as f:
+        json.dump(out, f, indent=1, sort_keys=True)
+
+
 if __name__ == '__main__':
-    main(sys.argv[1], sys.argv[2])
+    if sys.argv[1] == 'merge':     # python tools/pmc_summary.py merge OUT TAG1 TAG2 ...
+        merge(sys.argv[3:], sys.argv[2])
+    else:
+        main(sys.argv[1], sys.argv[2])

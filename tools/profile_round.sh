@@ -1,25 +1,29 @@
 #!/bin/bash
-# GPU-box profiling sequence: full bench (with CPU baseline) -> rocprofv3
-# kernel-trace stats -> FETCH_SIZE pass -> WRITE_SIZE pass (separate passes:
-# FETCH_SIZE and WRITE_SIZE do not fit one TCC pass on gfx950) -> MFMA busy
-# cycles + GRBM_GUI_ACTIVE pass (MFMA utilisation, effective clock).
+# GPU-box profiling sequence for one round: full bench (with CPU baseline),
+# then for each arithmetic (exact = the headline, x3 = the opt-in leg):
+# rocprofv3 kernel-trace stats -> FETCH_SIZE pass -> WRITE_SIZE pass
+# (separate passes: FETCH_SIZE and WRITE_SIZE do not fit one TCC pass on
+# gfx950) -> MFMA busy cycles + GRBM_GUI_ACTIVE pass (MFMA utilisation,
+# effective clock).  Profiling passes run the headline only (--no-side) on one
+# stream so per-kernel averages time un-overlapped launches.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/prof
 mkdir -p $OUT
-TAG=${TAG:-r01}
-ARGS="${BENCH_ARGS:-}"
 step() {
   local name=$1 t=$2; shift 2
   echo "== $name"
   timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1
   local rc=$?
-  echo "== $name rc=$rc"; tail -n 5 "$OUT/$name.log"
+  echo "== $name rc=$rc"; tail -n 3 "$OUT/$name.log" | cut -c1-300
   if [ $rc -ne 0 ]; then echo "stopping"; exit $rc; fi
 }
-step bench_full 600 python bench.py --steps 20 --warmup 3 $ARGS
-step kt 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o kt -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-side --streams 1 $ARGS
-step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o pmc -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-side --streams 1 $ARGS
-step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o pmc -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-side --streams 1 $ARGS
-step pmc_mfma 600 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $OUT/pmc_mfma -o pmc -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-side --streams 1 $ARGS
+[ -n "$NO_FULL" ] || step bench_full 600 python bench.py --steps 20 --warmup 3
+for P in ${PRECISIONS:-exact x3}; do
+  A="--no-cpu-baseline --no-side --streams 1 --precision $P"
+  step kt_$P 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/$P/kt -o kt -- python bench.py --steps 10 --warmup 2 $A
+  step fetch_$P 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/$P/pmc_fetch -o pmc -- python bench.py --steps 3 --warmup 1 $A
+  step write_$P 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/$P/pmc_write -o pmc -- python bench.py --steps 3 --warmup 1 $A
+  step mfma_$P 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $OUT/$P/pmc_mfma -o pmc -- python bench.py --steps 3 --warmup 1 $A
+done
 echo ALLDONE
