@@ -45,8 +45,7 @@ struct ExactGeom {
   static constexpr int W_SZ = 9 * KC * BN;           // floats: [tap][khalf][n][ks]
   static constexpr int BUF = A_SZ + W_SZ;            // one chunk's staging buffer
   static constexpr int NBUF = 3;                     // ring: DMA two chunks ahead
-  static constexpr int W1_OFF = NBUF * BUF;          // FUSE: conv1 weights + bias
-  static constexpr int MAIN = W1_OFF + (FUSE ? 64 * 9 + 64 : 0);
+  static constexpr int MAIN = NBUF * BUF;
   static constexpr int EC = BN / 2;                  // epilogue pass: half of the n-tile
   static constexpr int CPAD = EC + 4;
   static constexpr int LDS_EPI = BM * CPAD;
@@ -92,12 +91,20 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void conv3x3_kernel
 
   // fragment offsets (floats): A pixel p -> [p][khalf], [p][2 + khalf] =
   // (ks 0, ks 1); B [tap][khalf][n][ks]
+  // A row m of MFMA tile mt of wave wm is tile pixel (t, f) = pix_t / pix_f:
+  // row-major (pixel 64 wm + 32 mt + m) except at F = 64, where a wave
+  // covers two t-rows x 32 bins, so every 2x2 pooling window lies in one
+  // lane's accumulators (bins m, m+1 in registers r, r+1; rows in mt 0, 1)
+  auto pix_t = [&](int mt, int m) {
+    return F == 64 ? 2 * (wm >> 1) + mt : (wm * WM + mt * 32 + m) / F;
+  };
+  auto pix_f = [&](int mt, int m) {
+    return F == 64 ? 32 * (wm & 1) + m : (wm * WM + mt * 32 + m) % F;
+  };
   int a_off[MT];
 #pragma unroll
-  for (int mt = 0; mt < MT; ++mt) {
-    const int p = wm * WM + mt * 32 + (lane & 31);
-    a_off[mt] = ((p / F) * CS + (p % F)) * KC + khalf;
-  }
+  for (int mt = 0; mt < MT; ++mt)
+    a_off[mt] = (pix_t(mt, lane & 31) * CS + pix_f(mt, lane & 31)) * KC + khalf;
   int b_off[NT];
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) b_off[nt] = (khalf * BN + wn * 64 + nt * 32 + (lane & 31)) * 2;
@@ -153,40 +160,47 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void conv3x3_kernel
     asm volatile("" ::: "memory");                                                                     \
   }
 
-  // ---- FUSE: conv1 weights in LDS, the 3x3 X0 window of each staged pixel in
-  // registers; conv1 (BN folded + ReLU) of a chunk's 4 channels computed into
-  // the halo image while the previous chunk's MFMAs run ----
+  // ---- FUSE: the 3x3 X0 window of each staged pixel in registers; conv1
+  // (BN folded + ReLU) of a chunk's 4 channels computed into the halo image
+  // while the previous chunk's MFMAs run (its weights by scalar loads) ----
   bool pin[G::NA];
+  float pmask[G::NA];
   float xw[FUSE ? G::NA : 1][9];
   if constexpr (FUSE) {
-    for (int i = tid; i < 64 * 9 + 64; i += EX_THREADS)
-      smem[G::W1_OFF + i] = i < 64 * 9 ? w1[i] : b1[i - 64 * 9];
 #pragma unroll
     for (int i = 0; i < G::NA; ++i) {
       const int pix = tid + EX_THREADS * i;
       const int r = pix / CS, c = pix - (pix / CS) * CS;
       const int t = t0 - 1 + r, f = c - 1;
       pin[i] = pix < PL && t >= 0 && t < T && f >= 0 && f < F;
+      pmask[i] = pin[i] ? 1.0f : 0.0f;
       // X0pad [B][T+2][66]: (t, f) of X0 at (t+1, f+1); window corner (t, f)
       const int64_t src = pin[i] ? ((int64_t)b * (T + 2) + t) * 66 + f : 0;
 #pragma unroll
-      for (int k = 0; k < 9; ++k) xw[i][k] = pin[i] ? in[src + (k / 3) * 66 + (k % 3)] : 0.0f;
+      for (int k = 0; k < 9; ++k) xw[i][k] = in[src + (k / 3) * 66 + (k % 3)];   // masked by pmask
     }
-    __syncthreads();   // w1 / b1 in LDS; no DMA in flight yet
+    // the window loads retire here, on every path, so the compiler's wait
+    // tracking does not carry them into the chunk loop, where a wait for them
+    // would drain the LDS-DMAs in flight (vmcnt 0; expcnt, lgkmcnt untouched)
+    __builtin_amdgcn_s_waitcnt(0x0F70);
   }
 #define SEDX_EX_CONV1(chunk_, buf_)                                                                    \
   {                                                                                                    \
     float* As_ = smem + (buf_) * G::BUF;                                                               \
-    const float* w1s_ = smem + G::W1_OFF + (chunk_) * KC * 9;                                          \
-    const float* b1s_ = smem + G::W1_OFF + 64 * 9 + (chunk_) * KC;                                     \
+    /* wave-uniform addresses: scalar (SMEM) loads, FMAs with SGPR operands */                       \
+    float wv_[KC][9], bv_[KC];                                                                         \
+    _Pragma("unroll") for (int c = 0; c < KC; ++c) {                                                   \
+      bv_[c] = b1[(chunk_) * KC + c];                                                                  \
+      _Pragma("unroll") for (int k = 0; k < 9; ++k) wv_[c][k] = w1[((chunk_) * KC + c) * 9 + k];      \
+    }                                                                                                  \
     _Pragma("unroll") for (int i = 0; i < G::NA; ++i) {                                                \
       const int pix = tid + EX_THREADS * i;                                                            \
-      if (pix < PL) {                                                                                  \
+      if (G::NA * EX_THREADS == PL || pix < PL) {                                                      \
         float v_[KC];                                                                                  \
         _Pragma("unroll") for (int c = 0; c < KC; ++c) {                                               \
           float s_ = 0.0f;                                                                             \
-          _Pragma("unroll") for (int k = 0; k < 9; ++k) s_ = fmaf(w1s_[c * 9 + k], xw[i][k], s_);     \
-          v_[c] = pin[i] ? fmaxf(s_ + b1s_[c], 0.0f) : 0.0f;                                           \
+          _Pragma("unroll") for (int k = 0; k < 9; ++k) s_ = fmaf(wv_[c][k], xw[i][k], s_);           \
+          v_[c] = fmaxf(s_ + bv_[c], 0.0f) * pmask[i];   /* zero outside the clip */                   \
         }                                                                                              \
         *reinterpret_cast<float4*>(As_ + pix * KC) = make_float4(v_[0], v_[1], v_[2], v_[3]);          \
       }                                                                                                \
@@ -250,30 +264,86 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void conv3x3_kernel
 #undef SEDX_EX_CONV1
 #undef SEDX_EX_BAR
 
-  // ---- epilogue: bias + ReLU into LDS, then store / pool / freq-mean, in two
-  // passes over halves of the n-tile (pass h: columns wn*64 + h*32 + j of each
-  // wave; local column c = wn*32 + j), so the staging fits three workgroups
-  // per CU ----
-  constexpr int CPAD = G::CPAD, EC = G::EC;
-  constexpr int NQ = EC / 4;
-  float* Cs = smem;
+  // ---- epilogue.  Lane l holds output channel n = wn*64 + nt*32 + (l&31) of
+  // rows m = (r&3) + 8(r>>2) + 4(l>>5) of each 32-row tile (MFMA C layout).
+  // EPI_POOL2 / EPI_FMEAN: bias + ReLU, then the 2x2 average / the 8-bin mean
+  // in registers (plus one lane-32 swap for the mean) and 128-B row stores;
+  // EPI_STORE: through LDS in two passes (float4 stores). ----
+  if constexpr (EPI == EPI_POOL2) {
+    static_assert(F >= 16, "pooled epilogue: F in {16, 32, 64}");
+    constexpr int FO = F / 2;
+    const int To = T / 2;
 #pragma unroll
-  for (int h = 0; h < NT; ++h) {
-    {
-      const int col = wn * 32 + (lane & 31);
-      const float bv = bias[n0 + wn * 64 + h * 32 + (lane & 31)];
+    for (int nt = 0; nt < NT; ++nt) {
+      const int n = n0 + wn * 64 + nt * 32 + (lane & 31);
+      const float bv = bias[n];
+      auto rl = [&](int mt, int r) { return fmaxf(acc[mt][nt][r] + bv, 0.0f); };
+      if constexpr (F == 16) {
+        // rows m, m+1 (bins), m+16 (next t-row): registers r, r+1, r+8, r+9
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int r = 0; r < 8; r += 2) {
+            const float v = (((rl(mt, r) + rl(mt, r + 1)) + rl(mt, r + 8)) + rl(mt, r + 9)) * 0.25f;
+            const int m = (r & 3) + 8 * (r >> 2) + 4 * khalf;
+            const int to = t0 / 2 + (pix_t(mt, m) >> 1), fo = pix_f(mt, m) >> 1;
+            if (to < To) out[(((int64_t)b * To + to) * FO + fo) * Cout + n] = v;
+          }
+      } else {
+        // rows m, m+1 (bins) in registers r, r+1; t-rows in mt 0, 1
+        static_assert(MT == 2, "pooled epilogue: two MFMA row tiles per wave");
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) {
+          const float v = (((rl(0, r) + rl(0, r + 1)) + rl(1, r)) + rl(1, r + 1)) * 0.25f;
+          const int m = (r & 3) + 8 * (r >> 2) + 4 * khalf;
+          const int to = t0 / 2 + (pix_t(0, m) >> 1), fo = pix_f(0, m) >> 1;
+          if (to < To) out[(((int64_t)b * To + to) * FO + fo) * Cout + n] = v;
+        }
+      }
+    }
+  } else if constexpr (EPI == EPI_FMEAN) {
+    static_assert(F == 8, "freq-mean epilogue: F = 8");
+    // a 32-row tile = 4 t-rows x 8 bins: bins (r&3) + 4 khalf, t-row r>>2;
+    // sum the lane's 4 bins, add the other half-wave's 4 (lane ^ 32)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int n = n0 + wn * 64 + nt * 32 + (lane & 31);
+      const float bv = bias[n];
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int row = wm * WM + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * khalf;
-          Cs[row * CPAD + col] = fmaxf(acc[mt][h][r] + bv, 0.0f);
+        for (int q = 0; q < 4; ++q) {
+          float s4 = 0.0f;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) s4 += fmaxf(acc[mt][nt][4 * q + j] + bv, 0.0f);
+          const float o4 = __shfl_xor(s4, 32);
+          // torch.mean over the 8 bins: ((b0 + b1 + ... + b7) / 8, bins in order)
+          const float v = (khalf ? o4 + s4 : s4 + o4) * (1.0f / F);
+          const int t = t0 + pix_t(mt, 8 * q);
+          if (khalf == (q & 1) && t < T) out[((int64_t)b * T + t) * Cout + n] = v;
         }
     }
-    __syncthreads();
-    // global channel of local float4 group c4 (4 consecutive columns)
-    auto gch = [&](int c4) { return n0 + (c4 / 8) * 64 + h * 32 + (c4 % 8) * 4; };
-    if (EPI == EPI_STORE) {
+  } else {
+    constexpr int CPAD = G::CPAD, EC = G::EC;
+    constexpr int NQ = EC / 4;
+    float* Cs = smem;
+#pragma unroll
+    for (int h = 0; h < NT; ++h) {
+      {
+        const int col = wn * 32 + (lane & 31);
+        const float bv = bias[n0 + wn * 64 + h * 32 + (lane & 31)];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int m = (r & 3) + 8 * (r >> 2) + 4 * khalf;
+            const int row = pix_t(mt, m) * F + pix_f(mt, m);
+            Cs[row * CPAD + col] = fmaxf(acc[mt][h][r] + bv, 0.0f);
+          }
+      }
+      __syncthreads();
+      // global channel of local float4 group c4 (4 consecutive columns)
+      auto gch = [&](int c4) { return n0 + (c4 / 8) * 64 + h * 32 + (c4 % 8) * 4; };
       for (int i = tid; i < BM * NQ; i += EX_THREADS) {
         const int row = i / NQ, c4 = i - row * NQ;
         const int t = t0 + row / F, f = row % F;
@@ -282,46 +352,8 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void conv3x3_kernel
           *reinterpret_cast<float4*>(out + (((int64_t)b * T + t) * F + f) * Cout + gch(c4)) = v;
         }
       }
-    } else if (EPI == EPI_POOL2) {
-      constexpr int FO = F / 2;
-      const int To = T / 2;
-      for (int i = tid; i < (TT / 2) * FO * NQ; i += EX_THREADS) {
-        const int c4 = i % NQ;
-        const int pp = i / NQ;
-        const int tp = pp / FO, fp = pp % FO;
-        const int to = t0 / 2 + tp;
-        if (to < To) {
-          const int r00 = (2 * tp) * F + 2 * fp;
-          const float4 a0 = *reinterpret_cast<const float4*>(Cs + r00 * CPAD + 4 * c4);
-          const float4 a1 = *reinterpret_cast<const float4*>(Cs + (r00 + 1) * CPAD + 4 * c4);
-          const float4 a2 = *reinterpret_cast<const float4*>(Cs + (r00 + F) * CPAD + 4 * c4);
-          const float4 a3 = *reinterpret_cast<const float4*>(Cs + (r00 + F + 1) * CPAD + 4 * c4);
-          float4 v;
-          v.x = (((a0.x + a1.x) + a2.x) + a3.x) * 0.25f;
-          v.y = (((a0.y + a1.y) + a2.y) + a3.y) * 0.25f;
-          v.z = (((a0.z + a1.z) + a2.z) + a3.z) * 0.25f;
-          v.w = (((a0.w + a1.w) + a2.w) + a3.w) * 0.25f;
-          *reinterpret_cast<float4*>(out + (((int64_t)b * To + to) * FO + fp) * Cout + gch(c4)) = v;
-        }
-      }
-    } else {  // EPI_FMEAN
-      for (int i = tid; i < TT * NQ; i += EX_THREADS) {
-        const int tl = i / NQ, c4 = i % NQ;
-        const int t = t0 + tl;
-        if (t < T) {
-          float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-          for (int f = 0; f < F; ++f) {
-            const float4 v = *reinterpret_cast<const float4*>(Cs + (tl * F + f) * CPAD + 4 * c4);
-            s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
-          }
-          const float inv = 1.0f / F;
-          s.x *= inv; s.y *= inv; s.z *= inv; s.w *= inv;
-          *reinterpret_cast<float4*>(out + ((int64_t)b * T + t) * Cout + gch(c4)) = s;
-        }
-      }
+      if (h + 1 < NT) __syncthreads();
     }
-    if (h + 1 < NT) __syncthreads();
   }
 }
 
@@ -332,12 +364,25 @@ static void launch_f_bn_w(const float* in, int B, int T, int Cin, int Cout, cons
   constexpr int TT = ExactGeom<F, BN, FUSE, WAVES>::TT;
   constexpr int NT = 64 * WAVES;
   dim3 grid(B * ((T + TT - 1) / TT), Cout / BN);
-  if (epi == EPI_STORE)
-    launch_kernel(conv3x3_kernel<F, BN, EPI_STORE, FUSE, WAVES>, grid, NT, s, in, T, Cin, Cout, wp, bias, out, w1, b1, zero16);
-  else if (epi == EPI_POOL2)
-    launch_kernel(conv3x3_kernel<F, BN, EPI_POOL2, FUSE, WAVES>, grid, NT, s, in, T, Cin, Cout, wp, bias, out, w1, b1, zero16);
-  else
-    launch_kernel(conv3x3_kernel<F, BN, EPI_FMEAN, FUSE, WAVES>, grid, NT, s, in, T, Cin, Cout, wp, bias, out, w1, b1, zero16);
+  // only the model's (F, epilogue) pairs are instantiated
+  if constexpr (F != 64 && F != 8) {
+    if (epi == EPI_STORE)
+      return launch_kernel(conv3x3_kernel<F, BN, EPI_STORE, FUSE, WAVES>, grid, NT, s, in, T, Cin, Cout, wp, bias,
+                           out, w1, b1, zero16);
+  }
+  if constexpr (F == 8) {
+    if (epi == EPI_STORE)
+      return launch_kernel(conv3x3_kernel<F, BN, EPI_STORE, FUSE, WAVES>, grid, NT, s, in, T, Cin, Cout, wp, bias,
+                           out, w1, b1, zero16);
+    if (epi == EPI_FMEAN)
+      return launch_kernel(conv3x3_kernel<F, BN, EPI_FMEAN, FUSE, WAVES>, grid, NT, s, in, T, Cin, Cout, wp, bias,
+                           out, w1, b1, zero16);
+  } else {
+    if (epi == EPI_POOL2)
+      return launch_kernel(conv3x3_kernel<F, BN, EPI_POOL2, FUSE, WAVES>, grid, NT, s, in, T, Cin, Cout, wp, bias,
+                           out, w1, b1, zero16);
+  }
+  note_launch_error(hipErrorInvalidValue);
 }
 
 // 8-wave tiles when they make at least two workgroups per CU of the chip,

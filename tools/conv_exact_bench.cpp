@@ -61,7 +61,7 @@ int main(int argc, char** argv) {
     if (l.F == 64) fl += 2.0 * B * l.T * 64 * 64 * 9;   // fused conv1
     tot_ms += ms; tot_f += fl;
     printf("%s  T=%4d F=%2d %3d->%3d  %.4f ms  %.1f TF/s  (%.3f of 157.3)\n", l.name, l.T, l.F, l.cin, l.cout, ms,
-           fl / ms / 1e9, fl / ms / 1e9 / 157.3e3);
+           fl / ms / 1e9, fl / ms / 1e9 / 157.3);
   }
   printf("total %.4f ms  %.1f TF/s  (err=%s, launch=%s)\n", tot_ms, tot_f / tot_ms / 1e9,
          hipGetErrorString(hipGetLastError()), hipGetErrorString(sedx::take_launch_error()));

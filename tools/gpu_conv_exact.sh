@@ -4,7 +4,7 @@
 # variant; RUN=1 (GPU box): time each, then one SQ-counter pass of cx_full.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out tools/prev
-HIPCC="/opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -Wno-unused-result -Wno-unused-value -Isound-event-detection_amd/csrc"
+HIPCC="/opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -Wno-unused-result -Wno-unused-value -fno-slp-vectorize -fno-vectorize -Isound-event-detection_amd/csrc"
 C=sound-event-detection_amd/csrc
 O=tools/prev
 if [ -n "$BUILD" ]; then
