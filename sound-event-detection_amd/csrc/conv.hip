@@ -33,12 +33,18 @@ namespace sedx {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-// WAVES (8, or 4 for grids too small to fill the chip) waves per workgroup,
-// each owning a 64 x 64 output tile: WAVES / (BN / 64) along M
-template <int F, int BN, bool FUSE, int WAVES>
+// WAVES waves per workgroup, each owning a WT x WT output tile (WT = 64:
+// 2 x 2 MFMA tiles; WT = 32: one), BN / WT of them along N and the rest
+// along M.  WT = 64 with 8 waves (4 for grids too small to fill the chip) is
+// the throughput shape; WT = 32 is the small-batch shape: a quarter of the
+// MFMAs per wave per k-step, so a quarter of the serial K chain and four
+// times the waves, with every output's MFMA sequence (chunk, tap, k-step)
+// unchanged, so the results are bit-identical to the WT = 64 kernel.
+template <int F, int BN, bool FUSE, int WAVES, int WT>
 struct ExactGeom {
   static constexpr int THREADS = 64 * WAVES;
-  static constexpr int BM = 64 * (WAVES / (BN / 64)), TT = BM / F, RT = TT + 2, CS = F + 2, KC = 4;
+  static constexpr int WAVES_N = BN / WT, WAVES_M = WAVES / WAVES_N;
+  static constexpr int BM = WT * WAVES_M, TT = BM / F, RT = TT + 2, CS = F + 2, KC = 4;
   static constexpr int PL = RT * CS;                 // halo pixels
   static constexpr int PLP = (PL + 63) / 64 * 64;    // padded to whole 64-pixel DMA units
   static constexpr int A_SZ = KC * PLP;              // floats: [pixel][channel]
@@ -46,7 +52,7 @@ struct ExactGeom {
   static constexpr int BUF = A_SZ + W_SZ;            // one chunk's staging buffer
   static constexpr int NBUF = 3;                     // ring: DMA two chunks ahead
   static constexpr int MAIN = NBUF * BUF;
-  static constexpr int EC = BN / 2;                  // epilogue pass: half of the n-tile
+  static constexpr int EC = BN / (WT / 32);          // epilogue pass: one 32-column MFMA tile per wave
   static constexpr int CPAD = EC + 4;
   static constexpr int LDS_EPI = BM * CPAD;
   static constexpr int LDS_FLOATS = MAIN > LDS_EPI ? MAIN : LDS_EPI;
@@ -59,21 +65,24 @@ struct ExactGeom {
   static constexpr int NA = (PL + THREADS - 1) / THREADS;   // FUSE: halo pixels per thread
 };
 
-template <int F, int BN, int EPI, bool FUSE, int WAVES>
-__global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void conv3x3_kernel(const float* __restrict__ in, int T, int Cin,
+template <int F, int BN, int EPI, bool FUSE, int WAVES, int WT>
+__global__ __launch_bounds__(64 * WAVES, WAVES == 8 && WT == 64 ? 2 : 1) void conv3x3_kernel(const float* __restrict__ in, int T, int Cin,
                                                                 int Cout, const float* __restrict__ wp,
                                                                 const float* __restrict__ bias,
                                                                 float* __restrict__ out,
                                                                 const float* __restrict__ w1,
                                                                 const float* __restrict__ b1,
                                                                 const float* __restrict__ zero16) {
-  using G = ExactGeom<F, BN, FUSE, WAVES>;
+  using G = ExactGeom<F, BN, FUSE, WAVES, WT>;
   constexpr int EX_THREADS = G::THREADS;
   constexpr int BM = G::BM, TT = G::TT, CS = G::CS, KC = G::KC, PL = G::PL;
-  constexpr int WAVES_N = BN / 64;
-  constexpr int WAVES_M = WAVES / WAVES_N;
-  constexpr int WM = BM / WAVES_M;
-  constexpr int MT = WM / 32, NT = 2;   // 32x32 MFMA tiles per wave
+  constexpr int WAVES_N = G::WAVES_N;
+  constexpr int WM = WT;
+  constexpr int MT = WT / 32, NT = WT / 32;   // 32x32 MFMA tiles per wave
+  // WT = 32 pooled: a wave's 32 rows are 2 t-rows x 16 bins, so a 2x2
+  // window is registers r, r+1, r+8, r+9 of one lane (as at F = 16)
+  constexpr bool SEG16 = WT == 32 && EPI == EPI_POOL2;
+  static_assert(TT * F == BM && (EPI != EPI_POOL2 || TT % 2 == 0), "tile = whole (pairs of) t-rows");
 
   // ALL LDS in one array (a second __shared__ object can make hipcc drain
   // vmcnt before the fragment reads)
@@ -92,14 +101,17 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void conv3x3_kernel
   // fragment offsets (floats): A pixel p -> [p][khalf], [p][2 + khalf] =
   // (ks 0, ks 1); B [tap][khalf][n][ks]
   // A row m of MFMA tile mt of wave wm is tile pixel (t, f) = pix_t / pix_f:
-  // row-major (pixel 64 wm + 32 mt + m) except at F = 64, where a wave
-  // covers two t-rows x 32 bins, so every 2x2 pooling window lies in one
-  // lane's accumulators (bins m, m+1 in registers r, r+1; rows in mt 0, 1)
+  // row-major (pixel WT wm + 32 mt + m) except at WT = 64, F = 64, where a
+  // wave covers two t-rows x 32 bins, so every 2x2 pooling window lies in one
+  // lane's accumulators (bins m, m+1 in registers r, r+1; rows in mt 0, 1),
+  // and SEG16 (above)
   auto pix_t = [&](int mt, int m) {
-    return F == 64 ? 2 * (wm >> 1) + mt : (wm * WM + mt * 32 + m) / F;
+    if constexpr (SEG16) return 2 * (wm / (F / 16)) + (m >> 4);
+    return (F == 64 && WT == 64) ? 2 * (wm >> 1) + mt : (wm * WM + mt * 32 + m) / F;
   };
   auto pix_f = [&](int mt, int m) {
-    return F == 64 ? 32 * (wm & 1) + m : (wm * WM + mt * 32 + m) % F;
+    if constexpr (SEG16) return 16 * (wm % (F / 16)) + (m & 15);
+    return (F == 64 && WT == 64) ? 32 * (wm & 1) + m : (wm * WM + mt * 32 + m) % F;
   };
   int a_off[MT];
 #pragma unroll
@@ -107,7 +119,7 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void conv3x3_kernel
     a_off[mt] = (pix_t(mt, lane & 31) * CS + pix_f(mt, lane & 31)) * KC + khalf;
   int b_off[NT];
 #pragma unroll
-  for (int nt = 0; nt < NT; ++nt) b_off[nt] = (khalf * BN + wn * 64 + nt * 32 + (lane & 31)) * 2;
+  for (int nt = 0; nt < NT; ++nt) b_off[nt] = (khalf * BN + wn * WT + nt * 32 + (lane & 31)) * 2;
 
   f32x16 acc[MT][NT];
 #pragma unroll
@@ -275,10 +287,10 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void conv3x3_kernel
     const int To = T / 2;
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
-      const int n = n0 + wn * 64 + nt * 32 + (lane & 31);
+      const int n = n0 + wn * WT + nt * 32 + (lane & 31);
       const float bv = bias[n];
       auto rl = [&](int mt, int r) { return fmaxf(acc[mt][nt][r] + bv, 0.0f); };
-      if constexpr (F == 16) {
+      if constexpr (F == 16 || SEG16) {
         // rows m, m+1 (bins), m+16 (next t-row): registers r, r+1, r+8, r+9
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt)
@@ -307,7 +319,7 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void conv3x3_kernel
     // sum the lane's 4 bins, add the other half-wave's 4 (lane ^ 32)
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
-      const int n = n0 + wn * 64 + nt * 32 + (lane & 31);
+      const int n = n0 + wn * WT + nt * 32 + (lane & 31);
       const float bv = bias[n];
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
@@ -331,7 +343,7 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void conv3x3_kernel
     for (int h = 0; h < NT; ++h) {
       {
         const int col = wn * 32 + (lane & 31);
-        const float bv = bias[n0 + wn * 64 + h * 32 + (lane & 31)];
+        const float bv = bias[n0 + wn * WT + h * 32 + (lane & 31)];
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -343,7 +355,7 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void conv3x3_kernel
       }
       __syncthreads();
       // global channel of local float4 group c4 (4 consecutive columns)
-      auto gch = [&](int c4) { return n0 + (c4 / 8) * 64 + h * 32 + (c4 % 8) * 4; };
+      auto gch = [&](int c4) { return n0 + (c4 / 8) * WT + h * 32 + (c4 % 8) * 4; };
       for (int i = tid; i < BM * NQ; i += EX_THREADS) {
         const int row = i / NQ, c4 = i - row * NQ;
         const int t = t0 + row / F, f = row % F;
@@ -357,48 +369,56 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 1) void conv3x3_kernel
   }
 }
 
-template <int F, int BN, bool FUSE, int WAVES>
+template <int F, int BN, bool FUSE, int WAVES, int WT>
 static void launch_f_bn_w(const float* in, int B, int T, int Cin, int Cout, const float* wp,
                           const float* bias, float* out, int epi, const float* w1, const float* b1,
                           const float* zero16, hipStream_t s) {
-  constexpr int TT = ExactGeom<F, BN, FUSE, WAVES>::TT;
+  constexpr int TT = ExactGeom<F, BN, FUSE, WAVES, WT>::TT;
   constexpr int NT = 64 * WAVES;
   dim3 grid(B * ((T + TT - 1) / TT), Cout / BN);
+#define SEDX_EX_LAUNCH(E)                                                                              \
+  return launch_kernel(conv3x3_kernel<F, BN, E, FUSE, WAVES, WT>, grid, NT, s, in, T, Cin, Cout, wp, bias, out, \
+                       w1, b1, zero16)
   // only the model's (F, epilogue) pairs are instantiated
   if constexpr (F != 64 && F != 8) {
-    if (epi == EPI_STORE)
-      return launch_kernel(conv3x3_kernel<F, BN, EPI_STORE, FUSE, WAVES>, grid, NT, s, in, T, Cin, Cout, wp, bias,
-                           out, w1, b1, zero16);
+    if (epi == EPI_STORE) SEDX_EX_LAUNCH(EPI_STORE);
   }
   if constexpr (F == 8) {
-    if (epi == EPI_STORE)
-      return launch_kernel(conv3x3_kernel<F, BN, EPI_STORE, FUSE, WAVES>, grid, NT, s, in, T, Cin, Cout, wp, bias,
-                           out, w1, b1, zero16);
-    if (epi == EPI_FMEAN)
-      return launch_kernel(conv3x3_kernel<F, BN, EPI_FMEAN, FUSE, WAVES>, grid, NT, s, in, T, Cin, Cout, wp, bias,
-                           out, w1, b1, zero16);
+    if (epi == EPI_STORE) SEDX_EX_LAUNCH(EPI_STORE);
+    if (epi == EPI_FMEAN) SEDX_EX_LAUNCH(EPI_FMEAN);
   } else {
-    if (epi == EPI_POOL2)
-      return launch_kernel(conv3x3_kernel<F, BN, EPI_POOL2, FUSE, WAVES>, grid, NT, s, in, T, Cin, Cout, wp, bias,
-                           out, w1, b1, zero16);
+    if (epi == EPI_POOL2) SEDX_EX_LAUNCH(EPI_POOL2);
   }
+#undef SEDX_EX_LAUNCH
   note_launch_error(hipErrorInvalidValue);
 }
 
-// 8-wave tiles when they make at least two workgroups per CU of the chip,
-// else 4-wave tiles (half the pixels per tile: twice the workgroups)
+static int device_cus() {
+  int dev = 0, ncu = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  return ncu;
+}
+
+// Shape by grid size: 8-wave 64x64 wave tiles when they make at least two
+// workgroups per CU of the chip; 4-wave ones while those still give every CU
+// a workgroup; below that (small batches) 32x32 wave tiles over whole pairs
+// of t-rows (4 t-rows at F = 8), BN = 64: 8 waves at F = 64, 4 at F = 32,
+// 2 at F = 16 / 8.  All three give bit-identical outputs.
 template <int F, int BN, bool FUSE>
 static void launch_f_bn(const float* in, int B, int T, int Cin, int Cout, const float* wp,
                         const float* bias, float* out, int epi, const float* w1, const float* b1,
                         const float* zero16, hipStream_t s) {
-  constexpr int TT8 = ExactGeom<F, BN, FUSE, 8>::TT;
+  const int64_t ncu = device_cus();
+  constexpr int TT8 = ExactGeom<F, BN, FUSE, 8, 64>::TT, TT4 = ExactGeom<F, BN, FUSE, 4, 64>::TT;
   const int64_t tiles8 = (int64_t)B * ((T + TT8 - 1) / TT8) * (Cout / BN);
-  int dev = 0, ncu = 256;
-  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-  if (tiles8 >= 2 * (int64_t)ncu)
-    launch_f_bn_w<F, BN, FUSE, 8>(in, B, T, Cin, Cout, wp, bias, out, epi, w1, b1, zero16, s);
+  const int64_t tiles4 = (int64_t)B * ((T + TT4 - 1) / TT4) * (Cout / BN);
+  constexpr int SW = (F == 8 ? 32 : 2 * F) / 32 * 2;   // small shape: (BM / 32) x (64 / 32) waves
+  if (tiles8 >= 2 * ncu)
+    launch_f_bn_w<F, BN, FUSE, 8, 64>(in, B, T, Cin, Cout, wp, bias, out, epi, w1, b1, zero16, s);
+  else if (tiles4 >= ncu)
+    launch_f_bn_w<F, BN, FUSE, 4, 64>(in, B, T, Cin, Cout, wp, bias, out, epi, w1, b1, zero16, s);
   else
-    launch_f_bn_w<F, BN, FUSE, 4>(in, B, T, Cin, Cout, wp, bias, out, epi, w1, b1, zero16, s);
+    launch_f_bn_w<F, 64, FUSE, SW, 32>(in, B, T, Cin, Cout, wp, bias, out, epi, w1, b1, zero16, s);
 }
 
 void launch_conv3x3(const float* in, int B, int T, int F, int Cin, int Cout, const float* wp,

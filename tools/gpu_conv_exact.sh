@@ -19,7 +19,7 @@ fi
 export TMPDIR=/tmp
 for v in ${VARIANTS:-full}; do
   echo "== $v" | tee -a gpurun_out/conv_exact.log
-  timeout -k 10 120 $O/cx_$v 32 20 | tee -a gpurun_out/conv_exact.log || exit $?
+  for bb in ${BATCHES:-32}; do timeout -k 10 120 $O/cx_$v $bb 20 || exit $?; done | tee -a gpurun_out/conv_exact.log || exit $?
 done
 if [ -n "$PMC" ]; then
   timeout -k 10 180 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_INSTS_MFMA GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/cx_pmc -o p -- $O/cx_full 32 5 > gpurun_out/cx_pmc.log 2>&1 || exit $?
