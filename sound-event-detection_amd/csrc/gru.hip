@@ -67,7 +67,10 @@ __device__ __forceinline__ unsigned g_ld(const unsigned* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // sc1
 }
 
-constexpr int GRU_MAX_SLOTS = 4;      // 2 * slots (slot, dir) pairs on 8 XCD residues
+constexpr int GRU_MAX_SLOTS = 4;
+constexpr int GRU_VALU_CLIPS = 8;     // exact launches this small run the VALU product
+constexpr int GRU_HV_LD = 260;        // Hv row stride (floats): 8 rows fit the A-image space
+static_assert(GRU_VALU_CLIPS * GRU_HV_LD <= 16 * 32 * 4 * 4, "Hv inside Aimg");      // 2 * slots (slot, dir) pairs on 8 XCD residues
 constexpr unsigned GRU_SPIN = 1u << 24;
 
 struct GruSync {                      // zeroed every launch
@@ -91,7 +94,7 @@ struct GruSync {                      // zeroed every launch
 #define GRU_STAMP(i)
 #endif
 
-template <bool EXACT>
+template <bool EXACT, bool VALU>
 __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__ G, int B, int T,
                                                        const float* __restrict__ whh,
                                                        const float* __restrict__ bhh,
@@ -142,10 +145,15 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
 
   // W_hh slice -> B fragments: B[k][n] = W_hh[gate row n][k]
   bf16x8_g Bhi[4], Blo[4];
-  float Bf[EXACT ? 32 : 1];
+  static_assert(EXACT || !VALU, "the VALU product is the exact arithmetic");
+  float Bf[EXACT && !VALU ? 32 : 1];
+  float4 Wv[VALU ? 16 : 1];   // VALU: the lane's gate row over its whole K quarter
   {
     const float* wrow = whh + ((int64_t)dir * 768 + nt * 256 + 32 * p + (lane & 31)) * 256;
-    if constexpr (EXACT) {
+    if constexpr (VALU) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) Wv[q] = reinterpret_cast<const float4*>(wrow + 64 * kq)[q];
+    } else if constexpr (EXACT) {
 #pragma unroll
       for (int st = 0; st < 32; ++st) Bf[st] = wrow[64 * kq + 2 * st + h];
     } else {
@@ -174,6 +182,13 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
   for (int g = slot; g < ngroups; g += nslots, ++j) {
     const int c0 = g * 32;
     const int nc = min(32, B - c0);
+    // VALU (exact, launches of at most GRU_VALU_CLIPS clips): the recurrent
+    // product as VALU fma chains instead of MFMAs padded to 32 clips.
+    // v_mfma_f32_32x32x2_f32 is bit for bit acc = fma(a1, b1, fma(a0, b0,
+    // acc)) (measured over 16.7 M random elements incl. cancellation,
+    // tools/mfma_f32_semantics.cpp), so the chain over k ascending gives the
+    // MFMA kernel's bits: results do not depend on the batch size.  h_{s-1}
+    // then lives as Hv[clip][k] (row stride GRU_HV_LD) in the A-image space.
     for (int s = 0; s < T; ++s) {
       const int gs = j * T + s;                // step of this pair; flags/counts are gs-based
       const int t = dir ? T - 1 - s : s;
@@ -252,7 +267,13 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
           if (it >= 32 * 32) break;
           const int c = it >> 5, oct = it & 31;
           const float* v = vv[k2];
-          if constexpr (EXACT) {
+          if constexpr (VALU) {
+            float4* hv = reinterpret_cast<float4*>(Af + c * GRU_HV_LD + 8 * oct);
+            if (c < nc) {
+              hv[0] = make_float4(v[0], v[1], v[2], v[3]);
+              hv[1] = make_float4(v[4], v[5], v[6], v[7]);
+            }
+          } else if constexpr (EXACT) {
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
               const int k = 8 * oct + e;
@@ -276,7 +297,22 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
       f32x16_g acc;
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-      if constexpr (EXACT) {
+      if constexpr (VALU) {
+        // lane: gate row u = lane & 31 of gate nt, clips h, h + 2, ...
+        for (int c = h; c < nc; c += 2) {
+          const float4* hv = reinterpret_cast<const float4*>(Af + c * GRU_HV_LD + 64 * kq);
+          float a = 0.f;
+#pragma unroll
+          for (int q = 0; q < 16; ++q) {
+            const float4 x = hv[q], w = Wv[q];
+            a = fmaf(x.x, w.x, a);
+            a = fmaf(x.y, w.y, a);
+            a = fmaf(x.z, w.z, a);
+            a = fmaf(x.w, w.w, a);
+          }
+          part[kq][nt][c][lane & 31] = a;
+        }
+      } else if constexpr (EXACT) {
         const int c = lane & 31;
 #pragma unroll
         for (int st = 0; st < 32; ++st) {
@@ -296,9 +332,11 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
           acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(alo, Bhi[ks], acc, 0, 0, 0);
         }
       }
+      if constexpr (!VALU) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r)
-        part[kq][nt][(r & 3) + 8 * (r >> 2) + 4 * h][lane & 31] = acc[r];
+        for (int r = 0; r < 16; ++r)
+          part[kq][nt][(r & 3) + 8 * (r >> 2) + 4 * h][lane & 31] = acc[r];
+      }
       __syncthreads();
       GRU_STAMP(2);
       float* dst = Xs + (gs & 1) * 32 * 256;
@@ -365,13 +403,17 @@ void launch_gru_coop(const float* G, int B, int T, const float* whh, const float
   const int nslots = ngroups < GRU_MAX_SLOTS ? ngroups : GRU_MAX_SLOTS;
   GruSync* sync = static_cast<GruSync*>(ws);
   float* X = reinterpret_cast<float*>(static_cast<char*>(ws) + ((sizeof(GruSync) + 255) & ~size_t(255)));
-  (void)hipMemsetAsync(sync, 0, sizeof(GruSync), s);
-  if (exact)
-    launch_kernel(gru_coop_kernel<true>, dim3(64), 768, s, G, B, T, whh, bhh, H, X, sync, nslots,
-                allow_fast ? 1 : 0);
+  // one fill launch: the size rounded to 256 B (the exchange buffers start there)
+  (void)hipMemsetAsync(sync, 0, (sizeof(GruSync) + 255) & ~size_t(255), s);
+  if (exact && B <= GRU_VALU_CLIPS)
+    launch_kernel(gru_coop_kernel<true, true>, dim3(64), 768, s, G, B, T, whh, bhh, H, X, sync, nslots,
+                  allow_fast ? 1 : 0);
+  else if (exact)
+    launch_kernel(gru_coop_kernel<true, false>, dim3(64), 768, s, G, B, T, whh, bhh, H, X, sync, nslots,
+                  allow_fast ? 1 : 0);
   else
-    launch_kernel(gru_coop_kernel<false>, dim3(64), 768, s, G, B, T, whh, bhh, H, X, sync, nslots,
-                allow_fast ? 1 : 0);
+    launch_kernel(gru_coop_kernel<false, false>, dim3(64), 768, s, G, B, T, whh, bhh, H, X, sync, nslots,
+                  allow_fast ? 1 : 0);
 }
 
 }  // namespace sedx

@@ -75,9 +75,77 @@ __global__ __launch_bounds__(256) void linear_kernel(const float* __restrict__ A
   }
 }
 
+// Small-M shape (single clips, the head's 64 columns): one wave per 32 x 32
+// output tile, A / W fragments straight from global (L2) as float4 rows, 32 k
+// in flight per wave, no LDS and no barriers.  Every output's MFMA sequence
+// (k ascending in pairs, zero start, + bias, act) is linear_kernel's, so the
+// two shapes give identical bits.
+template <int ACT>
+__global__ __launch_bounds__(64) void linear_small_kernel(const float* __restrict__ A, int M, int K,
+                                                          const float* __restrict__ W, int N,
+                                                          const float* __restrict__ bias,
+                                                          float* __restrict__ C) {
+  const int lane = threadIdx.x, i = lane & 31, kh = lane >> 5;
+  const int m0 = blockIdx.x * 32, n0 = blockIdx.y * 32;
+  const float4* ap = reinterpret_cast<const float4*>(A + (int64_t)min(m0 + i, M - 1) * K);
+  const float4* wq = reinterpret_cast<const float4*>(W + (int64_t)(n0 + i) * K);
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+  constexpr int Q = 16;  // float4 per row per round (64 k); two rounds in registers
+  float4 xa0[Q], xw0[Q], xa1[Q], xw1[Q];
+  const int nr = K / (4 * Q);
+  auto load = [&](float4* xa, float4* xw, int rd) {
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      xa[q] = ap[rd * Q + q];
+      xw[q] = wq[rd * Q + q];
+    }
+  };
+  // k-step 2q: k = 4q + kh (element kh); k-step 2q + 1: k = 4q + 2 + kh
+  auto mma = [&](const float4* xa, const float4* xw) {
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const float4 a = xa[q], b = xw[q];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(kh ? a.y : a.x, kh ? b.y : b.x, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(kh ? a.w : a.z, kh ? b.w : b.z, acc, 0, 0, 0);
+    }
+  };
+  load(xa0, xw0, 0);
+  for (int rd = 0; rd < nr; rd += 2) {   // static buffer names: no dynamic register indexing
+    if (rd + 1 < nr) load(xa1, xw1, rd + 1);
+    mma(xa0, xw0);
+    if (rd + 1 < nr) {
+      if (rd + 2 < nr) load(xa0, xw0, rd + 2);
+      mma(xa1, xw1);
+    }
+  }
+  const int n = n0 + i;
+  const float bv = bias ? bias[n] : 0.0f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int m = m0 + (r & 3) + 8 * (r >> 2) + 4 * kh;
+    if (m < M) {
+      float v = acc[r] + bv;
+      if (ACT == 1) v = fmaxf(v, 0.0f);
+      C[(int64_t)m * N + n] = v;
+    }
+  }
+}
+
 void launch_linear(const float* A, int M, int K, const float* W, int N, const float* bias,
                    float* C, int act, hipStream_t s) {
   dim3 grid((M + 127) / 128, N / 64);
+  int dev = 0, ncu = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  if ((int64_t)grid.x * grid.y < ncu && K % 64 == 0 && N % 32 == 0) {
+    dim3 g2((M + 31) / 32, N / 32);
+    if (act == 1)
+      launch_kernel(linear_small_kernel<1>, g2, 64, s, A, M, K, W, N, bias, C);
+    else
+      launch_kernel(linear_small_kernel<0>, g2, 64, s, A, M, K, W, N, bias, C);
+    return;
+  }
   if (act == 1)
     launch_kernel(linear_kernel<1>, grid, 256, s, A, M, K, W, N, bias, C);
   else
@@ -219,13 +287,17 @@ __device__ __forceinline__ float sum8_(float v) {      // over the 8 lanes of a 
   return v;
 }
 
+// One workgroup per clip; the clip's att / cla logits are staged into LDS
+// 128 frames at a time by independent coalesced loads (a 10 s clip's 125
+// frames once, for both passes) instead of per-lane dependent global loads.
 __global__ __launch_bounds__(256) void att_head_kernel(const float* __restrict__ logits, int T,
                                                        int C, int ldl, int out_frames,
                                                        float* __restrict__ fw,
                                                        float* __restrict__ clip,
                                                        float* __restrict__ emb) {
   constexpr int TC = 128;
-  __shared__ float s_cla[TC][33];
+  __shared__ float s_att[TC][33];
+  __shared__ float s_cla[TC][33];             // cla logits, then sigmoid(cla)
   __shared__ float s_last[32];
   const int b = blockIdx.x, tid = threadIdx.x;
   const int cs = tid >> 3, l = tid & 7;
@@ -234,22 +306,38 @@ __global__ __launch_bounds__(256) void att_head_kernel(const float* __restrict__
     const int nc = min(32, C - c0);
     const bool act = cs < nc;
     const int c = c0 + cs;
-    // pass 1: sum over t of exp(clamp(att)) + 1e-6
+    auto stage = [&](int t0, int nt) {
+      __syncthreads();
+      for (int i = tid; i < nt * 2 * nc; i += 256) {
+        const int t = i / (2 * nc), j = i - t * 2 * nc;
+        const int half = j >= nc, cc = j - half * nc;
+        const float v = lg[(int64_t)(t0 + t) * ldl + half * C + c0 + cc];
+        if (half)
+          s_cla[t][cc] = v;
+        else
+          s_att[t][cc] = v;
+      }
+      __syncthreads();
+    };
+    // pass 1: sum over t of exp(clamp(att)) + 1e-6 (lane l: t = l, l + 8, ...)
     float sum = 0.f;
-    if (act)
-      for (int t = l; t < T; t += 8) sum += att_exp_(lg[(int64_t)t * ldl + c]);
+    for (int t0 = 0; t0 < T; t0 += TC) {
+      const int nt = min(TC, T - t0);
+      stage(t0, nt);
+      if (act)
+        for (int t = l; t < nt; t += 8) sum += att_exp_(s_att[t][cs]);
+    }
     sum = sum8_(sum);
     const float inv_tot = 1.0f / sum;
-    // pass 2: clipwise = sum_t norm_att * sigmoid(cla); cla -> LDS -> outputs
+    // pass 2: clipwise = sum_t norm_att * sigmoid(cla); sigmoid(cla) -> outputs
     float acc = 0.f;
     for (int t0 = 0; t0 < T; t0 += TC) {
       const int nt = min(TC, T - t0);
-      __syncthreads();
+      if (T > TC) stage(t0, nt);             // else still staged from pass 1
       if (act)
         for (int t = l; t < nt; t += 8) {
-          const int64_t o = (int64_t)(t0 + t) * ldl + c;
-          const float cl = 1.0f / (1.0f + expf(-lg[o + C]));
-          acc += (att_exp_(lg[o]) * inv_tot) * cl;
+          const float cl = 1.0f / (1.0f + expf(-s_cla[t][cs]));
+          acc += (att_exp_(s_att[t][cs]) * inv_tot) * cl;
           s_cla[t][cs] = cl;
         }
       __syncthreads();

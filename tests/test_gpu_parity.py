@@ -211,6 +211,25 @@ def test_gru_exact_recurrence_is_fp32():
         assert e_cs <= 2e-6 and e_ref <= 1e-5
 
 
+@pytest.mark.parametrize('prec', ['exact', 'x3'])
+def test_small_batch_shapes_bit_identical(prec):
+    """Small batches run other kernel shapes — 32x32-wave-tile convs, the
+    barrier-free small-M linear, and (exact) the VALU fma-chain GRU product for
+    groups of <= 8 clips instead of 32-clip MFMAs.  Each keeps every output's
+    operation sequence, so a clip's outputs are bit-identical whether it runs
+    alone or inside a full 32-clip group (40 clips: a full MFMA group + a
+    ragged 8-clip group)."""
+    m = build(GRU).set_precision(prec)
+    wave = synth.make_waveforms(40, seconds=10.0, sample_rate=16000, seed=31)
+    full = run(m, wave)
+    for i in (0, 17, 39):
+        one = run(m, wave[i:i + 1])
+        for k in ('framewise_output', 'clipwise_output', 'embedding'):
+            assert np.array_equal(one[k][0], full[k][i]), (prec, i, k, err(one[k][0], full[k][i]))
+    four = run(m, wave[8:12])
+    assert np.array_equal(four['framewise_output'], full['framewise_output'][8:12])
+
+
 def test_windowed_and_events(model, golden_dir):
     from sedx import inference
     mt, m = model

@@ -37,23 +37,24 @@ int main(int argc, char** argv) {
   hipMemcpy(Bb, hb.data(), hb.size() * 4, hipMemcpyHostToDevice);
   hipEvent_t e0, e1;
   hipEventCreate(&e0); hipEventCreate(&e1);
-  for (int mode = 0; mode < 2; ++mode) {
-    if (mode == 0) setenv("SEDX_GRU_GLOBAL_ONLY", "1", 1); else unsetenv("SEDX_GRU_GLOBAL_ONLY");
-    sedx::launch_gru_coop(G, B, T, W, Bb, H, ws, 0);
-    hipDeviceSynchronize();
-    hipEventRecord(e0, 0);
-    for (int r = 0; r < reps; ++r) sedx::launch_gru_coop(G, B, T, W, Bb, H, ws, 0);
-    hipEventRecord(e1, 0);
-    hipEventSynchronize(e1);
-    float ms = 0;
-    hipEventElapsedTime(&ms, e0, e1);
-    Sync sy;
-    hipMemcpy(&sy, ws, sizeof(Sync), hipMemcpyDeviceToHost);
-    const double tot = (double)(sy.stamps[0] + sy.stamps[1] + sy.stamps[2] + sy.stamps[3]);
-    printf("%s: mode=%u err=%u  %.3f ms/launch  %.2f us/step | wait %.0f%% gather %.0f%% mfma %.0f%% gates+publish %.0f%% (s_memtime ticks/step %.0f)\n",
-           mode ? "auto" : "global", sy.mode, sy.err, ms / reps, ms / reps * 1e3 / T,
-           100 * sy.stamps[0] / tot, 100 * sy.stamps[1] / tot, 100 * sy.stamps[2] / tot,
-           100 * sy.stamps[3] / tot, tot / T);
-  }
+  for (int exact = 1; exact >= 0; --exact)
+    for (int fast = 0; fast < 2; ++fast) {
+      sedx::launch_gru_coop(G, B, T, W, Bb, H, ws, exact, fast, 0);
+      hipDeviceSynchronize();
+      hipEventRecord(e0, 0);
+      for (int r = 0; r < reps; ++r) sedx::launch_gru_coop(G, B, T, W, Bb, H, ws, exact, fast, 0);
+      hipEventRecord(e1, 0);
+      hipEventSynchronize(e1);
+      float ms = 0;
+      hipEventElapsedTime(&ms, e0, e1);
+      Sync sy;
+      hipMemcpy(&sy, ws, sizeof(Sync), hipMemcpyDeviceToHost);
+      const double tot = (double)(sy.stamps[0] + sy.stamps[1] + sy.stamps[2] + sy.stamps[3]);
+      printf("B=%d %s %s: mode=%u err=%u  %.3f ms/launch  %.2f us/step | wait %.0f%% gather %.0f%% product %.0f%% "
+             "gates+publish %.0f%% (s_memtime ticks/step %.0f)\n",
+             B, exact ? "exact" : "x3", fast ? "auto" : "global", sy.mode, sy.err, ms / reps, ms / reps * 1e3 / T,
+             100 * sy.stamps[0] / tot, 100 * sy.stamps[1] / tot, 100 * sy.stamps[2] / tot, 100 * sy.stamps[3] / tot,
+             tot / T);
+    }
   return 0;
 }
