@@ -50,7 +50,9 @@ struct ExactGeom {
   static constexpr int A_SZ = KC * PLP;              // floats: [pixel][channel]
   static constexpr int W_SZ = 9 * KC * BN;           // floats: [tap][khalf][n][ks]
   static constexpr int BUF = A_SZ + W_SZ;            // one chunk's staging buffer
-  static constexpr int NBUF = 3;                     // ring: DMA two chunks ahead
+  // ring: DMA NBUF - 1 chunks ahead (deeper for the small-batch shape, whose
+  // one or two waves per SIMD cannot hide a DMA behind other waves' MFMAs)
+  static constexpr int NBUF = WT == 32 ? 5 : 3;
   static constexpr int MAIN = NBUF * BUF;
   static constexpr int EC = BN / (WT / 32);          // epilogue pass: one 32-column MFMA tile per wave
   static constexpr int CPAD = EC + 4;
@@ -224,18 +226,27 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 && WT == 64 ? 2 : 1) void co
 #define SEDX_EX_BAR(n_) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(n_) : "memory")
 
   const int nchunks = Cin / KC;
-  SEDX_EX_DMA(0, 0);
-  if (nchunks > 1) SEDX_EX_DMA(1, 1);
+  constexpr int NB = G::NBUF;
+#pragma unroll
+  for (int c = 0; c < NB - 1; ++c)
+    if (c < nchunks) SEDX_EX_DMA(c, c);
   if constexpr (FUSE) SEDX_EX_CONV1(0, 0);
+  int buf = 0;
   for (int chunk = 0; chunk < nchunks; ++chunk) {
-    // chunk's DMAs (issued two chunks ago) landed for every wave; buffer
-    // (chunk + 2) % 3 was last read in chunk - 1, finished by every wave
-    if (chunk + 1 < nchunks)
+    // chunk's DMAs (issued NB - 1 chunks ago) landed for every wave: at most
+    // the younger chunks' DMAs (up to NB - 2 of them) still in flight; buffer
+    // (chunk + NB - 1) % NB was last read in chunk - 1, finished by every wave
+    const int younger = min(NB - 2, nchunks - 1 - chunk);
+    if (younger >= 3 && NB > 4)
+      SEDX_EX_BAR(3 * G::VM_MIN);
+    else if (younger == 2 && NB > 3)
+      SEDX_EX_BAR(2 * G::VM_MIN);
+    else if (younger >= 1)
       SEDX_EX_BAR(G::VM_MIN);
     else
       SEDX_EX_BAR(0);
-    const int buf = chunk % 3;
-    if (chunk + 2 < nchunks) SEDX_EX_DMA(chunk + 2, (chunk + 2) % 3);
+    const int dbuf = buf == 0 ? NB - 1 : buf - 1;   // (chunk + NB - 1) % NB
+    if (chunk + NB - 1 < nchunks) SEDX_EX_DMA(chunk + NB - 1, dbuf);
     const float* As = smem + buf * G::BUF;
     const float* Ws = As + G::A_SZ;
     float2 a[2][MT], bb[2][NT];   // [slot][.]: (.x, .y) = (ks 0, ks 1)
@@ -267,9 +278,12 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 && WT == 64 ? 2 : 1) void co
         for (int nt = 0; nt < NT; ++nt)
           acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[cur][mt].y, bb[cur][nt].y, acc[mt][nt], 0, 0, 0);
     }
-    // FUSE: the next chunk's halo (its buffer was last read in chunk - 2)
+    const int nbuf = buf + 1 == NB ? 0 : buf + 1;
+    // FUSE: the next chunk's halo (its buffer's A region was last read in
+    // chunk + 1 - NB)
     if constexpr (FUSE)
-      if (chunk + 1 < nchunks) SEDX_EX_CONV1(chunk + 1, (chunk + 1) % 3);
+      if (chunk + 1 < nchunks) SEDX_EX_CONV1(chunk + 1, nbuf);
+    buf = nbuf;
   }
   SEDX_EX_BAR(0);   // every wave's fragment reads done before the epilogue reuses the LDS
 #undef SEDX_EX_DMA

@@ -67,10 +67,12 @@ __device__ __forceinline__ unsigned g_ld(const unsigned* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // sc1
 }
 
-constexpr int GRU_MAX_SLOTS = 4;
+constexpr int GRU_MAX_SLOTS = 4;      // 2 * slots (slot, dir) pairs on 8 XCD residues
 constexpr int GRU_VALU_CLIPS = 8;     // exact launches this small run the VALU product
 constexpr int GRU_HV_LD = 260;        // Hv row stride (floats): 8 rows fit the A-image space
-static_assert(GRU_VALU_CLIPS * GRU_HV_LD <= 16 * 32 * 4 * 4, "Hv inside Aimg");      // 2 * slots (slot, dir) pairs on 8 XCD residues
+static_assert(GRU_VALU_CLIPS * GRU_HV_LD <= 16 * 32 * 4 * 4, "Hv inside Aimg");
+// VALU granules [2 pairs][2 parities][clips][256] u64 at the start of the exchange space
+static_assert(2 * 2 * GRU_VALU_CLIPS * 256 * 8 <= 8 * 2 * 32 * 256 * 4, "granules inside X");
 constexpr unsigned GRU_SPIN = 1u << 24;
 
 struct GruSync {                      // zeroed every launch
@@ -189,6 +191,14 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
     // tools/mfma_f32_semantics.cpp), so the chain over k ascending gives the
     // MFMA kernel's bits: results do not depend on the batch size.  h_{s-1}
     // then lives as Hv[clip][k] (row stride GRU_HV_LD) in the A-image space.
+    // Its hand-off is data-tagged (cdna_hip_programming.md Guideline 16 R2):
+    // each h value travels as one 8-byte {tag = step + 1, value} granule
+    // written by ONE sc1 store and swept with sc1 loads until the tag
+    // matches, so the data is the flag: no drain, no flag store, no
+    // separate poll, and placement-independent (granules zeroed every launch).
+    unsigned long long* Gx =
+        reinterpret_cast<unsigned long long*>(X) + (int64_t)pair * 2 * GRU_VALU_CLIPS * 256;
+    float hreg[2] = {0.f, 0.f};   // VALU: this thread's h_{s-1} for its (clip, unit) pairs
     for (int s = 0; s < T; ++s) {
       const int gs = j * T + s;                // step of this pair; flags/counts are gs-based
       const int t = dir ? T - 1 - s : s;
@@ -206,7 +216,7 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
           gi[i][0] = gi[i][1] = gi[i][2] = 0.f;
         }
       }
-      if (gs > 0) {
+      if (!VALU && gs > 0) {
         if (fast) {
           if (tid < 8) {
             unsigned spins = 0;
@@ -236,6 +246,34 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
       if (s == 0) {
         for (int i = tid; i < 16 * 32 * 4; i += 768) Aimg[i] = make_uint4(0, 0, 0, 0);
         for (int i = tid; i < 32 * 32; i += 768) hprev[i >> 5][i & 31] = 0.f;
+      } else if constexpr (VALU) {
+        // sweep: every granule loaded once, then re-polled until its tag == gs
+        const unsigned long long* src = Gx + ((gs - 1) & 1) * GRU_VALU_CLIPS * 256;
+        constexpr int NGR = (GRU_VALU_CLIPS * 256 + 767) / 768;
+        unsigned long long w[NGR];
+#pragma unroll
+        for (int k = 0; k < NGR; ++k) {
+          const int it = tid + 768 * k;
+          w[k] = it < nc * 256 ? __hip_atomic_load(src + it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+        }
+#pragma unroll
+        for (int k = 0; k < NGR; ++k) {
+          const int it = tid + 768 * k;
+          if (it < nc * 256) {
+            unsigned spins = 0;
+            while ((unsigned)(w[k] >> 32) != (unsigned)gs) {
+              if (++spins > GRU_SPIN) {
+                atomicOr(&sync->err, 4u);
+                s_err = 1;
+                break;
+              }
+              w[k] = __hip_atomic_load(src + it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            const int c = it >> 8, kk = it & 255;
+            const float v = __uint_as_float((unsigned)w[k]);
+            Af[c * GRU_HV_LD + kk] = v;
+          }
+        }
       } else {
         const float* src = Xs + ((gs - 1) & 1) * 32 * 256;
         // all of a thread's loads are issued before any is consumed (one L2
@@ -354,11 +392,16 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
             const float r = g_sigmoid(gi[i][0] + ghr);
             const float z = g_sigmoid(gi[i][1] + ghz);
             const float n = g_tanh(gi[i][2] + r * ghn);
-            hvs[i] = s_err ? __builtin_nanf("") : n + z * (hprev[c][u] - n);   // NaN propagates to every slice
+            const float hp = VALU ? hreg[i] : hprev[c][u];
+            hvs[i] = s_err ? __builtin_nanf("") : n + z * (hp - n);   // NaN propagates to every slice
           }
           float* xp = dst + c * 256 + 32 * p + u;
           if (c >= nc) {
             // absent clip: nothing to publish
+          } else if (VALU) {
+            __hip_atomic_store(Gx + (gs & 1) * GRU_VALU_CLIPS * 256 + c * 256 + 32 * p + u,
+                               ((unsigned long long)(gs + 1) << 32) | __float_as_uint(hvs[i]), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
           } else if (fast) {
             *xp = hvs[i];
           } else {
@@ -367,6 +410,13 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
           }
         }
       }
+      if constexpr (VALU) {
+        // h_prev stays in this thread's registers (same (clip, unit) every
+        // step), Hv and part are next written behind the post-sweep barrier:
+        // no barrier and no drain here
+        hreg[0] = hvs[0];
+        hreg[1] = hvs[1];
+      } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (tid == 0) {
@@ -374,6 +424,7 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
           *reinterpret_cast<volatile unsigned*>(Fl + p * 16) = (unsigned)(gs + 1);
         else
           __hip_atomic_fetch_add(C, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
       }
       GRU_STAMP(3);
       // the H output is not part of the hand-off: store it after the publish
@@ -403,9 +454,12 @@ void launch_gru_coop(const float* G, int B, int T, const float* whh, const float
   const int nslots = ngroups < GRU_MAX_SLOTS ? ngroups : GRU_MAX_SLOTS;
   GruSync* sync = static_cast<GruSync*>(ws);
   float* X = reinterpret_cast<float*>(static_cast<char*>(ws) + ((sizeof(GruSync) + 255) & ~size_t(255)));
-  // one fill launch: the size rounded to 256 B (the exchange buffers start there)
-  (void)hipMemsetAsync(sync, 0, (sizeof(GruSync) + 255) & ~size_t(255), s);
-  if (exact && B <= GRU_VALU_CLIPS)
+  // one fill launch: the sync block rounded to 256 B (the exchange buffers
+  // start there) and, for the tagged hand-off, its granules (every tag 0)
+  const size_t sync_bytes = (sizeof(GruSync) + 255) & ~size_t(255);
+  const bool valu = exact && B <= GRU_VALU_CLIPS;
+  (void)hipMemsetAsync(sync, 0, sync_bytes + (valu ? (size_t)2 * 2 * GRU_VALU_CLIPS * 256 * 8 : 0), s);
+  if (valu)
     launch_kernel(gru_coop_kernel<true, true>, dim3(64), 768, s, G, B, T, whh, bhh, H, X, sync, nslots,
                   allow_fast ? 1 : 0);
   else if (exact)
