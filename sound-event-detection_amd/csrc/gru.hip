@@ -103,7 +103,10 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
                                                        float* __restrict__ H, float* X,
                                                        GruSync* sync, int nslots, int allow_fast) {
   __shared__ uint4 Aimg[16 * 32 * 4];          // h_{s-1} hi/lo, [kstep][clip][4 slots]
-  __shared__ float part[4][3][32][33];         // K-quarter partial gate pre-activations
+  // partial gate pre-activations: K quarters (x3) / eighths (exact: two
+  // independent chains per wave, summed in order in the gate phase)
+  constexpr int KP = EXACT ? 8 : 4;
+  __shared__ float part[KP][3][32][33];
   __shared__ float hprev[32][33];              // own-slice h_{s-1}
   __shared__ int s_fast;
   __shared__ int s_err;                        // a bounded spin timed out: outputs become NaN
@@ -332,31 +335,40 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
       }
       __syncthreads();
       GRU_STAMP(1);
-      f32x16_g acc;
+      f32x16_g acc, acc1;
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[r] = 0.f;
       if constexpr (VALU) {
         // lane: gate row u = lane & 31 of gate nt, clips h, h + 2, ...
         for (int c = h; c < nc; c += 2) {
           const float4* hv = reinterpret_cast<const float4*>(Af + c * GRU_HV_LD + 64 * kq);
-          float a = 0.f;
+          float a0 = 0.f, a1 = 0.f;   // K eighths 2 kq and 2 kq + 1
 #pragma unroll
-          for (int q = 0; q < 16; ++q) {
-            const float4 x = hv[q], w = Wv[q];
-            a = fmaf(x.x, w.x, a);
-            a = fmaf(x.y, w.y, a);
-            a = fmaf(x.z, w.z, a);
-            a = fmaf(x.w, w.w, a);
+          for (int q = 0; q < 8; ++q) {
+            const float4 x = hv[q], w = Wv[q], y = hv[q + 8], v = Wv[q + 8];
+            a0 = fmaf(x.x, w.x, a0);
+            a1 = fmaf(y.x, v.x, a1);
+            a0 = fmaf(x.y, w.y, a0);
+            a1 = fmaf(y.y, v.y, a1);
+            a0 = fmaf(x.z, w.z, a0);
+            a1 = fmaf(y.z, v.z, a1);
+            a0 = fmaf(x.w, w.w, a0);
+            a1 = fmaf(y.w, v.w, a1);
           }
-          part[kq][nt][c][lane & 31] = a;
+          part[2 * kq][nt][c][lane & 31] = a0;
+          part[2 * kq + 1][nt][c][lane & 31] = a1;
         }
       } else if constexpr (EXACT) {
         const int c = lane & 31;
 #pragma unroll
-        for (int st = 0; st < 32; ++st) {
-          const int k = 64 * kq + 2 * st + h;
+        for (int r = 0; r < 16; ++r) acc1[r] = 0.f;
+#pragma unroll
+        for (int st = 0; st < 16; ++st) {   // two chains: K eighths 2 kq (acc), 2 kq + 1 (acc1)
+          const int k = 64 * kq + 2 * st + h, k1 = k + 32;
           const float a = Af[k * 32 + (c ^ ((k >> 3) & 31))];
+          const float a1 = Af[k1 * 32 + (c ^ ((k1 >> 3) & 31))];
           acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, Bf[st], acc, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, Bf[st + 16], acc1, 0, 0, 0);
         }
       } else {
         const int c = lane & 31, sw = (c >> 2) & 3;
@@ -370,7 +382,13 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
           acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(alo, Bhi[ks], acc, 0, 0, 0);
         }
       }
-      if constexpr (!VALU) {
+      if constexpr (EXACT && !VALU) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          part[2 * kq][nt][(r & 3) + 8 * (r >> 2) + 4 * h][lane & 31] = acc[r];
+          part[2 * kq + 1][nt][(r & 3) + 8 * (r >> 2) + 4 * h][lane & 31] = acc1[r];
+        }
+      } else if constexpr (!EXACT) {
 #pragma unroll
         for (int r = 0; r < 16; ++r)
           part[kq][nt][(r & 3) + 8 * (r >> 2) + 4 * h][lane & 31] = acc[r];
@@ -386,9 +404,16 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
         if (pr < 1024) {
           const int c = pr >> 5;
           if (c < nc) {
-            const float ghr = (((part[0][0][c][u] + part[1][0][c][u]) + part[2][0][c][u]) + part[3][0][c][u]) + br;
-            const float ghz = (((part[0][1][c][u] + part[1][1][c][u]) + part[2][1][c][u]) + part[3][1][c][u]) + bz;
-            const float ghn = (((part[0][2][c][u] + part[1][2][c][u]) + part[2][2][c][u]) + part[3][2][c][u]) + bn;
+            float ghr = part[0][0][c][u], ghz = part[0][1][c][u], ghn = part[0][2][c][u];
+#pragma unroll
+            for (int q = 1; q < KP; ++q) {   // partials in K order
+              ghr += part[q][0][c][u];
+              ghz += part[q][1][c][u];
+              ghn += part[q][2][c][u];
+            }
+            ghr += br;
+            ghz += bz;
+            ghn += bn;
             const float r = g_sigmoid(gi[i][0] + ghr);
             const float z = g_sigmoid(gi[i][1] + ghz);
             const float n = g_tanh(gi[i][2] + r * ghn);

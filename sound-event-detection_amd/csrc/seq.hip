@@ -80,21 +80,27 @@ __global__ __launch_bounds__(256) void linear_kernel(const float* __restrict__ A
 // in flight per wave, no LDS and no barriers.  Every output's MFMA sequence
 // (k ascending in pairs, zero start, + bias, act) is linear_kernel's, so the
 // two shapes give identical bits.
-template <int ACT>
-__global__ __launch_bounds__(64) void linear_small_kernel(const float* __restrict__ A, int M, int K,
-                                                          const float* __restrict__ W, int N,
-                                                          const float* __restrict__ bias,
-                                                          float* __restrict__ C) {
-  const int lane = threadIdx.x, i = lane & 31, kh = lane >> 5;
+//
+// KS = 4 (the AttBlock att|cla projection, N <= 64, at every M): four waves
+// per tile, wave q chaining K quarter q, the quarters summed in order
+// ((q0 + q1) + q2) + q3 — a different (fixed) summation order, used for
+// every call of that projection, so results stay batch-size independent.
+template <int ACT, int KS>
+__global__ __launch_bounds__(64 * KS) void linear_small_kernel(const float* __restrict__ A, int M, int K,
+                                                               const float* __restrict__ W, int N,
+                                                               const float* __restrict__ bias,
+                                                               float* __restrict__ C) {
+  const int lane = threadIdx.x & 63, i = lane & 31, kh = lane >> 5, wq_ = threadIdx.x >> 6;
   const int m0 = blockIdx.x * 32, n0 = blockIdx.y * 32;
-  const float4* ap = reinterpret_cast<const float4*>(A + (int64_t)min(m0 + i, M - 1) * K);
-  const float4* wq = reinterpret_cast<const float4*>(W + (int64_t)(n0 + i) * K);
+  const int KQ = K / KS;   // this wave's K range: [wq_ KQ, (wq_ + 1) KQ)
+  const float4* ap = reinterpret_cast<const float4*>(A + (int64_t)min(m0 + i, M - 1) * K + wq_ * KQ);
+  const float4* wq = reinterpret_cast<const float4*>(W + (int64_t)(n0 + i) * K + wq_ * KQ);
   f32x16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
   constexpr int Q = 16;  // float4 per row per round (64 k); two rounds in registers
   float4 xa0[Q], xw0[Q], xa1[Q], xw1[Q];
-  const int nr = K / (4 * Q);
+  const int nr = KQ / (4 * Q);
   auto load = [&](float4* xa, float4* xw, int rd) {
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
@@ -120,6 +126,18 @@ __global__ __launch_bounds__(64) void linear_small_kernel(const float* __restric
       mma(xa1, xw1);
     }
   }
+  if constexpr (KS > 1) {
+    __shared__ float part[KS - 1][32][33];
+    if (wq_ > 0)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) part[wq_ - 1][(r & 3) + 8 * (r >> 2) + 4 * kh][i] = acc[r];
+    __syncthreads();
+    if (wq_ > 0) return;
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+#pragma unroll
+      for (int q = 0; q < KS - 1; ++q) acc[r] += part[q][(r & 3) + 8 * (r >> 2) + 4 * kh][i];
+  }
   const int n = n0 + i;
   const float bv = bias ? bias[n] : 0.0f;
 #pragma unroll
@@ -138,12 +156,14 @@ void launch_linear(const float* A, int M, int K, const float* W, int N, const fl
   dim3 grid((M + 127) / 128, N / 64);
   int dev = 0, ncu = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  const dim3 g2((M + 31) / 32, N / 32);
+  if (N <= 64 && act == 0 && K % 256 == 0 && N % 32 == 0)   // the head projection, every M
+    return launch_kernel(linear_small_kernel<0, 4>, g2, 256, s, A, M, K, W, N, bias, C);
   if ((int64_t)grid.x * grid.y < ncu && K % 64 == 0 && N % 32 == 0) {
-    dim3 g2((M + 31) / 32, N / 32);
     if (act == 1)
-      launch_kernel(linear_small_kernel<1>, g2, 64, s, A, M, K, W, N, bias, C);
+      launch_kernel(linear_small_kernel<1, 1>, g2, 64, s, A, M, K, W, N, bias, C);
     else
-      launch_kernel(linear_small_kernel<0>, g2, 64, s, A, M, K, W, N, bias, C);
+      launch_kernel(linear_small_kernel<0, 1>, g2, 64, s, A, M, K, W, N, bias, C);
     return;
   }
   if (act == 1)
@@ -306,17 +326,18 @@ __global__ __launch_bounds__(256) void att_head_kernel(const float* __restrict__
     const int nc = min(32, C - c0);
     const bool act = cs < nc;
     const int c = c0 + cs;
+    // (index maps by shifts and masks: no integer division in the loops)
     auto stage = [&](int t0, int nt) {
       __syncthreads();
-      for (int i = tid; i < nt * 2 * nc; i += 256) {
-        const int t = i / (2 * nc), j = i - t * 2 * nc;
-        const int half = j >= nc, cc = j - half * nc;
-        const float v = lg[(int64_t)(t0 + t) * ldl + half * C + c0 + cc];
-        if (half)
-          s_cla[t][cc] = v;
-        else
-          s_att[t][cc] = v;
-      }
+      const int j = tid & 63, half = j >> 5, cc = j & 31;
+      if (cc < nc)
+        for (int t = tid >> 6; t < nt; t += 4) {
+          const float v = lg[(int64_t)(t0 + t) * ldl + half * C + c0 + cc];
+          if (half)
+            s_cla[t][cc] = v;
+          else
+            s_att[t][cc] = v;
+        }
       __syncthreads();
     };
     // pass 1: sum over t of exp(clamp(att)) + 1e-6 (lane l: t = l, l + 8, ...)
@@ -341,25 +362,21 @@ __global__ __launch_bounds__(256) void att_head_kernel(const float* __restrict__
           s_cla[t][cs] = cl;
         }
       __syncthreads();
-      for (int i = tid; i < nt * 8 * nc; i += 256) {
-        const int cc = i % nc, fr = i / nc;
-        fw[((int64_t)b * out_frames + 8 * t0 + fr) * C + c0 + cc] = s_cla[fr >> 3][cc];
-      }
+      if ((tid & 31) < nc)
+        for (int fr = tid >> 5; fr < nt * 8; fr += 8)
+          fw[((int64_t)b * out_frames + 8 * t0 + fr) * C + c0 + (tid & 31)] = s_cla[fr >> 3][tid & 31];
       if (emb)
-        for (int i = tid; i < nt * nc; i += 256) {
-          const int t = i % nt, cc = i / nt;
-          emb[((int64_t)b * C + c0 + cc) * T + t0 + t] = s_cla[t][cc];
-        }
+        for (int cc = tid >> 7; cc < nc; cc += 2)
+          if ((tid & 127) < nt) emb[((int64_t)b * C + c0 + cc) * T + t0 + (tid & 127)] = s_cla[tid & 127][cc];
       if (t0 + nt == T && tid < nc) s_last[tid] = s_cla[nt - 1][tid];
     }
     acc = sum8_(acc);
     if (act && l == 0) clip[(int64_t)b * C + c] = acc;
     __syncthreads();
     const int npad = out_frames - 8 * T;          // GRU: last frame repeated
-    for (int i = tid; i < npad * nc; i += 256) {
-      const int cc = i % nc, f = 8 * T + i / nc;
-      fw[((int64_t)b * out_frames + f) * C + c0 + cc] = s_last[cc];
-    }
+    if ((tid & 31) < nc)
+      for (int f = 8 * T + (tid >> 5); f < 8 * T + npad; f += 8)
+        fw[((int64_t)b * out_frames + f) * C + c0 + (tid & 31)] = s_last[tid & 31];
   }
 }
 
