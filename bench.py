@@ -319,8 +319,8 @@ def conv_kernel_name(stage, precision):
     bn = 64 if cout == 64 else 128
     if precision == 'x3':
         return 'sedx::conv3x3_x3_kernel<%d, %d, %d, %s>' % (F, bn, epi, 'true' if stage == 'b1c2' else 'false')
-    # exact: 8-wave tiles at the bench shapes (4-wave tiles only for small grids)
-    return 'sedx::conv3x3_kernel<%d, %d, %d, %s, 8>' % (F, bn, epi, 'true' if stage == 'b1c2' else 'false')
+    # exact: 8-wave 64x64 wave tiles at the bench shapes (4-wave / 32x32 only for small grids)
+    return 'sedx::conv3x3_kernel<%d, %d, %d, %s, 8, 64>' % (F, bn, epi, 'true' if stage == 'b1c2' else 'false')
 
 
 def profiled(kernel):

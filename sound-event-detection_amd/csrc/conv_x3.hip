@@ -810,7 +810,7 @@ static void launch_x3_epi(const float* in, int B, int T, int Cin, int Cout, cons
   constexpr int TT = ConvGeom<F, BN>::TT;
   // workgroups resident on the whole device (per device)
   const LaunchInfo li =
-      launch_info(reinterpret_cast<const void*>(conv3x3_x3_kernel<F, BN, EPI, FUSE>), 512, 0, false);
+      launch_info(reinterpret_cast<const void*>(conv3x3_x3_kernel<F, BN, EPI, FUSE>), 512, 0);
   if (!li.ok) return;
   const int resident = li.ncu * li.per_cu;
   const size_t pad = li.dyn;

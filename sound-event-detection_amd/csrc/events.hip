@@ -298,8 +298,8 @@ void launch_events(const EventArgs& a, int mode, hipStream_t s) {
   const unsigned blocks = (unsigned)((n + wpb - 1) / wpb);
   const size_t lds = (size_t)wpb * 2 * W * 8;
   // > 64 KB of dynamic LDS must be opted into (per device: launch_info)
-  if (!launch_info(reinterpret_cast<const void*>(events_series_kernel<0>), 64, EV_LDS_BYTES, false).ok ||
-      !launch_info(reinterpret_cast<const void*>(events_series_kernel<1>), 64, EV_LDS_BYTES, false).ok)
+  if (!launch_info(reinterpret_cast<const void*>(events_series_kernel<0>), 64, EV_LDS_BYTES).ok ||
+      !launch_info(reinterpret_cast<const void*>(events_series_kernel<1>), 64, EV_LDS_BYTES).ok)
     return;
   if (mode == 0)
     hipLaunchKernelGGL(events_series_kernel<0>, dim3(blocks), dim3(64 * wpb), lds, s, a, W, wpb);

@@ -223,7 +223,7 @@ constexpr size_t FE_MEL_LDS = 16 * 1024;   // room for the packed mel weights (<
 template <int NFFT, bool I16>
 static void launch_logmel_t(const FrontendParams& p0, int64_t total, hipStream_t s) {
   const LaunchInfo li =
-      launch_info(reinterpret_cast<const void*>(logmel_kernel<NFFT, I16>), 64 * FE_WAVES, FE_MEL_LDS, false);
+      launch_info(reinterpret_cast<const void*>(logmel_kernel<NFFT, I16>), 64 * FE_WAVES, FE_MEL_LDS);
   if (!li.ok) return;
   FrontendParams p = p0;
   p.mel_lds_floats = (int32_t)(li.dyn / 4);
@@ -518,7 +518,7 @@ size_t gamma_workspace_bytes(int64_t B, int64_t T, int nfft) {
 template <int NFFT>
 static void launch_gamma_spec(const GammaParams& p, hipStream_t s) {
   const void* k = reinterpret_cast<const void*>(gamma_spec_kernel<NFFT>);
-  const LaunchInfo li = launch_info(k, GAMMA_SPEC_THREADS, gamma_spec_lds<NFFT>(), false);
+  const LaunchInfo li = launch_info(k, GAMMA_SPEC_THREADS, gamma_spec_lds<NFFT>());
   if (!li.ok) return;
   const int64_t total = (int64_t)p.B * p.T;
   int64_t blocks = std::min<int64_t>(total, (int64_t)li.ncu * li.per_cu * 4);

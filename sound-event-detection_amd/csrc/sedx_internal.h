@@ -83,6 +83,7 @@ void launch_block1_exact(const float* xpad, int B, int T, const float* w1, const
                          const float* bias, float* out, const float* zero16, hipStream_t s);
 
 enum ConvEpi { EPI_STORE = 0, EPI_POOL2 = 1, EPI_FMEAN = 2 };
+constexpr int CONV_SCHED_INTS = 256;   // per conv launch: 8 tile-claim counters, 128 B apart
 // 3x3 conv (pad 1) + folded BN + ReLU (+ epilogue), implicit GEMM on fp32 MFMA.
 //  in [B][T][F][Cin] -> EPI_STORE: [B][T][F][Cout], EPI_POOL2: [B][T/2][F/2][Cout],
 //  EPI_FMEAN: [B][T][Cout].  wp = packed [Cin/4][9][2][Cout][2] (channel 2 ks + khalf), bias [Cout].
@@ -126,7 +127,6 @@ inline hipError_t take_launch_error() {
   return e;
 }
 
-constexpr int LDS_PER_CU = 160 * 1024;   // gfx950 LDS per CU (the device attribute reports 64 KB)
 
 // Per (device, kernel) launch facts, computed once under a mutex: the CU
 // count, the kernel's workgroups per CU at its own LDS footprint, and the
@@ -138,9 +138,8 @@ struct LaunchInfo {
   int per_cu = 0;
   size_t dyn = 0;
 };
-// dyn_need: dynamic LDS the kernel itself uses.  exclusive: pad the dynamic
-// LDS so the kernel's workgroups fill the CU's LDS at its own occupancy.
-inline LaunchInfo launch_info(const void* kernel, int block_threads, size_t dyn_need, bool exclusive) {
+// dyn_need: dynamic LDS the kernel uses (set as its maximum once).
+inline LaunchInfo launch_info(const void* kernel, int block_threads, size_t dyn_need) {
   static std::mutex mu;
   static std::map<std::pair<int, const void*>, LaunchInfo> cache;
   int dev = 0;
@@ -154,9 +153,7 @@ inline LaunchInfo launch_info(const void* kernel, int block_threads, size_t dyn_
   auto it = cache.find(key);
   if (it != cache.end()) return it->second;
   LaunchInfo li;
-  hipFuncAttributes fa{};
-  if ((e = hipFuncGetAttributes(&fa, kernel)) != hipSuccess ||
-      (e = hipDeviceGetAttribute(&li.ncu, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) {
+  if ((e = hipDeviceGetAttribute(&li.ncu, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) {
     note_launch_error(e);
     return LaunchInfo{};
   }
@@ -173,23 +170,8 @@ inline LaunchInfo launch_info(const void* kernel, int block_threads, size_t dyn_
   if (li.per_cu < 1) li.per_cu = 1;
   if (li.ncu < 1) li.ncu = 256;
   li.dyn = dyn_need;
-  if (exclusive) {
-    const size_t per_wg = ((size_t)LDS_PER_CU / (size_t)li.per_cu) & ~size_t(511);
-    const size_t used = fa.sharedSizeBytes + dyn_need;
-    if (per_wg > used) {
-      li.dyn = dyn_need + (per_wg - used);
-      if ((e = hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)li.dyn)) !=
-          hipSuccess) {
-        note_launch_error(e);
-        return LaunchInfo{};
-      }
-    }
-  }
   li.ok = true;
   cache[key] = li;
-  if (getenv("SEDX_DEBUG_LDS"))
-    fprintf(stderr, "sedx: dev %d kernel %p static LDS %zu B, dyn %zu B, %d workgroups/CU\n", dev, kernel,
-            (size_t)fa.sharedSizeBytes, li.dyn, li.per_cu);
   return li;
 }
 
@@ -211,12 +193,11 @@ __device__ __forceinline__ void sedx_glds16(const void* src, uint32_t m0) {
 // skipped (error noted) if they could not be
 template <typename... P, typename... A>
 inline void launch_kernel(void (*kern)(P...), dim3 grid, int threads, hipStream_t s, A... args) {
-  if (!launch_info(reinterpret_cast<const void*>(kern), threads, 0, false).ok) return;
+  if (!launch_info(reinterpret_cast<const void*>(kern), threads, 0).ok) return;
   hipLaunchKernelGGL(kern, grid, dim3(threads), 0, s, args...);
 }
 
 // sched: CONV_SCHED_INTS zeroed ints per launch (the 8 per-XCD tile-claim counters)
-constexpr int CONV_SCHED_INTS = 256;
 void launch_conv3x3_x3(const float* in, int B, int T, int F, int Cin, int Cout, const void* wp,
                        const float* bias, float* out, int epi, int* sched, hipStream_t s);
 // block 1 of the CNN in one conv launch (x3): with x0, pads the bn0 output
