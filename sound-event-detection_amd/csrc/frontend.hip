@@ -134,37 +134,51 @@ __global__ __launch_bounds__(64 * FE_WAVES) void logmel_kernel(FrontendParams p)
   const float bmu = p.bn_mean[m], bsc = p.bn_scale[m], bbi = p.bn_bias[m];
   __syncthreads();
 
-  const int64_t total = (int64_t)p.n_clips * p.n_win * p.T;
-  const int64_t L = p.sig_len;
+  // frame bookkeeping in 32-bit (the host checks items * T < 2^31 and
+  // sig_len < 2^31): 64-bit division costs hundreds of instructions
+  const int total = p.n_clips * p.n_win * p.T;
+  const int L = (int)p.sig_len;
   float2* X = s_buf[wave][0];
   float2* Y = s_buf[wave][1];
   // samples of frame fr: lane holds j = pos0 + 2 (lane + 64 i) + e
-  auto load = [&](int64_t fr, float* v) {
-    const int64_t item = fr / p.T;
-    const int t = (int)(fr - item * p.T);
-    const int64_t clip = item / p.n_win;
-    const int w = (int)(item - clip * p.n_win);
+  auto load = [&](int fr, float* v) {
+    const unsigned item = (unsigned)fr / (unsigned)p.T;
+    const int t = fr - (int)item * p.T;
+    const unsigned clip = item / (unsigned)p.n_win;
+    const int w = (int)(item - clip * (unsigned)p.n_win);
     const int64_t wstart = p.win_start[w];
-    const int64_t src_off = clip * p.clip_stride + wstart;
-    const int64_t avail = p.clip_len - wstart;      // samples of this item backed by audio
-    const int64_t pos0 = (int64_t)t * p.hop - N2;   // start in un-padded coordinates
+    const int64_t src_off = (int64_t)clip * p.clip_stride + wstart;
+    const int64_t av64 = p.clip_len - wstart;        // samples of this item backed by audio
+    const int avail = av64 > L ? L : (int)av64;       // (j < L always)
+    const int pos0 = t * p.hop - N2;                  // start in un-padded coordinates
+    if (!I16 && pos0 >= 0 && pos0 + NFFT <= avail && ((src_off + pos0) & 1) == 0) {
+      // interior frame (no reflection, no pad_truncate): 8-byte loads
+      const float2* src = reinterpret_cast<const float2*>(p.audio + src_off + pos0);
+#pragma unroll
+      for (int i = 0; i < NS / 2; ++i) {
+        const float2 q = src[lane + 64 * i];
+        v[2 * i] = q.x;
+        v[2 * i + 1] = q.y;
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < NS / 2; ++i)
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
-        int64_t j = pos0 + 2 * (lane + 64 * i) + e;
+        int j = pos0 + 2 * (lane + 64 * i) + e;
         if (j < 0) j = -j;                           // reflect (F.pad mode='reflect')
         if (j >= L) j = 2 * (L - 1) - j;
         const bool ok = j < avail;                   // pad_truncate zeros
-        const int64_t jc = ok ? j : 0;
+        const int jc = ok ? j : 0;
         if (I16)   // int16_to_float32: float64 x / 32767, rounded to float32
           v[2 * i + e] = ok ? (float)((double)p.audio_i16[src_off + jc] / 32767.0) : 0.0f;
         else
           v[2 * i + e] = ok ? p.audio[src_off + jc] : 0.0f;
       }
   };
-  int64_t fr = (int64_t)blockIdx.x * FE_WAVES + wave;
-  const int64_t fstride = (int64_t)gridDim.x * FE_WAVES;
+  int fr = (int)blockIdx.x * FE_WAVES + wave;
+  const int fstride = (int)gridDim.x * FE_WAVES;
   float v[NS];
   if (fr < total) load(fr, v);
   for (; fr < total; fr += fstride) {
@@ -210,7 +224,7 @@ __global__ __launch_bounds__(64 * FE_WAVES) void logmel_kernel(FrontendParams p)
     }
     float db = 10.0f * log10f(fmaxf(acc, 1e-10f));
     db = (db - bmu) * bsc + bbi;
-    p.out[fr * 64 + m] = db;
+    p.out[(int64_t)fr * 64 + m] = db;
     wave_lds_sync();                      // P / Z reads done before the next frame's writes
   }
 }
@@ -235,6 +249,7 @@ static void launch_logmel_t(const FrontendParams& p0, int64_t total, hipStream_t
 
 void launch_logmel(const FrontendParams& p, int n_fft, hipStream_t s) {
   const int64_t total = (int64_t)p.n_clips * p.n_win * p.T;
+  if (total >= (int64_t)1 << 31 || p.sig_len >= (int64_t)1 << 31) return note_launch_error(hipErrorInvalidValue);
   const bool i16 = p.audio_i16 != nullptr;
   switch (n_fft) {
     case 256:
