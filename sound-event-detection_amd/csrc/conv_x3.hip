@@ -199,7 +199,6 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
   constexpr int NW = (WS_U4 + 511) / 512;
   // store instructions one epilogue issues per wave (all of them issue)
   constexpr int EPI_NST = (EPI == EPI_FMEAN) ? 2 * MT * 2 : 4 * MT * 2;
-#ifndef SEDX_NO_GLDS_W
   // weight stages go global -> LDS by LDS-DMA (global_load_lds_dwordx4): the
   // host-prepared image is copied lane-linearly, no VGPR round trip, no
   // ds_write pass.  A DMA issued after a stage barrier must land before the
@@ -207,9 +206,6 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
   // (not FUSE: block 1 measured 2 % slower with it — its conv1 VALU work
   // and conditional halo loads force vmcnt(0) at every barrier)
   constexpr bool GW = !FUSE;
-#else
-  constexpr bool GW = false;
-#endif
 
   // one LDS object per W slot and one for the halo images: every fragment
   // read is (lane base VGPR) + immediate, and the compiler's alias scopes
@@ -450,10 +446,8 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
     }                                                                                   \
     __builtin_amdgcn_sched_barrier(0);                                                  \
   }
-// cache policy of the epilogue stores (A/B builds: -DSEDX_EPI_AUX=2 is nt)
-#ifndef SEDX_EPI_AUX
-#define SEDX_EPI_AUX 0
-#endif
+// epilogue stores: default cache policy (nt measured neutral in the model)
+constexpr int EPI_AUX = 0;
 #ifdef SEDX_SETPRIO
 #define SEDX_PRIO(p) __builtin_amdgcn_s_setprio(p)
 #else
@@ -504,11 +498,6 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
     for (int nt = 0; nt < NT; ++nt) {
       const int n = n0 + wn * 64 + nt * 32 + (lane_ & 31);
       const float bv = bcur[nt];
-#ifdef SEDX_CONV_ABL_NOSTORE
-      const bool live = bv == -1e30f;   // diagnostic: stores never taken, MFMAs kept
-#else
-      constexpr bool live = true;
-#endif
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
         const int Rbase = wm * WM + mt * 32;
@@ -516,17 +505,6 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
 #pragma unroll
         for (int i = 0; i < 16; ++i) r[i] = fmaxf(acc[mt][nt][i] + bv, 0.0f);
         if (EPI == EPI_STORE) {
-#ifdef SEDX_EPI_DWORD
-          float* ob = out + ((int64_t)c.b * T + c.t0) * F * Cout + n;
-          const int tlim = T - c.t0;
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            int tl, f;
-            rowmap<F, EPI>(Rbase + (i & 3) + 8 * (i >> 2) + 4 * h, tl, f);
-            if (live && tl < tlim) ob[(tl * F + f) * Cout] = r[i];
-            if ((i & 3) == 3) __builtin_amdgcn_sched_barrier(0);
-          }
-#else
           // regs 4g..4g+3 are 4 consecutive pixels of this lane's channel; a
           // 4x4 transpose inside each lane quad gives every lane 4 consecutive
           // channels of one pixel: 4 dwordx4 stores instead of 16 dword stores,
@@ -539,13 +517,12 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
             quad_transpose4(v, j);
             int tl, f;
             rowmap<F, EPI>(Rbase + 8 * g + 4 * h + j, tl, f);
-            const uint32_t off = (live && tl < tlim) ? (uint32_t)(((tl * F + f) * Cout + n - j) * 4) : OOB;
+            const uint32_t off = (tl < tlim) ? (uint32_t)(((tl * F + f) * Cout + n - j) * 4) : OOB;
             typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
             const u32x4 w = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
-            __builtin_amdgcn_raw_buffer_store_b128(w, ors, off, 0, SEDX_EPI_AUX);
+            __builtin_amdgcn_raw_buffer_store_b128(w, ors, off, 0, EPI_AUX);
             __builtin_amdgcn_sched_barrier(0);
           }
-#endif
         } else if (EPI == EPI_POOL2) {
           constexpr int FO = F / 2;
           const int To = T / 2;
@@ -555,18 +532,18 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
             const int tp = q / FO, fp = q % FO;
             const int to = c.t0 / 2 + tp;
             const float v = (((r[4 * g] + r[4 * g + 1]) + r[4 * g + 2]) + r[4 * g + 3]) * 0.25f;
-            const uint32_t off = (live && to < To) ? (uint32_t)(((tp * FO + fp) * Cout + n) * 4) : OOB;
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), ors, off, 0, SEDX_EPI_AUX);
+            const uint32_t off = (to < To) ? (uint32_t)(((tp * FO + fp) * Cout + n) * 4) : OOB;
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), ors, off, 0, EPI_AUX);
           }
         } else {  // EPI_FMEAN, F == 8: regs {0-3,12-15} and {4-11} are one t each (rowmap)
           const float sa = (((r[0] + r[1]) + (r[2] + r[3])) + ((r[12] + r[13]) + (r[14] + r[15])));
           const float sb = (((r[4] + r[5]) + (r[6] + r[7])) + ((r[8] + r[9]) + (r[10] + r[11])));
           const int tb = c.t0 + 4 * (Rbase >> 5);
           const int ta = tb + (h ? 3 : 0), tb2 = tb + (h ? 2 : 1);
-          const uint32_t offa = (live && ta < T) ? (uint32_t)(((ta - c.t0) * Cout + n) * 4) : OOB;
-          const uint32_t offb = (live && tb2 < T) ? (uint32_t)(((tb2 - c.t0) * Cout + n) * 4) : OOB;
-          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(sa * 0.125f), ors, offa, 0, SEDX_EPI_AUX);
-          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(sb * 0.125f), ors, offb, 0, SEDX_EPI_AUX);
+          const uint32_t offa = (ta < T) ? (uint32_t)(((ta - c.t0) * Cout + n) * 4) : OOB;
+          const uint32_t offb = (tb2 < T) ? (uint32_t)(((tb2 - c.t0) * Cout + n) * 4) : OOB;
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(sa * 0.125f), ors, offa, 0, EPI_AUX);
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(sb * 0.125f), ors, offb, 0, EPI_AUX);
         }
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc[mt][nt][i] = 0.0f;
@@ -629,28 +606,6 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
   //   KY 2: W(n1, 1)  -> slot U
   // each followed by the load of the weights two stages further on into the
   // register set just drained (W(n1, 1), W(n1, 2), W(n2, 0)).
-#ifdef SEDX_ABL_NOLDS     // diagnostics (tools/gpu_conv_bench.sh): drop the stage's LDS writes
-#define SEDX_ABL_STORE_W(rs, slot)
-#define SEDX_ABL_STORE_A(buf, c_)
-#else
-#define SEDX_ABL_STORE_W(rs, slot) SEDX_STORE_W(rs, slot)
-#define SEDX_ABL_STORE_A(buf, c_) SEDX_STORE_A(buf, c_)
-#endif
-#if defined(SEDX_ABL_NOLOAD) || defined(SEDX_ABL_NOLOADW)   // ... or its global loads
-#define SEDX_ABL_LOAD_W(rs, c_, ky_)
-#else
-#define SEDX_ABL_LOAD_W(rs, c_, ky_) SEDX_LOAD_W(rs, c_, ky_)
-#endif
-#if defined(SEDX_ABL_NOLOAD) || defined(SEDX_ABL_NOLOADA)
-#define SEDX_ABL_LOAD_A(c_)
-#else
-#define SEDX_ABL_LOAD_A(c_) SEDX_LOAD_A(c_)
-#endif
-#ifdef SEDX_ABL_NOBAR     // ... or its barrier
-#define SEDX_ABL_SYNC()
-#else
-#define SEDX_ABL_SYNC() __syncthreads()
-#endif
 // After the stage barrier the wave interleaves the stage's LDS writes and
 // global refill loads with the 4 MFMA groups of the stage's last tap (whose
 // fragments were read before the barrier), so the matrix pipe is not idle
@@ -664,13 +619,8 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
     acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[set][2 * (mt) + 1], fb[set][2 * (nt)], acc[mt][nt], 0, 0, 0); \
     __builtin_amdgcn_sched_barrier(0);                                                  \
   }
-#ifdef SEDX_NO_INTERLEAVE
-#define SEDX_MFMA_PIECE(set, mt, nt)
-#define SEDX_MFMA_REST(set) SEDX_MFMAS(set)
-#else
 #define SEDX_MFMA_PIECE(set, mt, nt) SEDX_MFMA_G(set, mt, nt)
 #define SEDX_MFMA_REST(set) SEDX_MFMA_G(set, 1, 1)
-#endif
 // FUSE: the conv1 work of n1's halo items (VALU-heavy) is issued between the
 // MFMAs of the stage's first tap, BEFORE the stage barrier.  Legal: A buffer
 // U^1 was last read by unit U-1 before its stage-2 barrier, and n1's inputs
@@ -681,7 +631,7 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
     /* DMA of the stage after next into the slot just freed, then halo(n2)   */          \
     SEDX_MFMA_PIECE(set, 0, 0);                                                         \
     if ((KY) == 0) {                                                                    \
-      SEDX_ABL_STORE_A((U) ^ 1, n1);                                                    \
+      SEDX_STORE_A((U) ^ 1, n1);                                                    \
     }                                                                                   \
     SEDX_MFMA_PIECE(set, 0, 1);                                                         \
     if ((KY) == 0) {                                                                    \
@@ -694,26 +644,26 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
     }                                                                                   \
     SEDX_MFMA_PIECE(set, 1, 0);                                                         \
     if ((KY) == 0) {                                                                    \
-      SEDX_ABL_LOAD_A(n2);                                                              \
+      SEDX_LOAD_A(n2);                                                              \
     }                                                                                   \
     SEDX_MFMA_REST(set);                                                                \
   } else {                                                                              \
     SEDX_MFMA_PIECE(set, 0, 0);                                                         \
     if ((KY) == 0) {                                                                    \
-      SEDX_ABL_STORE_W((U) & 1, U);                                                     \
+      SEDX_STORE_W((U) & 1, U);                                                     \
     } else if ((KY) == 1) {                                                             \
-      SEDX_ABL_STORE_W(((U) + 1) & 1, ((U) + 1) & 1);                                   \
+      SEDX_STORE_W(((U) + 1) & 1, ((U) + 1) & 1);                                   \
     } else {                                                                            \
-      SEDX_ABL_STORE_W((U) & 1, (U) & 1);                                               \
+      SEDX_STORE_W((U) & 1, (U) & 1);                                               \
     }                                                                                   \
     SEDX_MFMA_PIECE(set, 0, 1);                                                         \
     if ((KY) == 0) {                                                                    \
-      SEDX_ABL_LOAD_W((U) & 1, n1, 1);                                                  \
+      SEDX_LOAD_W((U) & 1, n1, 1);                                                  \
     } else if ((KY) == 1) {                                                             \
-      SEDX_ABL_LOAD_W(((U) + 1) & 1, n1, 2);                                            \
+      SEDX_LOAD_W(((U) + 1) & 1, n1, 2);                                            \
     } else {                                                                            \
       if (tid == 0) claim_land();                                                       \
-      SEDX_ABL_LOAD_W((U) & 1, n2, 0);                                                  \
+      SEDX_LOAD_W((U) & 1, n2, 0);                                                  \
     }                                                                                   \
     SEDX_MFMA_PIECE(set, 1, 0);                                                         \
     if constexpr (FUSE) {                                                               \
@@ -723,8 +673,8 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
         SEDX_LOAD_A(n2);                                                                \
       }                                                                                 \
     } else if ((KY) == 0) {                                                             \
-      SEDX_ABL_STORE_A((U) ^ 1, n1);                                                    \
-      SEDX_ABL_LOAD_A(n2);                                                              \
+      SEDX_STORE_A((U) ^ 1, n1);                                                    \
+      SEDX_LOAD_A(n2);                                                              \
     }                                                                                   \
     SEDX_MFMA_REST(set);                                                                \
   }
@@ -749,7 +699,7 @@ __global__ __launch_bounds__(512) void conv3x3_x3_kernel(const float* __restrict
       else if ((KY) == 0 && epi_prev) SEDX_BAR_VM(EPI_NST);                            \
       else SEDX_BAR_VM(0);                              \
     } else {                                                                            \
-      SEDX_ABL_SYNC();                                                                  \
+      __syncthreads();                                                                  \
     }                                                                                   \
     SEDX_ST_END(st_bar);                                                                \
     SEDX_ST_VMWAIT();                                                                   \
