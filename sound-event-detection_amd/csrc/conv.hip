@@ -32,6 +32,41 @@
 namespace sedx {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+#ifdef SEDX_EXACT_STAMPS
+// diagnostic build (tools/conv_exact_bench.cpp): per-wave s_memtime sums —
+// [0] wave cycles, [1] barrier waits, [2] FUSE conv1, [3] epilogue, [4] waves,
+// [5] wave realtime (100 MHz)
+__device__ unsigned long long g_exact_stamps[8];
+#define SEDX_XS_DECL                                                                    \
+  unsigned long long xs_bar = 0, xs_c1 = 0, xs_epi = 0, xs_x = 0;                       \
+  const unsigned long long xs_t0 = __builtin_amdgcn_s_memtime();                        \
+  const unsigned long long xs_r0 = __builtin_amdgcn_s_memrealtime();
+#define SEDX_XS_BEGIN() xs_x = __builtin_amdgcn_s_memtime()
+#define SEDX_XS_END(a) a += __builtin_amdgcn_s_memtime() - xs_x
+#define SEDX_XS_FLUSH()   /* sampled: every 16th workgroup (few atomics) */         \
+  if (lane == 0 && (blockIdx.x & 15) == 0) {                                            \
+    atomicAdd(&g_exact_stamps[0], __builtin_amdgcn_s_memtime() - xs_t0);                \
+    atomicAdd(&g_exact_stamps[1], xs_bar);                                              \
+    atomicAdd(&g_exact_stamps[2], xs_c1);                                               \
+    atomicAdd(&g_exact_stamps[3], xs_epi);                                              \
+    atomicAdd(&g_exact_stamps[4], 1ull);                                                \
+    atomicAdd(&g_exact_stamps[5], __builtin_amdgcn_s_memrealtime() - xs_r0);            \
+  }
+void exact_stamps_rw(unsigned long long* out8, bool reset) {
+  (void)hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_exact_stamps), 8 * sizeof(unsigned long long));
+  if (reset) {
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_exact_stamps), z, sizeof(z));
+  }
+}
+#else
+#define SEDX_XS_DECL
+#define SEDX_XS_BEGIN()
+#define SEDX_XS_END(a)
+#define SEDX_XS_FLUSH()
+#endif
 
 // WAVES waves per workgroup, each owning a WT x WT output tile (WT = 64:
 // 2 x 2 MFMA tiles; WT = 32: one), BN / WT of them along N and the rest
@@ -57,7 +92,8 @@ struct ExactGeom {
   static constexpr int EC = BN / (WT / 32);          // epilogue pass: one 32-column MFMA tile per wave
   static constexpr int CPAD = EC + 4;
   static constexpr int LDS_EPI = BM * CPAD;
-  static constexpr int LDS_FLOATS = MAIN > LDS_EPI ? MAIN : LDS_EPI;
+  static constexpr int W1_OFF = MAIN > LDS_EPI ? MAIN : LDS_EPI;   // FUSE: conv1 weights + bias
+  static constexpr int LDS_FLOATS = W1_OFF + (FUSE ? 64 * 9 + 64 : 0);
   // LDS-DMA units (one wave-instruction = 64 lanes x 16 B = 1 KiB) per chunk
   static constexpr int UW = W_SZ / 256;              // weight slab
   static constexpr int UA = FUSE ? 0 : PLP / 64;     // halo (FUSE computes it instead)
@@ -176,22 +212,36 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 && WT == 64 ? 2 : 1) void co
 
   // ---- FUSE: the 3x3 X0 window of each staged pixel in registers; conv1
   // (BN folded + ReLU) of a chunk's 4 channels computed into the halo image
-  // while the previous chunk's MFMAs run (its weights by scalar loads) ----
-  bool pin[G::NA];
-  float pmask[G::NA];
+  // while the previous chunk's MFMAs run, on the matrix pipe:
+  // v_mfma_f32_4x4x1f32 (16 blocks of 4 pixels x 4 channels, one tap per
+  // instruction) over taps 0..8 from zero is bit for bit the fma chain
+  // s = fma(w_k, x_k, s) (fp32 MFMAs on gfx950 are in-order fma chains:
+  // tools/mfma_f32_semantics.cpp, tools/mfma16_f32_semantics.cpp), so it
+  // equals the VALU conv1 it replaces (14.8 % of b1c2's wave time, s_memtime).
+  // Lane l supplies pixel 64 g + l's tap value (A) and w1[channel l & 3][tap]
+  // (B); it receives pixels 64 g + 4 (l >> 2) + r, r = 0..3, channel l & 3. ----
   float xw[FUSE ? G::NA : 1][9];
+  float omask[FUSE ? G::NA : 1][4];   // validity of the 4 output pixels of each group
   if constexpr (FUSE) {
+    for (int i = tid; i < 64 * 9 + 64; i += EX_THREADS) smem[G::W1_OFF + i] = i < 576 ? w1[i] : b1[i - 576];
+    __syncthreads();
 #pragma unroll
     for (int i = 0; i < G::NA; ++i) {
       const int pix = tid + EX_THREADS * i;
       const int r = pix / CS, c = pix - (pix / CS) * CS;
       const int t = t0 - 1 + r, f = c - 1;
-      pin[i] = pix < PL && t >= 0 && t < T && f >= 0 && f < F;
-      pmask[i] = pin[i] ? 1.0f : 0.0f;
+      const bool pin = pix < PL && t >= 0 && t < T && f >= 0 && f < F;
       // X0pad [B][T+2][66]: (t, f) of X0 at (t+1, f+1); window corner (t, f)
-      const int64_t src = pin[i] ? ((int64_t)b * (T + 2) + t) * 66 + f : 0;
+      const int64_t src = pin ? ((int64_t)b * (T + 2) + t) * 66 + f : 0;
 #pragma unroll
-      for (int k = 0; k < 9; ++k) xw[i][k] = in[src + (k / 3) * 66 + (k % 3)];   // masked by pmask
+      for (int k = 0; k < 9; ++k) xw[i][k] = in[src + (k / 3) * 66 + (k % 3)];   // masked via omask
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int po = EX_THREADS * i + 64 * wv + 4 * (lane >> 2) + q;
+        const int ro = po / CS, co = po - ro * CS;
+        const int to = t0 - 1 + ro, fo = co - 1;
+        omask[i][q] = (po < PL && to >= 0 && to < T && fo >= 0 && fo < F) ? 1.0f : 0.0f;
+      }
     }
     // the window loads retire here, on every path, so the compiler's wait
     // tracking does not carry them into the chunk loop, where a wait for them
@@ -201,22 +251,18 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 && WT == 64 ? 2 : 1) void co
 #define SEDX_EX_CONV1(chunk_, buf_)                                                                    \
   {                                                                                                    \
     float* As_ = smem + (buf_) * G::BUF;                                                               \
-    /* wave-uniform addresses: scalar (SMEM) loads, FMAs with SGPR operands */                       \
-    float wv_[KC][9], bv_[KC];                                                                         \
-    _Pragma("unroll") for (int c = 0; c < KC; ++c) {                                                   \
-      bv_[c] = b1[(chunk_) * KC + c];                                                                  \
-      _Pragma("unroll") for (int k = 0; k < 9; ++k) wv_[c][k] = w1[((chunk_) * KC + c) * 9 + k];      \
-    }                                                                                                  \
+    const int ch_ = (chunk_) * KC + (lane & 3);                                                        \
+    float wv_[9];                                                                                      \
+    _Pragma("unroll") for (int k = 0; k < 9; ++k) wv_[k] = smem[G::W1_OFF + ch_ * 9 + k];             \
+    const float bv_ = smem[G::W1_OFF + 576 + ch_];                                                     \
     _Pragma("unroll") for (int i = 0; i < G::NA; ++i) {                                                \
-      const int pix = tid + EX_THREADS * i;                                                            \
-      if (G::NA * EX_THREADS == PL || pix < PL) {                                                      \
-        float v_[KC];                                                                                  \
-        _Pragma("unroll") for (int c = 0; c < KC; ++c) {                                               \
-          float s_ = 0.0f;                                                                             \
-          _Pragma("unroll") for (int k = 0; k < 9; ++k) s_ = fmaf(wv_[c][k], xw[i][k], s_);           \
-          v_[c] = fmaxf(s_ + bv_[c], 0.0f) * pmask[i];   /* zero outside the clip */                   \
-        }                                                                                              \
-        *reinterpret_cast<float4*>(As_ + pix * KC) = make_float4(v_[0], v_[1], v_[2], v_[3]);          \
+      if (G::NA * EX_THREADS == PL || EX_THREADS * i + 64 * wv < PL) {   /* wave-uniform */            \
+        f32x4 d_ = {0.0f, 0.0f, 0.0f, 0.0f};                                                           \
+        _Pragma("unroll") for (int k = 0; k < 9; ++k)                                                  \
+            d_ = __builtin_amdgcn_mfma_f32_4x4x1f32(xw[i][k], wv_[k], d_, 0, 0, 0);                    \
+        const int p0_ = EX_THREADS * i + 64 * wv + 4 * (lane >> 2);                                    \
+        _Pragma("unroll") for (int q = 0; q < 4; ++q)                                                  \
+            As_[(p0_ + q) * KC + (lane & 3)] = fmaxf(d_[q] + bv_, 0.0f) * omask[i][q];                 \
       }                                                                                                \
     }                                                                                                  \
   }
@@ -225,6 +271,7 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 && WT == 64 ? 2 : 1) void co
   // __syncthreads() would drain every DMA in flight)
 #define SEDX_EX_BAR(n_) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(n_) : "memory")
 
+  SEDX_XS_DECL
   const int nchunks = Cin / KC;
   constexpr int NB = G::NBUF;
 #pragma unroll
@@ -237,6 +284,7 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 && WT == 64 ? 2 : 1) void co
     // the younger chunks' DMAs (up to NB - 2 of them) still in flight; buffer
     // (chunk + NB - 1) % NB was last read in chunk - 1, finished by every wave
     const int younger = min(NB - 2, nchunks - 1 - chunk);
+    SEDX_XS_BEGIN();
     if (younger >= 3 && NB > 4)
       SEDX_EX_BAR(3 * G::VM_MIN);
     else if (younger == 2 && NB > 3)
@@ -245,6 +293,7 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 && WT == 64 ? 2 : 1) void co
       SEDX_EX_BAR(G::VM_MIN);
     else
       SEDX_EX_BAR(0);
+    SEDX_XS_END(xs_bar);
     const int dbuf = buf == 0 ? NB - 1 : buf - 1;   // (chunk + NB - 1) % NB
     if (chunk + NB - 1 < nchunks) SEDX_EX_DMA(chunk + NB - 1, dbuf);
     const float* As = smem + buf * G::BUF;
@@ -281,11 +330,17 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 && WT == 64 ? 2 : 1) void co
     const int nbuf = buf + 1 == NB ? 0 : buf + 1;
     // FUSE: the next chunk's halo (its buffer's A region was last read in
     // chunk + 1 - NB)
-    if constexpr (FUSE)
+    if constexpr (FUSE) {
+      SEDX_XS_BEGIN();
       if (chunk + 1 < nchunks) SEDX_EX_CONV1(chunk + 1, nbuf);
+      SEDX_XS_END(xs_c1);
+    }
     buf = nbuf;
   }
+  SEDX_XS_BEGIN();
   SEDX_EX_BAR(0);   // every wave's fragment reads done before the epilogue reuses the LDS
+  SEDX_XS_END(xs_bar);
+  SEDX_XS_BEGIN();
 #undef SEDX_EX_DMA
 #undef SEDX_EX_CONV1
 #undef SEDX_EX_BAR
@@ -381,6 +436,8 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 && WT == 64 ? 2 : 1) void co
       if (h + 1 < NT) __syncthreads();
     }
   }
+  SEDX_XS_END(xs_epi);
+  SEDX_XS_FLUSH();
 }
 
 template <int F, int BN, bool FUSE, int WAVES, int WT>

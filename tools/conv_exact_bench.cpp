@@ -8,6 +8,9 @@
 #include <cstring>
 #include <vector>
 #include "../sound-event-detection_amd/csrc/sedx_internal.h"
+#ifdef SEDX_EXACT_STAMPS
+namespace sedx { void exact_stamps_rw(unsigned long long* out8, bool reset); }
+#endif
 
 struct Layer { const char* name; int T, F, cin, cout, epi; };
 
@@ -50,6 +53,10 @@ int main(int argc, char** argv) {
     };
     go();
     hipDeviceSynchronize();
+#ifdef SEDX_EXACT_STAMPS
+    unsigned long long st[8];
+    sedx::exact_stamps_rw(st, true);
+#endif
     hipEventRecord(e0, 0);
     for (int r = 0; r < reps; ++r) go();
     hipEventRecord(e1, 0);
@@ -62,6 +69,15 @@ int main(int argc, char** argv) {
     tot_ms += ms; tot_f += fl;
     printf("%s  T=%4d F=%2d %3d->%3d  %.4f ms  %.1f TF/s  (%.3f of 157.3)\n", l.name, l.T, l.F, l.cin, l.cout, ms,
            fl / ms / 1e9, fl / ms / 1e9 / 157.3);
+#ifdef SEDX_EXACT_STAMPS
+    sedx::exact_stamps_rw(st, true);
+    {
+      const double tot = (double)st[0];
+      printf("      stamps: waves %llu  barrier %.1f%%  conv1 %.1f%%  epilogue %.1f%%  (cycles/wave %.0f, clock %.2f GHz)\n",
+             st[4], 100 * st[1] / tot, 100 * st[2] / tot, 100 * st[3] / tot, tot / (double)st[4],
+             tot / (double)st[5] * 0.1);
+    }
+#endif
   }
   printf("total %.4f ms  %.1f TF/s  (err=%s, launch=%s)\n", tot_ms, tot_f / tot_ms / 1e9,
          hipGetErrorString(hipGetLastError()), hipGetErrorString(sedx::take_launch_error()));

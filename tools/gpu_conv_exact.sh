@@ -9,6 +9,7 @@ C=sound-event-detection_amd/csrc
 O=tools/prev
 if [ -n "$BUILD" ]; then
   $HIPCC -o $O/cx_full tools/conv_exact_bench.cpp $C/conv.hip || exit 1
+  $HIPCC -DSEDX_EXACT_STAMPS -o $O/cx_stamps tools/conv_exact_bench.cpp $C/conv.hip || exit 1
   for v in $O/conv_*.hip; do
     [ -f "$v" ] || continue
     n=$(basename $v .hip); n=${n#conv_}
