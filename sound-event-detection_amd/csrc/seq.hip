@@ -223,70 +223,77 @@ void launch_gru(const float* G, int B, int T, const float* whhT, const float* bh
 // (the cooperative multi-CU recurrence lives in gru.hip)
 
 // ---------------------------------------------------------------------------
-// MHA core.  grid (ceil(T/128), B*8); thread = query row.
+// MHA core.  grid (ceil(T/32), B*8), 128 threads: 4 lanes per query row
+// (lane quarter g = lane & 3 owns dims 16g..16g+15), so a row's serial dot /
+// p.v chain is 16 long instead of 64 and a single clip fills 32x more
+// threads.  q.k = the 4 partial dots summed in a fixed order (quad shuffles);
+// exact two-pass softmax as before.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(128) void mha_kernel(const float* __restrict__ QKV, int T,
                                                   float* __restrict__ O) {
-  constexpr int KC = 64;
-  __shared__ float Ks[KC][64];
-  __shared__ float Vs[KC][64];
+  constexpr int KC = 64, DG = 16;
+  __shared__ float Ks[KC][68];
+  __shared__ float Vs[KC][68];
   const int bh = blockIdx.y;
   const int b = bh >> 3, head = bh & 7;
-  const int qi = blockIdx.x * 128 + threadIdx.x;
+  const int g = threadIdx.x & 3;
+  const int qi = blockIdx.x * 32 + (threadIdx.x >> 2);
   const bool valid = qi < T;
   const float* base = QKV + (int64_t)b * T * 1536;
-  float q[64], o[64];
+  float q[DG], o[DG];
 #pragma unroll
-  for (int d = 0; d < 64; ++d) {
-    q[d] = valid ? base[(int64_t)qi * 1536 + head * 64 + d] : 0.0f;
+  for (int d = 0; d < DG; ++d) {
+    q[d] = valid ? base[(int64_t)qi * 1536 + head * 64 + DG * g + d] : 0.0f;
     o[d] = 0.0f;
   }
+  // q.k of this row with key row jj: partial dots over 16 dims, then
+  // ((p0 + p1) + (p2 + p3)) by two quad shuffles (every lane gets the sum)
+  auto dot = [&](int jj) {
+    float s = 0.f;
+#pragma unroll
+    for (int d = 0; d < DG; ++d) s = fmaf(q[d], Ks[jj][DG * g + d], s);
+    s += __shfl_xor(s, 1);
+    s += __shfl_xor(s, 2);
+    return s;
+  };
+  auto stage = [&](int c0, int nk, bool v) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < nk * 64; i += 128) {
+      const int64_t r = (int64_t)(c0 + (i >> 6)) * 1536 + head * 64 + (i & 63);
+      Ks[i >> 6][i & 63] = base[r + 512];
+      if (v) Vs[i >> 6][i & 63] = base[r + 1024];
+    }
+    __syncthreads();
+  };
   // pass 1: row max of q.k / 8
   float mx = -INFINITY;
   for (int c0 = 0; c0 < T; c0 += KC) {
     const int nk = min(KC, T - c0);
-    __syncthreads();
-    for (int i = threadIdx.x; i < nk * 64; i += 128)
-      Ks[i >> 6][i & 63] = base[(int64_t)(c0 + (i >> 6)) * 1536 + 512 + head * 64 + (i & 63)];
-    __syncthreads();
-    for (int jj = 0; jj < nk; ++jj) {
-      float s = 0.f;
-#pragma unroll
-      for (int d = 0; d < 64; ++d) s = fmaf(q[d], Ks[jj][d], s);
-      mx = fmaxf(mx, s / 8.0f);
-    }
+    stage(c0, nk, false);
+    for (int jj = 0; jj < nk; ++jj) mx = fmaxf(mx, dot(jj) / 8.0f);
   }
   // pass 2: exp, sum, p.v
   float l = 0.f;
   for (int c0 = 0; c0 < T; c0 += KC) {
     const int nk = min(KC, T - c0);
-    __syncthreads();
-    for (int i = threadIdx.x; i < nk * 64; i += 128) {
-      const int64_t r = (int64_t)(c0 + (i >> 6)) * 1536 + head * 64 + (i & 63);
-      Ks[i >> 6][i & 63] = base[r + 512];
-      Vs[i >> 6][i & 63] = base[r + 1024];
-    }
-    __syncthreads();
+    stage(c0, nk, true);
     for (int jj = 0; jj < nk; ++jj) {
-      float s = 0.f;
-#pragma unroll
-      for (int d = 0; d < 64; ++d) s = fmaf(q[d], Ks[jj][d], s);
-      const float p = expf(s / 8.0f - mx);
+      const float p = expf(dot(jj) / 8.0f - mx);
       l += p;
 #pragma unroll
-      for (int d = 0; d < 64; ++d) o[d] = fmaf(p, Vs[jj][d], o[d]);
+      for (int d = 0; d < DG; ++d) o[d] = fmaf(p, Vs[jj][DG * g + d], o[d]);
     }
   }
   if (valid) {
     const float inv = 1.0f / l;
-    float* dst = O + ((int64_t)b * T + qi) * 512 + head * 64;
+    float* dst = O + ((int64_t)b * T + qi) * 512 + head * 64 + DG * g;
 #pragma unroll
-    for (int d = 0; d < 64; ++d) dst[d] = o[d] * inv;
+    for (int d = 0; d < DG; ++d) dst[d] = o[d] * inv;
   }
 }
 
 void launch_mha(const float* QKV, int B, int T, float* O, hipStream_t s) {
-  hipLaunchKernelGGL(mha_kernel, dim3((T + 127) / 128, B * 8), dim3(128), 0, s, QKV, T, O);
+  hipLaunchKernelGGL(mha_kernel, dim3((T + 31) / 32, B * 8), dim3(128), 0, s, QKV, T, O);
 }
 
 // ---------------------------------------------------------------------------
