@@ -510,6 +510,15 @@ def main():
     extra = {}
     if world == 1 and rank == 0 and not args.no_side and args.mode == 'clip':
         extra['stage_ms_isolated'] = stage_times_isolated(model, wave, dev, max(3, min(args.steps, 10)))
+        if roof is not None:
+            # the same launch one batch at a time (no other batch's GRU / head /
+            # frontend sharing the chip): the kernel's own rate beside the
+            # timed-region figure above
+            dom = roof['kernel'].rsplit('(', 1)[-1].rstrip(')')
+            iso = extra['stage_ms_isolated'].get(dom)
+            if iso:
+                roof['avg_launch_ms_isolated'] = iso
+                roof['frac_isolated'] = round(roof['flops_per_launch'] / (iso * 1e-3) / 1e12 / roof['peak'], 4)
         if extra['stage_ms_isolated'].get('frontend'):
             fe = extra['stage_ms_isolated']['frontend']
             extra['frontend_roofline'] = {
