@@ -541,8 +541,9 @@ static int device_cus() {
 }
 
 // Shape by grid size: 8-wave 64x64 wave tiles when they make at least two
-// workgroups per CU of the chip; 4-wave ones while those still give every CU
-// a workgroup; below that (small batches) 32x32 wave tiles over whole pairs
+// workgroups per CU of the chip; 4-wave ones likewise (one workgroup per CU
+// and a half-empty second round measured slower than the small shapes);
+// below that (small batches) 32x32 wave tiles over whole pairs
 // of t-rows (F = 64: 8 waves, F = 32: 4), or at F = 16 / 8 16x16 wave tiles
 // over pairs of t-rows (8 / 4 waves), BN = 64.  All give bit-identical
 // outputs.
@@ -557,7 +558,7 @@ static void launch_f_bn(const float* in, int B, int T, int Cin, int Cout, const 
   constexpr int SW = (F == 8 ? 32 : 2 * F) / 32 * 2;   // WT = 32 shape: (BM / 32) x (64 / 32) waves
   if (tiles8 >= 2 * ncu)
     launch_f_bn_w<F, BN, FUSE, 8, 64>(in, B, T, Cin, Cout, wp, bias, out, epi, w1, b1, zero16, s);
-  else if (tiles4 >= ncu)
+  else if (tiles4 >= 2 * ncu)
     launch_f_bn_w<F, BN, FUSE, 4, 64>(in, B, T, Cin, Cout, wp, bias, out, epi, w1, b1, zero16, s);
   else if constexpr (F <= 16)   // WT = 16: 2 t-rows x F bins, BN = 64 -> (2F / 16) x 4 waves
     launch_f_bn_w<F, 64, FUSE, F / 2, 16>(in, B, T, Cin, Cout, wp, bias, out, epi, w1, b1, zero16, s);
