@@ -23,9 +23,12 @@ __global__ __launch_bounds__(256) void linear_kernel(const float* __restrict__ A
                                                      const float* __restrict__ W, int N,
                                                      const float* __restrict__ bias,
                                                      float* __restrict__ C) {
+  // 128 x 64 tile, 4 waves of 32 rows x 64 columns; K in slices of 16 staged
+  // through a 2-slot LDS ring, the next slice's global loads in flight (in
+  // registers) while the current slice's MFMAs run: one barrier per slice
   constexpr int BM = 128, BN = 64, BK = 16;
-  __shared__ float As[BK][BM + 4];
-  __shared__ float Ws[BK][BN + 4];
+  __shared__ float As[2][BK][BM + 4];
+  __shared__ float Ws[2][BK][BN + 4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
   const int kh = lane >> 5;
@@ -34,28 +37,50 @@ __global__ __launch_bounds__(256) void linear_kernel(const float* __restrict__ A
   for (int j = 0; j < 2; ++j)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[j][r] = 0.0f;
-  for (int k0 = 0; k0 < K; k0 += BK) {
-    // A tile: 128 rows x 16 k  (512 float4)
-    for (int i = tid; i < BM * BK / 4; i += 256) {
+  // per thread: 2 float4 of the A slice (128 rows x 4 quads), 1 of the W slice
+  float4 ra[2], rw;
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int i = tid + 256 * e;
       const int m = i % BM, q = i / BM;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (m0 + m < M) v = *reinterpret_cast<const float4*>(A + (int64_t)(m0 + m) * K + k0 + 4 * q);
-      As[4 * q + 0][m] = v.x; As[4 * q + 1][m] = v.y; As[4 * q + 2][m] = v.z; As[4 * q + 3][m] = v.w;
+      const int row = min(m0 + m, M - 1);   // rows past M: any valid row, never stored
+      ra[e] = *reinterpret_cast<const float4*>(A + (int64_t)row * K + k0 + 4 * q);
     }
-    for (int i = tid; i < BN * BK / 4; i += 256) {
-      const int n = i % BN, q = i / BN;
-      const float4 v = *reinterpret_cast<const float4*>(W + (int64_t)(n0 + n) * K + k0 + 4 * q);
-      Ws[4 * q + 0][n] = v.x; Ws[4 * q + 1][n] = v.y; Ws[4 * q + 2][n] = v.z; Ws[4 * q + 3][n] = v.w;
+    const int n = tid % BN, q = tid / BN;
+    rw = *reinterpret_cast<const float4*>(W + (int64_t)(n0 + n) * K + k0 + 4 * q);
+  };
+  auto store = [&](int slot) {
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int i = tid + 256 * e;
+      const int m = i % BM, q = i / BM;
+      As[slot][4 * q + 0][m] = ra[e].x; As[slot][4 * q + 1][m] = ra[e].y;
+      As[slot][4 * q + 2][m] = ra[e].z; As[slot][4 * q + 3][m] = ra[e].w;
     }
-    __syncthreads();
+    const int n = tid % BN, q = tid / BN;
+    Ws[slot][4 * q + 0][n] = rw.x; Ws[slot][4 * q + 1][n] = rw.y;
+    Ws[slot][4 * q + 2][n] = rw.z; Ws[slot][4 * q + 3][n] = rw.w;
+  };
+  const int nk = K / BK;
+  load(0);
+  store(0);
+  if (nk > 1) load(BK);
+  __syncthreads();
+  for (int it = 0; it < nk; ++it) {
+    const int slot = it & 1;
 #pragma unroll
     for (int ks = 0; ks < BK / 2; ++ks) {
-      const float a = As[2 * ks + kh][wave * 32 + (lane & 31)];
+      const float a = As[slot][2 * ks + kh][wave * 32 + (lane & 31)];
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const float bb = Ws[2 * ks + kh][j * 32 + (lane & 31)];
+        const float bb = Ws[slot][2 * ks + kh][j * 32 + (lane & 31)];
         acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bb, acc[j], 0, 0, 0);
       }
+    }
+    if (it + 1 < nk) {
+      store(slot ^ 1);                     // slot ^ 1 was last read in it - 1 (barrier below it)
+      if (it + 2 < nk) load((it + 2) * BK);
     }
     __syncthreads();
   }
