@@ -36,6 +36,12 @@ struct WaveSync {
   __device__ void operator()() const { wave_lds_sync(); }
 };
 
+// FFT buffers hold one pad element per 32 (pidx): the radix-4 stages write
+// with strides 4 Ns, which unpadded put 8 lanes of a write on one bank
+__device__ __forceinline__ int pidx(int i) { return i + (i >> 5); }
+template <int N2>
+constexpr int fe_buf_len() { return N2 + N2 / 32; }
+
 // In-LDS Stockham FFT of N2 complex points (forward, e^{-2 pi i}); one wave.
 // tw = exp(-2 pi i m / NFFT) with NFFT = 2*N2.  Radix 4 while N2/Ns allows,
 // then radix 2; every stage's geometry is a compile-time constant.
@@ -56,7 +62,7 @@ __device__ __forceinline__ float2* stockham_stages(float2* X, float2* Y, const f
       const int k = j & (Ns - 1);
       const int base = (j - k) * R + k;
       if constexpr (R == 4) {
-        float2 v0 = X[j], v1 = X[j + nb], v2 = X[j + 2 * nb], v3 = X[j + 3 * nb];
+        float2 v0 = X[pidx(j)], v1 = X[pidx(j + nb)], v2 = X[pidx(j + 2 * nb)], v3 = X[pidx(j + 3 * nb)];
         if constexpr (Ns > 1) {
           v1 = cmul(v1, tw[k * step]);
           v2 = cmul(v2, tw[2 * k * step]);
@@ -65,15 +71,15 @@ __device__ __forceinline__ float2* stockham_stages(float2* X, float2* Y, const f
         const float2 a0 = cadd(v0, v2), a1 = csub(v0, v2);
         const float2 b0 = cadd(v1, v3), b1 = csub(v1, v3);
         const float2 mib1 = make_float2(b1.y, -b1.x);   // -i * b1
-        Y[base] = cadd(a0, b0);
-        Y[base + Ns] = cadd(a1, mib1);
-        Y[base + 2 * Ns] = csub(a0, b0);
-        Y[base + 3 * Ns] = csub(a1, mib1);
+        Y[pidx(base)] = cadd(a0, b0);
+        Y[pidx(base + Ns)] = cadd(a1, mib1);
+        Y[pidx(base + 2 * Ns)] = csub(a0, b0);
+        Y[pidx(base + 3 * Ns)] = csub(a1, mib1);
       } else {
-        float2 v0 = X[j], v1 = X[j + nb];
+        float2 v0 = X[pidx(j)], v1 = X[pidx(j + nb)];
         if constexpr (Ns > 1) v1 = cmul(v1, tw[k * step]);
-        Y[base] = cadd(v0, v1);
-        Y[base + Ns] = csub(v0, v1);
+        Y[pidx(base)] = cadd(v0, v1);
+        Y[pidx(base + Ns)] = csub(v0, v1);
       }
     }
     Sync()();
@@ -91,8 +97,8 @@ __device__ __forceinline__ void stockham_fft(float2* X, float2* Y, const float2*
 // z[m] = x[2m] + i x[2m+1].
 template <int N2>
 __device__ __forceinline__ float2 real_bin(const float2* Z, const float2* tw, int k) {
-  const float2 A = Z[k & (N2 - 1)];
-  const float2 Bz = Z[(N2 - k) & (N2 - 1)];
+  const float2 A = Z[pidx(k & (N2 - 1))];
+  const float2 Bz = Z[pidx((N2 - k) & (N2 - 1))];
   const float2 Bc = make_float2(Bz.x, -Bz.y);
   const float2 E = make_float2(0.5f * (A.x + Bc.x), 0.5f * (A.y + Bc.y));
   const float2 O = make_float2(0.5f * (A.y - Bc.y), -0.5f * (A.x - Bc.x));  // -i (A - Bc) / 2
@@ -117,7 +123,7 @@ __global__ __launch_bounds__(64 * FE_WAVES) void logmel_kernel(FrontendParams p)
   constexpr int NS = NFFT / 64;          // samples per lane per frame
   __shared__ float2 s_tw[NFFT];
   __shared__ float s_win[NFFT];
-  __shared__ float2 s_buf[FE_WAVES][2][N2];
+  __shared__ float2 s_buf[FE_WAVES][2][fe_buf_len<N2>()];
   extern __shared__ float s_melw[];      // [p.mel_lds_floats]: packed mel weights, then padding
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -185,7 +191,7 @@ __global__ __launch_bounds__(64 * FE_WAVES) void logmel_kernel(FrontendParams p)
 #pragma unroll
     for (int i = 0; i < NS / 2; ++i) {
       const int mm = lane + 64 * i;
-      X[mm] = make_float2(v[2 * i] * s_win[2 * mm], v[2 * i + 1] * s_win[2 * mm + 1]);
+      X[pidx(mm)] = make_float2(v[2 * i] * s_win[2 * mm], v[2 * i + 1] * s_win[2 * mm + 1]);
     }
     if (fr + fstride < total) load(fr + fstride, v);   // next frame, in flight during the FFT
     wave_lds_sync();
@@ -232,17 +238,31 @@ __global__ __launch_bounds__(64 * FE_WAVES) void logmel_kernel(FrontendParams p)
 // at most the resident workgroups of the chip; every wave walks several
 // frames, so the register prefetch of the next frame overlaps the current FFT
 // (launch facts per device: launch_info)
-constexpr size_t FE_MEL_LDS = 16 * 1024;   // room for the packed mel weights (<= 2 (n_fft/2+1) floats)
+// room for the packed mel weights: at most 2 (n_fft/2 + 1) floats (each bin
+// in at most two triangular bands), rounded to 256 B
+template <int NFFT>
+constexpr size_t fe_mel_lds() { return ((size_t)2 * (NFFT / 2 + 1) * 4 + 255) / 256 * 256; }
+// the kernel's static LDS: twiddles, window, two FFT buffers per wave
+template <int NFFT>
+constexpr size_t fe_static_lds() {
+  return (size_t)NFFT * 8 + NFFT * 4 + (size_t)FE_WAVES * 2 * fe_buf_len<NFFT / 2>() * 8;
+}
 
 template <int NFFT, bool I16>
 static void launch_logmel_t(const FrontendParams& p0, int64_t total, hipStream_t s) {
   const LaunchInfo li =
-      launch_info(reinterpret_cast<const void*>(logmel_kernel<NFFT, I16>), 64 * FE_WAVES, FE_MEL_LDS);
+      launch_info(reinterpret_cast<const void*>(logmel_kernel<NFFT, I16>), 64 * FE_WAVES, fe_mel_lds<NFFT>());
   if (!li.ok) return;
   FrontendParams p = p0;
   p.mel_lds_floats = (int32_t)(li.dyn / 4);
+  // the frame loop is LDS-latency bound (PMC: VALU busy ~27 %), so fill the
+  // CU: as many 16-wave workgroups as its 160 KB LDS holds, up to 32 waves
+  // (the occupancy query assumes 64 KB of LDS per CU on this part)
+  constexpr int64_t per_cu = std::max<int64_t>(1, std::min<int64_t>(2, (int64_t)(160 * 1024) /
+                                                                       (int64_t)(fe_static_lds<NFFT>() +
+                                                                                 fe_mel_lds<NFFT>())));
   int64_t blocks = (total + FE_WAVES - 1) / FE_WAVES;
-  blocks = std::min<int64_t>(blocks, (int64_t)li.ncu * li.per_cu);
+  blocks = std::min<int64_t>(blocks, (int64_t)li.ncu * per_cu);
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL((logmel_kernel<NFFT, I16>), dim3((unsigned)blocks), dim3(64 * FE_WAVES), li.dyn, s, p);
 }
