@@ -257,14 +257,17 @@ def host_to_host_step(model, host_wave, host_out, dev, world, rank):
 
 
 def latency_b1(model, dev, reps=20):
-    """End-to-end latency of ONE 10 s clip: clip mode and
-    window mode (its 6 windows in one launch) with the input on the device,
-    and clip mode from a host buffer to the framewise output back on the
-    host (PCIe-inclusive)."""
+    """End-to-end latency of ONE 10 s clip: clip mode (eager,
+    and replayed from a HIP graph: sedx.inference.GraphedForward), window mode
+    (its 6 windows in one launch) with the input on the device, and clip mode
+    from a host buffer to the framewise output back on the host
+    (PCIe-inclusive)."""
     w1 = torch.from_numpy(synth.make_waveforms(1, seconds=10.0, sample_rate=16000, seed=11))
     wd = w1.to(dev)
     out = {}
+    graphed = inference.GraphedForward(model, wd)
     for key, fn in (('clip', lambda: model(wd)['framewise_output']),
+                    ('clip_graph', lambda: graphed(wd)['framewise_output']),
                     ('window', lambda: inference.predict_windows(model, wd, 5, 1)),
                     ('clip_host_to_host', lambda: model(w1.to(dev))['framewise_output'].cpu())):
         with torch.no_grad():

