@@ -51,11 +51,16 @@ METRICS = {'gru': '10s@16kHz clips/sec (whole node) + ms/clip p50, Cnn_9_Gru_Fra
            'transformer': '10s@16kHz clips/sec (whole node) + ms/clip p50, Cnn_9_Transformer_FrameAtt logmel'}
 # MI355X_MICROARCH.md: FP32 matrix peak 157.3 TF; BF16 dense MFMA ~2.5 PF.  The
 # x3 scheme issues 3 bf16 MFMAs per useful MAC, so its arithmetic peak is 2.5/3 PF.
-PEAK_TF = {'exact': 157.3, 'x3': 2500.0 / 3}
+PEAK_TF = {'exact': 157.3, 'winograd': 157.3, 'x3': 2500.0 / 3}
 PEAK_HBM_GBPS = 8000.0
 PEAK_FP64_TF = 78.6        # MI355X datasheet FP64 vector (not in MI355X_MICROARCH.md)
 DTYPE = {'exact': 'f32',
+         'winograd': 'f32 (conv blocks 2-4 as Winograd F(2x2,3x3): f32 transforms, f32 MFMA, f32 accumulate)',
          'x3': 'bf16x3-split (3 bf16 MFMAs per f32 MAC: hi*hi + hi*lo + lo*hi, f32 accumulate)'}
+# Winograd F(2x2,3x3): 16 matrix-pipe multiplies per 2x2 output tile where the
+# direct conv does 36 (blocks 2-4 in 'winograd' mode; block 1 stays direct)
+WINO_STAGES = ('b2c1', 'b2c2', 'b3c1', 'b3c2', 'b4c1', 'b4c2')
+WINO_MUL = 16.0 / 36.0
 # conv stages of sedx_stage_times: (F, Cin, Cout, number of 2x poolings before it)
 CONV_STAGES = {'b1c2': (64, 64, 64, 0), 'b2c1': (32, 64, 128, 1), 'b2c2': (32, 128, 128, 1),
                'b3c1': (16, 128, 256, 2), 'b3c2': (16, 256, 256, 2), 'b4c1': (8, 256, 512, 3),
@@ -312,7 +317,7 @@ PROFILE_SUMMARY = os.path.join(REPO, 'profiles', 'r02_kernel_summary.json')
 
 
 # block 1's conv1 (Cin 1 -> 64) computed inside the b1c2 launch
-FUSED_BLOCK1 = {'x3': True, 'exact': True}
+FUSED_BLOCK1 = {'x3': True, 'exact': True, 'winograd': True}
 
 
 def conv_kernel_name(stage, precision):
@@ -322,6 +327,9 @@ def conv_kernel_name(stage, precision):
     bn = 64 if cout == 64 else 128
     if precision == 'x3':
         return 'sedx::conv3x3_x3_kernel<%d, %d, %d, %s>' % (F, bn, epi, 'true' if stage == 'b1c2' else 'false')
+    if precision == 'winograd' and stage in WINO_STAGES:
+        # 4 tile groups (8 waves) at the bench shapes
+        return 'sedx::conv3x3_wino_kernel<%d, %d, 4>' % (F, epi)
     # exact: 8-wave 64x64 wave tiles at the bench shapes (4-wave / 32x32 only for small grids)
     return 'sedx::conv3x3_kernel<%d, %d, %d, %s, 8, 64>' % (F, bn, epi, 'true' if stage == 'b1c2' else 'false')
 
@@ -348,17 +356,26 @@ def roofline(stage_ms, B, precision, T=1001):
     B=32, 10 s shapes only."""
     conv = {s: stage_ms[s] for s in CONV_STAGES}
     dom = max(conv, key=conv.get)
-    flops = conv_flops(dom, B, T)
+    wino = precision == 'winograd'
+    # matrix-pipe FLOPs the launch executes (Winograd layers: 16/36 of the
+    # direct conv's) — the roofline's numerator; the direct-conv equivalent
+    # is reported beside it
+    mul = {st: (WINO_MUL if wino and st in WINO_STAGES else 1.0) for st in CONV_STAGES}
+    flops = conv_flops(dom, B, T) * mul[dom]
     if dom == 'b1c2' and FUSED_BLOCK1[precision]:
         flops += 2.0 * B * T * 64 * 64 * 9      # conv1 (Cin 1 -> 64) computed inside the launch
     achieved = flops / (conv[dom] * 1e-3) / 1e12
     peak = PEAK_TF[precision]
-    total = sum(conv_flops(s, B, T) for s in CONV_STAGES) + 2.0 * B * T * 64 * 64 * 9
+    conv1 = 2.0 * B * T * 64 * 64 * 9
+    total = sum(conv_flops(st, B, T) * mul[st] for st in CONV_STAGES) + conv1
+    total_direct = sum(conv_flops(st, B, T) for st in CONV_STAGES) + conv1
     conv_ms = sum(conv.values()) + stage_ms.get('b1c1', 0.0)
     kname = conv_kernel_name(dom, precision)
     traffic, rocprof_ms, mfma_util, clock = profiled(kname) if (B, T) == (32, 1001) else (None,) * 4
     return {'bound': 'mfma', 'kernel': '%s (%s)' % (kname, dom),
             'arith': {'exact': 'fp32 MFMA v_mfma_f32_32x32x2_f32 (f32 in, f32 acc)',
+                      'winograd': 'fp32 MFMA v_mfma_f32_32x32x2_f32 (f32 in, f32 acc); blocks 2-4 Winograd '
+                                  'F(2x2,3x3), their FLOPs counted as executed (16/36 of direct)',
                       'x3': '3xbf16-split MFMA 32x32x16, f32 acc (peak = bf16 dense 2.5 PF / 3)'}[precision],
             'achieved': round(achieved, 2), 'peak': round(peak, 1), 'unit': 'TFLOP/s',
             'frac': round(achieved / peak, 4),
@@ -371,7 +388,9 @@ def roofline(stage_ms, B, precision, T=1001):
                       '(one event set per forward, all steps averaged); avg_launch_ms_rocprof: '
                       'rocprofv3 --kernel-trace --stats of this bench (--streams 1 --no-side), committed summary',
             'conv_stack_tflops': round(total / (conv_ms * 1e-3) / 1e12, 2),
-            'conv_stack_frac': round(total / (conv_ms * 1e-3) / 1e12 / peak, 4)}
+            'conv_stack_frac': round(total / (conv_ms * 1e-3) / 1e12 / peak, 4),
+            'conv_stack_direct_equiv_tflops': round(total_direct / (conv_ms * 1e-3) / 1e12, 2),
+            'conv_stack_ms': round(conv_ms, 4)}
 
 
 # ---------------------------------------------------------------------------
@@ -531,17 +550,19 @@ def main():
                 'ms_per_batch': fe, 'bytes_per_clip': FRONTEND_BYTES_PER_CLIP}
         extra.update(events_side(model, wave))
         extra['latency_b1'] = latency_b1(model, dev)
-        other = 'x3' if args.precision == 'exact' else 'exact'
-        model.set_precision(other)
-        extra['latency_b1_%s' % other] = latency_b1(model, dev)
-        model.set_precision(args.precision)
-        v2, e2, st2, p2, _ = clip_leg(model, wave, args, 1, 0, dev, other)
-        extra['value_%s' % other] = {'value': round(v2, 2), 'unit': 'clips/s', 'dtype': DTYPE[other],
-                                     'ms_per_step': round(e2 / args.steps * 1e3, 4),
-                                     'ms_per_clip_p50_device': round(p2, 4),
-                                     'roofline': roofline(st2, B, other), 'stage_ms': st2,
-                                     'note': 'opt-in arithmetic, same workload' if other == 'x3' else
-                                             'the reference arithmetic, same workload'}
+        notes = {'x3': 'opt-in arithmetic (operands narrowed to 16 significant bits), same workload',
+                 'exact': 'fp32, direct 3x3 conv everywhere (bit-reproducible reference arithmetic), same workload',
+                 'winograd': 'fp32, blocks 2-4 as Winograd F(2x2,3x3), same workload'}
+        for other in [p for p in ('exact', 'winograd', 'x3') if p != args.precision]:
+            model.set_precision(other)
+            extra['latency_b1_%s' % other] = latency_b1(model, dev)
+            model.set_precision(args.precision)
+            v2, e2, st2, p2, _ = clip_leg(model, wave, args, 1, 0, dev, other)
+            extra['value_%s' % other] = {'value': round(v2, 2), 'unit': 'clips/s', 'dtype': DTYPE[other],
+                                         'ms_per_step': round(e2 / args.steps * 1e3, 4),
+                                         'ms_per_clip_p50_device': round(p2, 4),
+                                         'roofline': roofline(st2, B, other), 'stage_ms': st2,
+                                         'note': notes[other]}
         model.set_precision(args.precision)
         cfgs = {}
         if args.model == 'gru':

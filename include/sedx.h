@@ -173,13 +173,22 @@ sedx_status sedx_forward_windows_vote(sedx_handle* h, const float* d_audio, int6
  * the AttBlock projection.
  *  SEDX_PRECISION_EXACT (default) fp32 operands, fp32 accumulation
  *                       (v_mfma_f32_32x32x2_f32 / fp32 FMA): the reference's
- *                       arithmetic (pytorch/models.py:614-615, :663-670).
+ *                       arithmetic (pytorch/models.py:614-615, :663-670),
+ *                       direct 3x3 convolution.
+ *  SEDX_PRECISION_WINOGRAD  fp32 throughout as EXACT, with the six conv
+ *                       layers of blocks 2-4 computed by Winograd F(2x2,3x3):
+ *                       input / weight / output transforms and the 16
+ *                       element-wise GEMMs all in fp32 (weights transformed
+ *                       in float64, rounded once), 2.25x fewer multiplies;
+ *                       |error| vs a float64 conv equal to or below the
+ *                       direct conv's (tools/wino_bench.cpp).  Different
+ *                       rounding from EXACT, so not bit-identical to it.
  *  SEDX_PRECISION_X3    opt-in: bf16 MFMA with a 3-term hi/lo operand split
  *                       (hi*hi + hi*lo + lo*hi, fp32 accumulate): operands
  *                       carry 16 significant bits, products err ~2^-16 rel.
  * The frontend (FFT, mel, dB), the gates, softmax and the head's
- * element-wise work are fp32 in both modes; the gammatone frontend float64. */
-typedef enum { SEDX_PRECISION_EXACT = 0, SEDX_PRECISION_X3 = 1 } sedx_precision;
+ * element-wise work are fp32 in every mode; the gammatone frontend float64. */
+typedef enum { SEDX_PRECISION_EXACT = 0, SEDX_PRECISION_X3 = 1, SEDX_PRECISION_WINOGRAD = 2 } sedx_precision;
 sedx_status sedx_set_precision(sedx_handle* h, int32_t mode);
 
 /* Implementation choices that leave the arithmetic's meaning unchanged (A/B

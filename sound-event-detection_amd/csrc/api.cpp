@@ -42,6 +42,7 @@ struct DevWeights {
   float* wp[8] = {};    // packed conv weights: block k conv j -> index 2(k-1)+(j-1); [0] unused
   float* cb[8] = {};    // folded biases
   void* wx3[8] = {};    // split bf16 hi/lo packs for conv3x3_x3 (same indices)
+  float* wu[8] = {};    // Winograd U = G g G^T packs for conv3x3_wino (same indices)
   float* w_ih = nullptr;   // [1536][512]
   float* b_ih = nullptr;   // [1536]
   float* whhT = nullptr;   // [2][256][768]
@@ -365,6 +366,8 @@ sedx_status run_body(sedx_handle* h, int64_t B, const Geometry& g, float* ws, co
     else if (x3)
       launch_conv3x3_x3(c.in, iB, c.T, c.F, c.cin, c.cout, w.wx3[c.idx], w.cb[c.idx], c.out, c.epi,
                         sched + i * CONV_SCHED_INTS, s);
+    else if (h->precision == SEDX_PRECISION_WINOGRAD)
+      launch_conv3x3_wino(c.in, iB, c.T, c.F, c.cin, c.cout, w.wu[c.idx], w.cb[c.idx], c.out, c.epi, w.zero, s);
     else
       launch_conv3x3(c.in, iB, c.T, c.F, c.cin, c.cout, w.wp[c.idx], w.cb[c.idx], c.out, c.epi, w.zero, s);
     const size_t px = c.epi == EPI_STORE ? (size_t)c.T * c.F : c.epi == EPI_POOL2 ? (size_t)(c.T / 2) * (c.F / 2)
@@ -484,7 +487,7 @@ const char* sedx_version(void) { return "sedx 0.2 (gfx950: fp32 MFMA exact + 3xb
 
 sedx_status sedx_set_precision(sedx_handle* h, int32_t mode) {
   if (!h) return SEDX_EINVAL;
-  if (mode != SEDX_PRECISION_EXACT && mode != SEDX_PRECISION_X3)
+  if (mode != SEDX_PRECISION_EXACT && mode != SEDX_PRECISION_X3 && mode != SEDX_PRECISION_WINOGRAD)
     return fail(h, SEDX_EINVAL, "unknown precision mode %d", mode);
   h->precision = mode;
   return SEDX_OK;
@@ -656,6 +659,7 @@ sedx_status sedx_finalize_weights(sedx_handle* h) {
   const int ch[5] = {1, 64, 128, 256, 512};
   std::vector<float> packed[8], cbias[8], c1w(64 * 9), c1b(64);
   std::vector<uint16_t> packed_x3[8];
+  std::vector<float> packed_wu[8];
   for (int k = 1; k <= 4; ++k)
     for (int j = 1; j <= 2; ++j) {
       const std::string p = "conv_block" + std::to_string(k);
@@ -683,6 +687,14 @@ sedx_status sedx_finalize_weights(sedx_handle* h) {
                 (float)(wt[((size_t)o * cin + i) * 9 + t] * sc[o]);
           }
       cbias[idx] = bias;
+      // Winograd pack: U = G g G^T from the float64 BN-folded weights
+      {
+        std::vector<double> wf((size_t)cout * cin * 9);
+        for (int o = 0; o < cout; ++o)
+          for (size_t k = 0; k < (size_t)cin * 9; ++k) wf[(size_t)o * cin * 9 + k] = wt[(size_t)o * cin * 9 + k] * sc[o];
+        packed_wu[idx].assign((size_t)cin * cout * 16, 0.f);
+        pack_conv_wino(wf.data(), cin, cout, packed_wu[idx].data());
+      }
       // 3xbf16 split pack: [Cout/BN][Cin/16][9][BN][4 slots x 8 bf16], slot c at c ^ ((n>>2)&3)
       {
         const int BN = (cout == 64) ? 64 : 128;
@@ -830,6 +842,7 @@ sedx_status sedx_finalize_weights(sedx_handle* h) {
     add((void**)&W.wp[i], packed[i].data(), packed[i].size() * 4);
     add((void**)&W.cb[i], cbias[i].data(), cbias[i].size() * 4);
     add((void**)&W.wx3[i], packed_x3[i].data(), packed_x3[i].size() * 2);
+    add((void**)&W.wu[i], packed_wu[i].data(), packed_wu[i].size() * 4);
   }
   if (is_gru(h)) {
     add((void**)&W.w_ih, w_ih.data(), w_ih.size() * 4);

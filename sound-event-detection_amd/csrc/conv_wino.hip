@@ -1,0 +1,488 @@
+// 3x3 conv of the 9-layer CNN (ConvBlock, pytorch/models.py:98-141) as fp32
+// Winograd F(2x2, 3x3) on v_mfma_f32_32x32x2_f32: every operand, product and
+// sum is fp32 (no narrower type anywhere), 16 multiplies per 2x2 output tile
+// instead of 36 (2.25x fewer matrix-pipe FLOPs than the direct conv.hip).
+//
+// Per output tile (2 t x 2 f) and input channel c the 4x4 input patch d
+// (rows t-1..t+2, cols f-1..f+2, zero outside the clip) is transformed to
+// V = B^T d B; the folded 3x3 weights g (BN scale applied) to U = G g G^T
+// (host, float64, rounded once to fp32); the 16 element-wise positions
+// p = 4 i + j are 16 independent GEMMs  M_p[tile][n] = sum_c V_p[tile][c] U_p[c][n]
+// and the output is Y = A^T M A, then + bias, ReLU and the block's epilogue
+// (Lavin & Gray 2016; B^T = [1 0 -1 0; 0 1 1 0; 0 -1 1 0; 0 1 0 -1],
+// G = [1 0 0; 1/2 1/2 1/2; 1/2 -1/2 1/2; 0 0 1], A^T = [1 1 1 0; 0 1 -1 -1]).
+//
+// Waves: a tile group = 32 tiles x 32 output channels, computed by a PAIR of
+// waves on one SIMD, wave half h owning the 8 positions of V rows i = 2h,
+// 2h+1 (8 MFMA accumulator tiles, 128 registers): two waves per SIMD, so one
+// wave's transform VALU, LDS reads and barrier wait run under its partner's
+// MFMAs (with all 16 positions in one wave — 256 accumulators, one wave per
+// SIMD — the matrix pipe idled through each of them: 0.60 of peak).
+// The input transform is in-lane: lane (tile m, k-half kh) reads the 3 patch
+// rows its V rows need (12 pixels, channels 2 kh and 2 kh + 1 of a 4-channel
+// chunk: 12 ds_read_b64) and its 8 transformed values per channel ARE its A
+// fragments — V never exists in LDS or HBM.  The output transform too: a
+// lane's register r holds the same (tile, channel) in all of its 8 position
+// tiles, so each wave reduces its rows to a partial 2x2 Y in registers; the
+// two halves meet once, in the epilogue, through LDS (each finishes half of
+// the registers, summing Y_0 + Y_1 in that order).
+// A workgroup is TG tile groups (2 TG waves) x 32 channels; per 4-channel
+// chunk the raw halo ([pixel][4 ch], 16 B per pixel, four parity planes) and
+// the chunk's U slab ([p][h][n][ks]) are copied global -> LDS by LDS-DMA into
+// a 3-buffer ring, NBUF - 1 chunks ahead, one counted-vmcnt barrier per chunk
+// (the exact kernel's pipeline); the next chunk's reads and transform are
+// spread between the current chunk's MFMAs.
+//
+// Workgroup -> (tile block, channel group) is XCD-aware: the channel groups
+// of one tile block are consecutive workgroups of one XCD (same halo, one
+// L2), so the halo comes from HBM once per layer.
+//
+// Every shape (TG = 4 / 2 / 1) performs the same operations in the same order
+// for each (tile, channel), so outputs do not depend on the batch size or the
+// shape chosen.
+#include "sedx_internal.h"
+
+namespace sedx {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+template <int F, int TG>
+struct WinoGeom {
+  static constexpr int WAVES = 2 * TG;
+  static constexpr int THREADS = 64 * WAVES;
+  static constexpr int P = 32 * TG;                  // tiles per workgroup
+  static constexpr int FT = F / 2;                   // tiles per tile row
+  static constexpr int TRW = P / FT;                 // tile rows per workgroup
+  static constexpr int RT = 2 * TRW + 2, CS = F + 2, KC = 4;
+  static constexpr int PL = RT * CS;                 // halo pixels
+  static constexpr int PLP = (PL + 63) / 64 * 64;    // whole 64-pixel DMA units
+  static constexpr int A_SZ = KC * PLP;              // floats: [pixel][4 ch]
+  static constexpr int W_SZ = 16 * KC * 32;          // floats: [p][h][n 32][ks]
+  static constexpr int BUF = A_SZ + W_SZ;
+  static constexpr int NBUF = 3;                     // ring depth (4 and 6 measured: no change)
+  static constexpr int UW = W_SZ / 256;              // 1-KiB DMA units per chunk
+  static constexpr int UA = PLP / 64;
+  static constexpr int U = UW + UA;
+  static constexpr int UPW = (U + WAVES - 1) / WAVES;
+  static constexpr int VM_MIN = U / WAVES;           // units of the wave with the fewest
+  static constexpr int XCH = WAVES * 8 * 4 * 64;     // floats: epilogue exchange, [wave][r 8][4][lane]
+  static constexpr int LDS_BYTES = 4 * (NBUF * BUF > XCH ? NBUF * BUF : XCH);
+  static_assert(P % FT == 0, "whole tile rows per workgroup");
+  static_assert(VM_MIN * (NBUF - 1) <= 63, "vmcnt field");
+};
+
+// raw workgroup barrier behind "this wave's DMAs older than its N youngest
+// VMEM ops landed, its LDS operations done" (__syncthreads() would drain
+// every DMA in flight); N = VM x y for y = min(younger, Y) chunks in flight
+template <int N>
+__device__ __forceinline__ void wino_bar_n() {
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+template <int VM, int Y>
+__device__ __forceinline__ void wino_bar(int younger) {
+  if constexpr (Y > 0) {
+    if (younger >= Y) {
+      wino_bar_n<VM * Y>();
+      return;
+    }
+    wino_bar<VM, Y - 1>(younger);
+  } else {
+    wino_bar_n<0>();
+  }
+}
+
+// 4-point column pass of B^T d B: (x0 - x2, x1 + x2, x2 - x1, x1 - x3)
+__device__ __forceinline__ void wino_bt4(float* x) {
+  const float e0 = x[0] - x[2], e1 = x[1] + x[2], e2 = x[2] - x[1], e3 = x[1] - x[3];
+  x[0] = e0; x[1] = e1; x[2] = e2; x[3] = e3;
+}
+
+// the kernel body for position half PH (wave-uniform; a template parameter so
+// the transform, the U rows and the patch offsets are static per wave)
+template <int F, int EPI, int TG, int PH>
+__device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, int T, int Cin, int Cout,
+                                          const float* __restrict__ U, const float* __restrict__ bias,
+                                          float* __restrict__ out, const float* __restrict__ zero16,
+                                          int tb_per_clip, int ngroups) {
+  constexpr int ph = PH;
+  using G = WinoGeom<F, TG>;
+  constexpr int WAVES = G::WAVES;
+  constexpr int CS = G::CS, KC = G::KC, FT = G::FT;
+  extern __shared__ __attribute__((aligned(16))) float smem[];   // G::LDS_BYTES (dynamic: > 64 KiB)
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tg = wv % TG;   // tile group (waves tg, tg + TG: position halves 0, 1 — one SIMD)
+  // XCD-aware decode: workgroup id -> XCD id & 7; on one XCD, tile blocks in
+  // order, each with its channel groups consecutive
+  const int id = blockIdx.x;
+  const int xcd = id & 7, j = id >> 3;
+  const int jb = j / ngroups;
+  const int tb = jb * 8 + xcd;
+  const int ng = j - jb * ngroups;
+  if (tb >= B * tb_per_clip) return;   // padding of the tile blocks to a multiple of 8 (uniform)
+  const int b = tb / tb_per_clip;
+  const int tr0 = (tb - b * tb_per_clip) * G::TRW;   // first tile row
+  const int t0 = 2 * tr0;
+  const int n0 = ng * 32;
+  const int khalf = lane >> 5;
+
+  // A side: this lane's tile (lane & 31) and channel pair (2 khalf, 2 khalf + 1).
+  // Halo image in LDS: 16 B per pixel ([4 ch]) in four parity planes, slot
+  // (r, c) -> ((r & 1) 2 + (c & 1)) Q + (r >> 1) HC + (c >> 1): a patch pixel
+  // (2 tr + i, 2 tf + j) of the 32 tiles of a wave is then one plane at
+  // consecutive slots along tf, so a fragment read spreads over all banks
+  // (row-major pixels put the tiles 8 floats apart: 4-way conflicts)
+  constexpr int HC = CS / 2, Q = G::PL / 4;
+  const int pt = 32 * tg + (lane & 31);
+  const int a_base = ((pt / FT) * HC + (pt % FT)) * KC + 2 * khalf;
+  auto a_off = [&](int i, int jj) { return ((((i & 1) << 1) | (jj & 1)) * Q + (i >> 1) * HC + (jj >> 1)) * KC; };
+  // B side: U slab [p][h][n][ks], lane (h = khalf, n = lane & 31), this
+  // wave's positions 8 ph .. 8 ph + 7
+  const int b_base = G::A_SZ + 8 * ph * 128 + khalf * 64 + 2 * (lane & 31);
+
+  // ---- LDS-DMA units of this wave (unit u -> wave u % WAVES) ----
+  const float* dsrc[G::UPW];
+  int64_t dstep[G::UPW];
+  int dlds[G::UPW];
+#pragma unroll
+  for (int k = 0; k < G::UPW; ++k) {
+    const int u = wv + WAVES * k;
+    dsrc[k] = zero16;
+    dstep[k] = 0;
+    dlds[k] = 0;
+    if (u < G::UW) {
+      const int row = 4 * u + (lane >> 4);   // (p, h) row of 2 x 32 floats
+      dsrc[k] = U + (int64_t)row * 2 * Cout + 2 * n0 + 4 * (lane & 15);
+      dstep[k] = (int64_t)32 * 2 * Cout;
+      dlds[k] = G::A_SZ + 256 * u;
+    } else if (u < G::U) {
+      const int slot = 64 * (u - G::UW) + lane;
+      const int q = slot / Q, rem = slot - q * Q;
+      const int r = 2 * (rem / HC) + (q >> 1), c = 2 * (rem % HC) + (q & 1);
+      const int t = t0 - 1 + r, f = c - 1;
+      if (slot < G::PL && t >= 0 && t < T && f >= 0 && f < F) {
+        dsrc[k] = in + (((int64_t)b * T + t) * F + f) * Cin;
+        dstep[k] = KC;
+      }
+      dlds[k] = 256 * (u - G::UW);
+    }
+  }
+#define SEDX_WG_DMA(chunk_, buf_)                                                                      \
+  {                                                                                                    \
+    _Pragma("unroll") for (int k = 0; k < G::UPW; ++k) {                                               \
+      if (wv + WAVES * k < G::U) {                                                                     \
+        const uint32_t m0_ = (uint32_t)(size_t)(__attribute__((address_space(3))) float*)(             \
+            smem + (buf_) * G::BUF + dlds[k]);                                                         \
+        sedx_glds16(dsrc[k] + (int64_t)(chunk_) * dstep[k], __builtin_amdgcn_readfirstlane(m0_));      \
+      }                                                                                                \
+    }                                                                                                  \
+    asm volatile("" ::: "memory");                                                                     \
+  }
+
+  f32x16 acc[8];
+#pragma unroll
+  for (int p = 0; p < 8; ++p)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[p][r] = 0.0f;
+
+  // a chunk's operands in registers: V of this wave's 8 positions (both
+  // k-steps) and the U fragments; two sets, ping-pong
+  float va[2][8], vb[2][8];
+  float2 ua[8], ubv[8];
+  // read chunk's patch rows + U fragments from LDS buffer buf (issue only)
+  auto issue_reads = [&](int buf, float2 (&pd)[3][4], float2 (&un)[8]) {
+    const float* sm = smem + buf * G::BUF;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj)
+        pd[i][jj] = *reinterpret_cast<const float2*>(sm + a_base + a_off(ph + i, jj));
+#pragma unroll
+    for (int p = 0; p < 8; ++p) un[p] = *reinterpret_cast<const float2*>(sm + b_base + p * 128);
+  };
+  // V rows 2 ph, 2 ph + 1 of B^T d B from patch rows ph .. ph + 2
+  //   ph 0: d0 - d2, d1 + d2      ph 1: d2 - d1, d1 - d3
+  auto transform = [&](const float2 (&pd)[3][4], float (&vn)[2][8]) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      float x[3][4];
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) x[i][jj] = ks ? pd[i][jj].y : pd[i][jj].x;
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        if constexpr (PH == 0) {
+          vn[ks][jj] = x[0][jj] - x[2][jj];
+          vn[ks][4 + jj] = x[1][jj] + x[2][jj];
+        } else {
+          vn[ks][jj] = x[1][jj] - x[0][jj];
+          vn[ks][4 + jj] = x[0][jj] - x[2][jj];
+        }
+      }
+      wino_bt4(&vn[ks][0]);
+      wino_bt4(&vn[ks][4]);
+    }
+    // pin V here: otherwise the compiler sinks each value's transform to the
+    // MFMA that consumes it (next chunk), a VALU -> MFMA chain in front of
+    // every matrix instruction
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) asm volatile("" : "+v"(vn[ks][q]));
+  };
+  // the 16 MFMAs of one chunk from (vc, uc) — k-step 0 (channel 2 khalf) then
+  // k-step 1 (2 khalf + 1) — with the next chunk's LDS reads spread over the
+  // first 8 and its transform over the last 8.  (Keeping the two k-steps of
+  // an accumulator apart with a scheduling barrier measured 6 % slower.)
+  auto step = [&](const float (&vc)[2][8], const float2 (&uc)[8], int nbuf, float (&vn)[2][8], float2 (&un)[8]) {
+#pragma unroll
+    for (int p = 0; p < 8; ++p) acc[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(vc[0][p], uc[p].x, acc[p], 0, 0, 0);
+#pragma unroll
+    for (int p = 0; p < 8; ++p) acc[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(vc[1][p], uc[p].y, acc[p], 0, 0, 0);
+    float2 pd[3][4];
+    issue_reads(nbuf, pd, un);
+    transform(pd, vn);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // 2 LDS reads
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
+      __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);   // 5 VALU
+    }
+  };
+
+  const int nchunks = Cin / KC;   // even (Cin % 8 == 0, checked by the launcher)
+  constexpr int NB = G::NBUF;
+#pragma unroll
+  for (int c = 0; c < NB; ++c)
+    if (c < nchunks) SEDX_WG_DMA(c, c);
+  // chunk 0 landed: younger chunks 1 .. NB - 1 may be in flight
+  wino_bar<G::VM_MIN, NB - 1>(min(NB - 1, nchunks - 1));
+  {
+    float2 pd[3][4];
+    issue_reads(0, pd, ua);
+    transform(pd, va);
+  }
+
+  // top of chunk c: chunk c + 1 landed (c + 2 .. c + NB - 1 may be in
+  // flight) and every wave has consumed chunk c's buffer (its reads were
+  // waited for in the previous step), which then receives chunk c + NB.  On
+  // the last chunk the step's reads of the "next" buffer are unused.
+  int buf = 0;
+  for (int chunk = 0; chunk < nchunks; chunk += 2) {
+    const int b1 = buf == NB - 1 ? 0 : buf + 1, b2 = b1 == NB - 1 ? 0 : b1 + 1;
+    wino_bar<G::VM_MIN, NB - 2>(max(0, min(NB - 2, nchunks - chunk - 2)));
+    if (chunk + NB < nchunks) SEDX_WG_DMA(chunk + NB, buf);
+    step(va, ua, b1, vb, ubv);
+    wino_bar<G::VM_MIN, NB - 2>(max(0, min(NB - 2, nchunks - chunk - 3)));
+    if (chunk + 1 + NB < nchunks) SEDX_WG_DMA(chunk + 1 + NB, b1);
+    step(vb, ubv, b2, va, ua);
+    buf = b2;
+  }
+#undef SEDX_WG_DMA
+
+  // ---- epilogue.  Register r of every position tile = MFMA row
+  // m = (r & 3) + 8 (r >> 2) + 4 khalf (tile 32 tg + m), column lane & 31.
+  // Each wave reduces its V rows i to a partial Y = A^T M A: with
+  // T_a[j] = sum_i A^T[a][i] M[i][j] over its rows (ph 0: T_0 = m0 + m1,
+  // T_1 = m1; ph 1: T_0 = m2, T_1 = -m2 - m3), Y[a] = (T_a0 + T_a1 + T_a2,
+  // T_a1 - T_a2 - T_a3).  Wave half h finishes registers 8 h .. 8 h + 7:
+  // it hands its partial of the other half's registers over through LDS
+  // and sums Y_0 + Y_1 (in that order) for its own. ----
+  auto partial = [&](int r, float y[4]) {
+    float t[2][4];
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const float m0 = acc[jj][r], m1 = acc[4 + jj][r];
+      if constexpr (PH == 0) {
+        t[0][jj] = m0 + m1;
+        t[1][jj] = m1;
+      } else {
+        t[0][jj] = m0;
+        t[1][jj] = -m0 - m1;
+      }
+    }
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      y[2 * a] = (t[a][0] + t[a][1]) + t[a][2];
+      y[2 * a + 1] = (t[a][1] - t[a][2]) - t[a][3];
+    }
+  };
+  wino_bar_n<0>();   // every wave's last fragment reads done: the ring is free
+  float* xo = smem + wv * (8 * 4 * 64);   // this wave's exchange slots [r 8][4][lane]
+  const int ro = 8 * (1 - ph);            // registers the partner finishes
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    float y[4];
+    partial(ro + k, y);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) xo[(k * 4 + e) * 64 + lane] = y[e];
+  }
+  __syncthreads();
+  const float* xi = smem + (tg + TG * (1 - ph)) * (8 * 4 * 64);   // the partner's slots
+  const int n = n0 + (lane & 31);
+  const float bv = bias[n];
+  // full Y of register 8 ph + k (+ bias, ReLU), as y[a][b]
+  auto outtile = [&](int k, float y[2][2]) {
+    float mine[4];
+    partial(8 * ph + k, mine);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float other = xi[(k * 4 + e) * 64 + lane];
+      const float s = PH == 0 ? mine[e] + other : other + mine[e];
+      y[e >> 1][e & 1] = fmaxf(s + bv, 0.0f);
+    }
+  };
+  if constexpr (EPI == EPI_FMEAN) {
+    // F = 8: registers 4q .. 4q + 3 are the 4 tiles (bins 0-7) of tile row
+    // 8 tg + 2 q + khalf; torch.mean over the 8 bins
+    static_assert(F == 8, "freq-mean epilogue: F = 8");
+#pragma unroll
+    for (int qq = 0; qq < 2; ++qq) {
+      const int q = 2 * ph + qq;
+      float y[4][2][2];
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) outtile(4 * qq + jj, y[jj]);
+      const int trl = 8 * tg + 2 * q + khalf;
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+        float sum = 0.0f;
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) sum = (sum + y[jj][a][0]) + y[jj][a][1];
+        const int t = t0 + 2 * trl + a;
+        if (t < T) out[((int64_t)b * T + t) * Cout + n] = sum * (1.0f / F);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int r = 8 * ph + k;
+      const int m = (r & 3) + 8 * (r >> 2) + 4 * khalf;
+      const int ptile = 32 * tg + m;
+      const int trl = ptile / FT, tf = ptile % FT;
+      float y[2][2];
+      outtile(k, y);
+      if constexpr (EPI == EPI_POOL2) {
+        const int To = T / 2;
+        const int to = tr0 + trl;
+        const float pv = (((y[0][0] + y[0][1]) + y[1][0]) + y[1][1]) * 0.25f;
+        if (to < To) out[(((int64_t)b * To + to) * (F / 2) + tf) * Cout + n] = pv;
+      } else {
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+          const int t = t0 + 2 * trl + a;
+          if (t < T) {
+            float* o = out + (((int64_t)b * T + t) * F + 2 * tf) * Cout + n;
+            o[0] = y[a][0];
+            o[Cout] = y[a][1];
+          }
+        }
+      }
+    }
+  }
+}
+
+template <int F, int EPI, int TG>
+__global__ __launch_bounds__(128 * TG, TG == 4 ? 1 : 2) void conv3x3_wino_kernel(
+    const float* __restrict__ in, int B, int T, int Cin, int Cout, const float* __restrict__ U,
+    const float* __restrict__ bias, float* __restrict__ out, const float* __restrict__ zero16, int tb_per_clip,
+    int ngroups) {
+  if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) < TG)
+    wino_body<F, EPI, TG, 0>(in, B, T, Cin, Cout, U, bias, out, zero16, tb_per_clip, ngroups);
+  else
+    wino_body<F, EPI, TG, 1>(in, B, T, Cin, Cout, U, bias, out, zero16, tb_per_clip, ngroups);
+}
+
+template <int F, int TG>
+static void launch_wino_w(const float* in, int B, int T, int Cin, int Cout, const float* U, const float* bias,
+                          float* out, int epi, const float* zero16, hipStream_t s) {
+  using G = WinoGeom<F, TG>;
+  // tile rows of a clip: POOL2 drops an odd last row (floor), the others keep it
+  const int trows = epi == EPI_POOL2 ? T / 2 : (T + 1) / 2;
+  const int tb_per_clip = (trows + G::TRW - 1) / G::TRW;
+  const int ngroups = Cout / 32;
+  const int64_t tblocks = (int64_t)B * tb_per_clip;
+  const int64_t nwg = (tblocks + 7) / 8 * 8 * ngroups;
+  if (nwg > INT32_MAX || tblocks <= 0) return note_launch_error(hipErrorInvalidValue);
+  dim3 grid((unsigned)nwg);
+#define SEDX_WG_LAUNCH(E)                                                                              \
+  {                                                                                                    \
+    auto* k_ = conv3x3_wino_kernel<F, E, TG>;                                                          \
+    if (!launch_info(reinterpret_cast<const void*>(k_), G::THREADS, G::LDS_BYTES).ok) return;          \
+    hipLaunchKernelGGL(k_, grid, dim3(G::THREADS), G::LDS_BYTES, s, in, B, T, Cin, Cout, U, bias, out, zero16, \
+                       tb_per_clip, ngroups);                                                          \
+    return;                                                                                            \
+  }
+  if constexpr (F == 8) {
+    if (epi == EPI_STORE) SEDX_WG_LAUNCH(EPI_STORE);
+    if (epi == EPI_FMEAN) SEDX_WG_LAUNCH(EPI_FMEAN);
+  } else {
+    if (epi == EPI_STORE) SEDX_WG_LAUNCH(EPI_STORE);
+    if (epi == EPI_POOL2) SEDX_WG_LAUNCH(EPI_POOL2);
+  }
+#undef SEDX_WG_LAUNCH
+  note_launch_error(hipErrorInvalidValue);
+}
+
+static int wino_device_cus() {
+  int dev = 0, ncu = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  return ncu;
+}
+
+// 4 tile groups (128 tiles) when that gives every CU a workgroup, else 2,
+// else 1: the same per-wave work, bit-identical outputs
+template <int F>
+static void launch_wino_f(const float* in, int B, int T, int Cin, int Cout, const float* U, const float* bias,
+                          float* out, int epi, const float* zero16, hipStream_t s) {
+  const int64_t ncu = wino_device_cus();
+  const int trows = epi == EPI_POOL2 ? T / 2 : (T + 1) / 2;
+  auto wgs = [&](int trw) { return (int64_t)B * ((trows + trw - 1) / trw) * (Cout / 32); };
+  if (wgs(WinoGeom<F, 4>::TRW) >= ncu)
+    launch_wino_w<F, 4>(in, B, T, Cin, Cout, U, bias, out, epi, zero16, s);
+  else if (wgs(WinoGeom<F, 2>::TRW) >= ncu)
+    launch_wino_w<F, 2>(in, B, T, Cin, Cout, U, bias, out, epi, zero16, s);
+  else
+    launch_wino_w<F, 1>(in, B, T, Cin, Cout, U, bias, out, epi, zero16, s);
+}
+
+void launch_conv3x3_wino(const float* in, int B, int T, int F, int Cin, int Cout, const float* U,
+                         const float* bias, float* out, int epi, const float* zero16, hipStream_t s) {
+  if (Cin % 8 != 0 || Cout % 32 != 0 || B <= 0 || T <= 0) return note_launch_error(hipErrorInvalidValue);
+  switch (F) {
+    case 32: launch_wino_f<32>(in, B, T, Cin, Cout, U, bias, out, epi, zero16, s); break;
+    case 16: launch_wino_f<16>(in, B, T, Cin, Cout, U, bias, out, epi, zero16, s); break;
+    case 8: launch_wino_f<8>(in, B, T, Cin, Cout, U, bias, out, epi, zero16, s); break;
+    default: note_launch_error(hipErrorInvalidValue); break;
+  }
+}
+
+// U = G g G^T per (input channel, output channel) in float64 from the
+// BN-folded weights, rounded once to fp32, packed [Cin/4][16 p][2 h][Cout][2 ks]
+// with channel 4 chunk + 2 h + ks (one 8-byte LDS read gives a lane both
+// k-steps of a position).
+void pack_conv_wino(const double* wf, int Cin, int Cout, float* Up) {
+  static const double Gm[4][3] = {{1, 0, 0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0, 0, 1}};
+  for (int o = 0; o < Cout; ++o)
+    for (int i = 0; i < Cin; ++i) {
+      const double* g = wf + ((size_t)o * Cin + i) * 9;
+      double tmp[4][3];
+      for (int a = 0; a < 4; ++a)
+        for (int y = 0; y < 3; ++y) tmp[a][y] = Gm[a][0] * g[0 * 3 + y] + Gm[a][1] * g[1 * 3 + y] + Gm[a][2] * g[2 * 3 + y];
+      const int chunk = i / 4, h = (i % 4) >> 1, ks = i & 1;
+      for (int a = 0; a < 4; ++a)
+        for (int c = 0; c < 4; ++c) {
+          const double u = tmp[a][0] * Gm[c][0] + tmp[a][1] * Gm[c][1] + tmp[a][2] * Gm[c][2];
+          const int p = 4 * a + c;
+          Up[((((size_t)chunk * 16 + p) * 2 + h) * Cout + o) * 2 + ks] = (float)u;
+        }
+    }
+}
+
+}  // namespace sedx

@@ -94,6 +94,14 @@ void launch_conv3x3(const float* in, int B, int T, int F, int Cin, int Cout,
                     const float* wp, const float* bias, float* out, int epi,
                     const float* zero16, hipStream_t s);
 
+// Same contract as fp32 Winograd F(2x2, 3x3) (conv_wino.hip): U from
+// pack_conv_wino (wf = BN-folded weights [Cout][Cin][9] in float64);
+// F in {32, 16, 8}, Cout % 32 == 0.
+void launch_conv3x3_wino(const float* in, int B, int T, int F, int Cin, int Cout,
+                         const float* U, const float* bias, float* out, int epi,
+                         const float* zero16, hipStream_t s);
+void pack_conv_wino(const double* wf, int Cin, int Cout, float* U);   // U: Cin * Cout * 16 floats
+
 // Same contract on bf16 MFMA with a 3-term hi/lo split (fp32-class accuracy).
 // wp = host-packed split weights [Cout/BN][Cin/16][9][BN][4 x 16 B] (BN = 64 if
 // Cout == 64 else 128), slots XOR-swizzled by ((n >> 2) & 3).

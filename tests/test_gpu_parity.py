@@ -47,8 +47,9 @@ def err(a, b):
     return float(np.max(np.abs(a - b)))
 
 
-@pytest.fixture(scope='module', params=[(GRU, 'exact'), (TRF, 'exact'), (GRU, 'x3'), (TRF, 'x3')],
-                ids=['gru-exact', 'trf-exact', 'gru-x3', 'trf-x3'])
+@pytest.fixture(scope='module', params=[(GRU, 'exact'), (TRF, 'exact'), (GRU, 'x3'), (TRF, 'x3'),
+                                        (GRU, 'winograd'), (TRF, 'winograd')],
+                ids=['gru-exact', 'trf-exact', 'gru-x3', 'trf-x3', 'gru-wino', 'trf-wino'])
 def model(request):
     mt, prec = request.param
     return mt, build(mt).set_precision(prec)
@@ -211,7 +212,8 @@ def test_gru_exact_recurrence_is_fp32():
         assert e_cs <= 2e-6 and e_ref <= 1e-5
 
 
-@pytest.mark.parametrize('prec,seconds', [('exact', 10.0), ('x3', 10.0), ('exact', 7.33)])
+@pytest.mark.parametrize('prec,seconds', [('exact', 10.0), ('x3', 10.0), ('exact', 7.33), ('winograd', 10.0),
+                                          ('winograd', 7.33)])
 def test_small_batch_shapes_bit_identical(prec, seconds):
     """Small batches run other kernel shapes — 32x32-wave-tile convs, the
     barrier-free small-M linear, and (exact) the VALU fma-chain GRU product for
@@ -427,7 +429,7 @@ def ctypes_ptr(t):
     return ctypes.c_void_p(t.data_ptr())
 
 
-@pytest.mark.parametrize('prec', ['exact', 'x3'])
+@pytest.mark.parametrize('prec', ['exact', 'x3', 'winograd'])
 @pytest.mark.parametrize('mt', [GRU, TRF])
 def test_stage_goldens(mt, prec, golden_dir):
     """Every stage of the HIP path against the reference's own per-stage
@@ -452,6 +454,27 @@ def test_stage_goldens(mt, prec, golden_dir):
         e = err(got, ref)
         print(mt, prec, 'stage', stage, shape, 'max|d| = %.3g (scale %.3g)' % (e, scale))
         assert e <= 1e-4 * scale, (stage, e)
+
+
+@pytest.mark.parametrize('mt', [GRU, TRF])
+def test_winograd_vs_exact(mt):
+    """fp32 Winograd F(2x2,3x3) conv (blocks 2-4) against the direct fp32 conv
+    on the headline batch: same arithmetic type, different rounding — the two
+    agree far inside the 1e-3 bar, the thresholded events are identical, and
+    both sit at the same distance from the oracle."""
+    from sedx import inference
+    wave = synth.make_waveforms(32, seconds=10.0, sample_rate=16000, seed=4321)
+    ex = run(build(mt).set_precision('exact'), wave)
+    wg = run(build(mt).set_precision('winograd'), wave)
+    ref = O.forward(O.full_state(synth.make_state_dict(mt, seed=SEEDS[mt])), mt, wave=wave)
+    e_we = err(wg['framewise_output'], ex['framewise_output'])
+    e_w = err(wg['framewise_output'], ref['framewise_output'].numpy())
+    e_e = err(ex['framewise_output'], ref['framewise_output'].numpy())
+    print(mt, 'winograd vs exact %.3g, vs oracle %.3g (exact vs oracle %.3g)' % (e_we, e_w, e_e))
+    assert e_we <= 2e-5 and e_w <= 2e-5
+    params = {'sed_high_threshold': 0.5, 'sed_low_threshold': 0.3, 'n_smooth': 10, 'n_salt': 10}
+    ev = inference.events_from_framewise(wg['framewise_output'], params)
+    assert len(ev) > 0 and ev == inference.events_from_framewise(ex['framewise_output'], params)
 
 
 def test_config5_transformer_b256():
