@@ -9,7 +9,8 @@ C=sound-event-detection_amd/csrc
 O=tools/prev
 if [ -n "$BUILD" ]; then
   $HIPCC -o $O/wb_full tools/wino_bench.cpp $C/conv.hip $C/conv_wino.hip || exit 1
-  for a in $ABLS; do $HIPCC -DSEDX_WABL_$a -o $O/wb_$a tools/wino_bench.cpp $C/conv.hip $C/conv_wino.hip || exit 1; done
+  # VARIANT_FLAGS: "name:-DFLAG=1,-DOTHER name2:..." extra builds
+  for vf in $VARIANT_FLAGS; do n=${vf%%:*}; f=${vf#*:}; $HIPCC ${f//,/ } -o $O/wb_$n tools/wino_bench.cpp $C/conv.hip $C/conv_wino.hip || exit 1; done
   for nb in $NBUFS; do $HIPCC -DSEDX_WINO_NBUF=$nb -o $O/wb_nb$nb tools/wino_bench.cpp $C/conv.hip $C/conv_wino.hip || exit 1; done
 fi
 [ -n "$RUN" ] || exit 0

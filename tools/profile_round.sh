@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU-box profiling sequence for one round: full bench (with CPU baseline),
-# then for each arithmetic (exact = the headline, x3 = the opt-in leg):
+# then for each arithmetic (winograd = the headline, exact, x3 = the opt-in leg):
 # rocprofv3 kernel-trace stats -> FETCH_SIZE pass -> WRITE_SIZE pass
 # (separate passes: FETCH_SIZE and WRITE_SIZE do not fit one TCC pass on
 # gfx950) -> MFMA busy cycles + GRBM_GUI_ACTIVE pass (MFMA utilisation,
@@ -19,7 +19,7 @@ step() {
   if [ $rc -ne 0 ]; then echo "stopping"; exit $rc; fi
 }
 [ -n "$NO_FULL" ] || step bench_full 600 python bench.py --steps 20 --warmup 3
-for P in ${PRECISIONS:-exact x3}; do
+for P in ${PRECISIONS:-winograd exact x3}; do
   A="--no-cpu-baseline --no-side --streams 1 --precision $P"
   step kt_$P 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/$P/kt -o kt -- python bench.py --steps 10 --warmup 2 $A
   step fetch_$P 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/$P/pmc_fetch -o pmc -- python bench.py --steps 3 --warmup 1 $A
