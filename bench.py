@@ -507,6 +507,8 @@ def main():
                     help='headline only (no x3 / config 3 / config 4 / window legs, no latency_b1): '
                          'profiling passes use it so per-kernel rocprof averages cover only the headline')
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
+    ap.add_argument('--wino-block1', type=int, choices=[0, 1], default=1,
+                    help='winograd precision: block 1 as Winograd too (1, default) or direct fused (0)')
     args = ap.parse_args()
 
     world, rank, local = distributed.init()
@@ -516,6 +518,7 @@ def main():
     torch.cuda.set_device(dev)
     name = MODEL_NAMES[args.model]
     model = build_model(name, dev)
+    model.set_tuning(_lib.TUNE_WINO_BLOCK1, args.wino_block1)
     B = args.batch
     wave = torch.from_numpy(synth.make_waveforms(B, 10.0, 16000, seed=1234 + rank)).to(dev)
 

@@ -201,8 +201,12 @@ sedx_status sedx_set_precision(sedx_handle* h, int32_t mode);
  *  SEDX_TUNE_GRU_HANDOFF  SEDX_GRU_HANDOFF_AUTO (default): XCD-local hand-off
  *                         when all 8 slices share an XCD, else global;
  *                         SEDX_GRU_HANDOFF_GLOBAL: always the global protocol
- *                         (same bytes, bit-identical results). */
-typedef enum { SEDX_TUNE_GRU_KERNEL = 0, SEDX_TUNE_GRU_HANDOFF = 1 } sedx_tuning_knob;
+ *                         (same bytes, bit-identical results).
+ *  SEDX_TUNE_WINO_BLOCK1  (SEDX_PRECISION_WINOGRAD only) 1 (default): block 1's
+ *                         conv2 as Winograd F(2x2,3x3) too, fed by a separate
+ *                         conv1 launch (the 64-channel activation goes through
+ *                         HBM); 0: block 1 as the direct fused fp32 kernel. */
+typedef enum { SEDX_TUNE_GRU_KERNEL = 0, SEDX_TUNE_GRU_HANDOFF = 1, SEDX_TUNE_WINO_BLOCK1 = 2 } sedx_tuning_knob;
 enum { SEDX_GRU_KERNEL_COOP = 0, SEDX_GRU_KERNEL_SIMPLE = 1 };
 enum { SEDX_GRU_HANDOFF_AUTO = 0, SEDX_GRU_HANDOFF_GLOBAL = 1 };
 sedx_status sedx_set_tuning(sedx_handle* h, int32_t knob, int32_t value);

@@ -30,6 +30,8 @@ struct DevWeights {
   float2* twiddle = nullptr;
   float* window = nullptr;
   float* mel_w = nullptr;
+  float* mel_tab = nullptr;   // logmel512_kernel's per-(slot, lane) band weights
+  int32_t mel_wmax = 0;
   int32_t* mel_off = nullptr;
   int32_t* mel_lo = nullptr;
   float* bn0_scale = nullptr;
@@ -85,6 +87,7 @@ struct sedx_handle {
   int precision = SEDX_PRECISION_EXACT;   // GEMM arithmetic (sedx_set_precision)
   int gru_kernel = SEDX_GRU_KERNEL_COOP;   // sedx_set_tuning
   int gru_handoff = SEDX_GRU_HANDOFF_AUTO;
+  int wino_block1 = 1;                     // SEDX_TUNE_WINO_BLOCK1
   // sedx_set_capture: copy one stage's output of every later forward
   int cap_stage = -1;
   float* cap_buf = nullptr;
@@ -277,6 +280,8 @@ struct WsLayout {
 
 size_t align_up(size_t x) { return (x + 63) & ~size_t(63); }
 
+bool wino_block1_on(const sedx_handle* h) { return h->precision == SEDX_PRECISION_WINOGRAD && h->wino_block1; }
+
 WsLayout ws_layout(const sedx_handle* h, int64_t B, const Geometry& g) {
   WsLayout l;
   size_t off = 0;
@@ -286,6 +291,7 @@ WsLayout ws_layout(const sedx_handle* h, int64_t B, const Geometry& g) {
   // modes: conv1's 64-channel activation never exists), then the conv1
   // outputs of blocks 2-4, then the head scratch
   size_t a = block1_pad_floats((int)B, (int)g.T);
+  if (wino_block1_on(h)) a = std::max(a, (size_t)B * g.T * 64 * 64);   // conv1's activation
   a = std::max(a, (size_t)B * g.T1 * 32 * 128);
   a = std::max(a, (size_t)B * g.T2 * 16 * 256);
   a = std::max(a, (size_t)B * g.T3 * 8 * 512);
@@ -342,7 +348,11 @@ sedx_status run_body(sedx_handle* h, int64_t B, const Geometry& g, float* ws, co
   // block 1 as one launch in both modes: conv1 computed inside conv2's halo
   // staging (the b1c1 stage is just the zero-bordered copy of the bn0 output)
   if (x3) HIP_TRY(h, hipMemsetAsync(sched, 0, 7 * CONV_SCHED_INTS * sizeof(int), s));
-  launch_pad_x0(X0, iB, (int)g.T, A, s);
+  const bool wb1 = wino_block1_on(h);
+  if (wb1)   // Winograd block 1: conv1's activation [B][T][64][64] into A
+    launch_conv1_nhwc(X0, iB, (int)g.T, w.c1_w, w.c1_b, A, s);
+  else
+    launch_pad_x0(X0, iB, (int)g.T, A, s);
   struct L {
     const float* in;
     int T, F, cin, cout, idx, epi;
@@ -361,6 +371,8 @@ sedx_status run_body(sedx_handle* h, int64_t B, const Geometry& g, float* ws, co
     if (x3 && i == 0)
       launch_block1_fused_x3(nullptr, iB, c.T, A, w.c1_wt, w.c1_b, w.wx3[c.idx], w.cb[c.idx], c.out,
                              sched, s);
+    else if (i == 0 && wb1)
+      launch_conv3x3_wino(A, iB, c.T, 64, 64, 64, w.wu[c.idx], w.cb[c.idx], c.out, EPI_POOL2, w.zero, s);
     else if (i == 0)
       launch_block1_exact(A, iB, c.T, w.c1_w, w.c1_b, w.wp[c.idx], w.cb[c.idx], c.out, w.zero, s);
     else if (x3)
@@ -521,6 +533,10 @@ sedx_status sedx_set_tuning(sedx_handle* h, int32_t knob, int32_t value) {
       if (value != SEDX_GRU_HANDOFF_AUTO && value != SEDX_GRU_HANDOFF_GLOBAL) break;
       h->gru_handoff = value;
       return SEDX_OK;
+    case SEDX_TUNE_WINO_BLOCK1:
+      if (value != 0 && value != 1) break;
+      h->wino_block1 = value;
+      return SEDX_OK;
     default:
       return fail(h, SEDX_EINVAL, "unknown tuning knob %d", (int)knob);
   }
@@ -631,6 +647,18 @@ sedx_status sedx_finalize_weights(sedx_handle* h) {
       for (int k = lo; k <= hi; ++k) mel_w.push_back(melW[(size_t)k * 64 + m]);
   }
   mel_off[64] = (int32_t)mel_w.size();
+  // the n_fft 512 kernel's band table: slot q of lane b is band
+  // fe16_band_host(b, q), zero-padded to FE16_MEL_MW bins
+  std::vector<float> mel_tab((size_t)4 * 16 * FE16_MEL_MW, 0.f);
+  int32_t mel_wmax = 0;
+  for (int m = 0; m < 64; ++m) mel_wmax = std::max(mel_wmax, mel_off[m + 1] - mel_off[m]);
+  mel_wmax = (mel_wmax + 3) & ~3;
+  for (int q = 0; q < 4; ++q)
+    for (int b = 0; b < 16; ++b) {
+      const int m = fe16_band_host(b, q), wd = mel_off[m + 1] - mel_off[m];
+      for (int e = 0; e < std::min(wd, FE16_MEL_MW); ++e)
+        mel_tab[((size_t)q * 16 + b) * FE16_MEL_MW + e] = mel_w[mel_off[m] + e];
+    }
   if (mel_w.empty()) mel_w.push_back(0.f);
 
   auto bn_fold = [&](const std::string& p, int n, std::vector<double>& sc, std::vector<float>& mu,
@@ -825,6 +853,8 @@ sedx_status sedx_finalize_weights(sedx_handle* h) {
   add((void**)&W.twiddle, tw.data(), tw.size() * 4);
   add((void**)&W.window, window.data(), window.size() * 4);
   add((void**)&W.mel_w, mel_w.data(), mel_w.size() * 4);
+  add((void**)&W.mel_tab, mel_tab.data(), mel_tab.size() * 4);
+  W.mel_wmax = mel_wmax;
   add((void**)&W.mel_off, mel_off.data(), mel_off.size() * 4);
   add((void**)&W.mel_lo, mel_lo.data(), mel_lo.size() * 4);
   add((void**)&W.bn0_scale, sc0f.data(), 64 * 4);
@@ -1006,6 +1036,8 @@ static sedx_status forward_wave(sedx_handle* h, const float* d_wave, const int16
   p.twiddle = h->w.twiddle;
   p.window = h->w.window;
   p.mel_w = h->w.mel_w;
+  p.mel_tab = h->w.mel_tab;
+  p.mel_wmax = h->w.mel_wmax;
   p.mel_off = h->w.mel_off;
   p.mel_lo = h->w.mel_lo;
   p.bn_scale = h->w.bn0_scale;
@@ -1170,6 +1202,8 @@ static sedx_status forward_windows_impl(sedx_handle* h, const float* d_audio, in
   p.twiddle = h->w.twiddle;
   p.window = h->w.window;
   p.mel_w = h->w.mel_w;
+  p.mel_tab = h->w.mel_tab;
+  p.mel_wmax = h->w.mel_wmax;
   p.mel_off = h->w.mel_off;
   p.mel_lo = h->w.mel_lo;
   p.bn_scale = h->w.bn0_scale;

@@ -456,11 +456,75 @@ void launch_conv3x3_wino(const float* in, int B, int T, int F, int Cin, int Cout
                          const float* bias, float* out, int epi, const float* zero16, hipStream_t s) {
   if (Cin % 8 != 0 || Cout % 32 != 0 || B <= 0 || T <= 0) return note_launch_error(hipErrorInvalidValue);
   switch (F) {
+    case 64: launch_wino_f<64>(in, B, T, Cin, Cout, U, bias, out, epi, zero16, s); break;
     case 32: launch_wino_f<32>(in, B, T, Cin, Cout, U, bias, out, epi, zero16, s); break;
     case 16: launch_wino_f<16>(in, B, T, Cin, Cout, U, bias, out, epi, zero16, s); break;
     case 8: launch_wino_f<8>(in, B, T, Cin, Cout, U, bias, out, epi, zero16, s); break;
     default: note_launch_error(hipErrorInvalidValue); break;
   }
+}
+
+// Block 1's conv1 (Cin = 1, BN folded, ReLU) as its own launch for the
+// Winograd block 1: X0 [B][T][64 bins] -> [B][T][64 bins][64 ch] NHWC, the
+// conv2 input.  A workgroup writes C1_ROWS whole t-rows of one clip (16 KB
+// each, contiguous): the X0 rows it needs (zero-bordered) and the weights
+// sit in LDS, a thread owns one pixel x 4 channels per step (one 16-byte
+// store; 16 consecutive threads write a pixel's 256 bytes).  Per channel the
+// 9 taps are one fma chain in tap order from 0, then + bias and ReLU — the
+// operation order of the direct kernel's fused conv1.
+constexpr int C1_ROWS = 4;
+__global__ __launch_bounds__(256) void conv1_nhwc_kernel(const float* __restrict__ x0, int T, int rb_per_clip,
+                                                         const float* __restrict__ w1, const float* __restrict__ b1,
+                                                         float* __restrict__ out) {
+  __shared__ float s_w[64 * 9], s_b[64];
+  __shared__ float s_x[C1_ROWS + 2][66];
+  const int b = blockIdx.x / rb_per_clip;
+  const int t0 = (blockIdx.x - b * rb_per_clip) * C1_ROWS;
+  for (int i = threadIdx.x; i < 64 * 9; i += 256) s_w[i] = w1[i];
+  if (threadIdx.x < 64) s_b[threadIdx.x] = b1[threadIdx.x];
+  const float* xb = x0 + (int64_t)b * T * 64;
+  for (int i = threadIdx.x; i < (C1_ROWS + 2) * 66; i += 256) {
+    const int r = i / 66, c = i - r * 66;
+    const int t = t0 - 1 + r, f = c - 1;
+    s_x[r][c] = (t >= 0 && t < T && f >= 0 && f < 64) ? xb[t * 64 + f] : 0.0f;
+  }
+  __syncthreads();
+  const int cq = threadIdx.x & 15;
+  float wr[4][9], br[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+#pragma unroll
+    for (int k = 0; k < 9; ++k) wr[c][k] = s_w[(4 * cq + c) * 9 + k];
+    br[c] = s_b[4 * cq + c];
+  }
+  float* ob = out + ((int64_t)b * T + t0) * 64 * 64 + 4 * cq;
+#pragma unroll
+  for (int it = 0; it < C1_ROWS * 4; ++it) {
+    const int pxl = it * 16 + (threadIdx.x >> 4);   // pixel within the rows: row pxl >> 6, bin pxl & 63
+    const int r = pxl >> 6, f = pxl & 63;
+    if (t0 + r >= T) break;
+    float xv[9];
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx) xv[dy * 3 + dx] = s_x[r + dy][f + dx];
+    float y[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      float acc = 0.0f;
+#pragma unroll
+      for (int k = 0; k < 9; ++k) acc = fmaf(xv[k], wr[c][k], acc);
+      y[c] = fmaxf(acc + br[c], 0.0f);
+    }
+    *reinterpret_cast<float4*>(ob + (int64_t)pxl * 64) = make_float4(y[0], y[1], y[2], y[3]);
+  }
+}
+
+void launch_conv1_nhwc(const float* x0, int B, int T, const float* w1, const float* b1, float* out, hipStream_t s) {
+  const int rb = (T + C1_ROWS - 1) / C1_ROWS;
+  const int64_t blocks = (int64_t)B * rb;
+  if (B <= 0 || T <= 0 || blocks > INT32_MAX || (int64_t)T * 64 > INT32_MAX) return note_launch_error(hipErrorInvalidValue);
+  hipLaunchKernelGGL(conv1_nhwc_kernel, dim3((unsigned)blocks), dim3(256), 0, s, x0, T, rb, w1, b1, out);
 }
 
 // U = G g G^T per (input channel, output channel) in float64 from the

@@ -235,6 +235,282 @@ __global__ __launch_bounds__(64 * FE_WAVES) void logmel_kernel(FrontendParams p)
   }
 }
 
+// ---------------------------------------------------------------------------
+// 16 kHz preset (n_fft 512): register FFT, four frames per wavefront.
+//
+// A 16-lane row of the wave owns one frame; the 256-point complex FFT of
+// z[m] = w x[2m] + i w x[2m+1] is a four-step 16 x 16 FFT with m = 16 a + b:
+//   1. lane b: 16-point DFT over a of z[16 a + b] (in registers; its 16
+//      samples are 16 float2 loads, the row's 16 lanes reading 128 contiguous
+//      bytes per a);
+//   2. times W256^(b k1) (per-lane constants, loaded once);
+//   3. one transpose through LDS (8 ds_write_b128 + 16 ds_read_b64 per lane),
+//      then lane k1: 16-point DFT over b -> Z[k1 + 16 k2], k2 = 0..15;
+//   4. real-input unpack in pairs (k, N2 - k): lane c takes k2 = 0..7 and
+//      gets the partner lane's (16 - c) values by 8 cross-lane permutes; both
+//      bins of a pair come from one E / W^k O (|X[N2 - k]| = |E - W^k O|).
+// The power spectrum (bit-identical to the Stockham kernel's formula given
+// the same Z) goes to LDS; lane b then sums mel bands b, 31 - b, 32 + b,
+// 63 - b (balanced widths) in bin order, dB, bn0, store.
+// Two LDS round trips per four frames instead of four per frame, and every
+// FFT stage has 16 independent complex values per lane.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void dft4(float2& a0, float2& a1, float2& a2, float2& a3) {
+  const float2 s02 = cadd(a0, a2), d02 = csub(a0, a2);
+  const float2 s13 = cadd(a1, a3), d13 = csub(a1, a3);
+  a0 = cadd(s02, s13);
+  a2 = csub(s02, s13);
+  a1 = make_float2(d02.x + d13.y, d02.y - d13.x);   // d02 - i d13
+  a3 = make_float2(d02.x - d13.y, d02.y + d13.x);   // d02 + i d13
+}
+
+// X[k] = sum_n x[n] W16^(n k), natural order in and out (4 x 4)
+__device__ __forceinline__ void dft16(float2 (&x)[16]) {
+  constexpr float C1 = 0.92387953251128674f, S1 = 0.38268343236508978f, R2 = 0.70710678118654757f;
+#pragma unroll
+  for (int n2 = 0; n2 < 4; ++n2) dft4(x[n2], x[4 + n2], x[8 + n2], x[12 + n2]);
+  // x[4 k1 + n2] now holds y[n2][k1]; twiddle by W16^(n2 k1)
+  auto w1 = [](float2 a) { return make_float2(C1 * a.x + S1 * a.y, C1 * a.y - S1 * a.x); };   // W^1
+  auto w2 = [](float2 a) { return make_float2(R2 * (a.x + a.y), R2 * (a.y - a.x)); };         // W^2
+  auto w3 = [](float2 a) { return make_float2(S1 * a.x + C1 * a.y, S1 * a.y - C1 * a.x); };   // W^3
+  auto w4 = [](float2 a) { return make_float2(a.y, -a.x); };                                  // W^4 = -i
+  auto w6 = [](float2 a) { return make_float2(R2 * (a.y - a.x), -R2 * (a.x + a.y)); };        // W^6
+  auto w9 = [](float2 a) { return make_float2(-C1 * a.x - S1 * a.y, S1 * a.x - C1 * a.y); };  // W^9
+  x[5] = w1(x[5]);
+  x[9] = w2(x[9]);
+  x[13] = w3(x[13]);
+  x[6] = w2(x[6]);
+  x[10] = w4(x[10]);
+  x[14] = w6(x[14]);
+  x[7] = w3(x[7]);
+  x[11] = w6(x[11]);
+  x[15] = w9(x[15]);
+  // DFT4 over n2 for each k1: inputs x[4 k1 + n2], outputs X[k1 + 4 k2]
+  float2 y[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) y[i] = x[i];
+#pragma unroll
+  for (int k1 = 0; k1 < 4; ++k1) {
+    float2 a0 = y[4 * k1], a1 = y[4 * k1 + 1], a2 = y[4 * k1 + 2], a3 = y[4 * k1 + 3];
+    dft4(a0, a1, a2, a3);
+    x[k1] = a0;
+    x[k1 + 4] = a1;
+    x[k1 + 8] = a2;
+    x[k1 + 12] = a3;
+  }
+}
+
+constexpr int FE16_WAVES = 4;
+constexpr int FE16_ROW = 36;                       // floats per transpose row (16 float2 + pad)
+constexpr int FE16_FRAME = 16 * FE16_ROW + 32;     // floats per frame (transpose, then power)
+constexpr int FE16_MW = FE16_MEL_MW;               // widest mel band of the table path (bins, multiple of 4)
+__device__ __forceinline__ int fe16_band(int b, int q) { return q == 0 ? b : q == 1 ? 31 - b : q == 2 ? 32 + b : 63 - b; }
+
+template <bool I16>
+__global__ __launch_bounds__(64 * FE16_WAVES) void logmel512_kernel(FrontendParams p) {
+  constexpr int NFFT = 512, N2 = 256;
+  __shared__ __attribute__((aligned(16))) float s_fr[FE16_WAVES][4 * FE16_FRAME];
+  extern __shared__ float s_melw[];   // [p.mel_lds_floats]
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int g = lane >> 4, b = lane & 15;
+  const int nnz = p.mel_off[64];
+  const bool mel_in_lds = nnz <= p.mel_lds_floats;
+  if (mel_in_lds && p.mel_wmax > FE16_MW)
+    for (int i = threadIdx.x; i < nnz; i += 64 * FE16_WAVES) s_melw[i] = p.mel_w[i];
+
+  // per-lane constants: window of its 32 samples, step-2 twiddles W256^(b k1),
+  // unpack twiddles W512^(b + 16 k2), its four mel bands
+  float win[32];
+#pragma unroll
+  for (int a = 0; a < 16; ++a) {
+    win[2 * a] = p.window[32 * a + 2 * b];
+    win[2 * a + 1] = p.window[32 * a + 2 * b + 1];
+  }
+  float2 tw1[16], tw2[9];
+#pragma unroll
+  for (int k1 = 0; k1 < 16; ++k1) tw1[k1] = p.twiddle[(2 * b * k1) & (NFFT - 1)];
+#pragma unroll
+  for (int k2 = 0; k2 < 9; ++k2) tw2[k2] = p.twiddle[b + 16 * k2];
+  int mlo[4], o0[4], o1[4];
+  float bmu[4], bsc[4], bbi[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int m = fe16_band(b, q);
+    mlo[q] = p.mel_lo[m];
+    o0[q] = p.mel_off[m];
+    o1[q] = p.mel_off[m + 1];
+    bmu[q] = p.bn_mean[m];
+    bsc[q] = p.bn_scale[m];
+    bbi[q] = p.bn_bias[m];
+  }
+  // band weights per (slot q, lane b), zero-padded to the widest band rounded
+  // to 4 (host table; fma(P, 0, acc) == acc exactly for finite P, so the
+  // padded chain gives the band's own bits); window offsets of the items
+  __shared__ __attribute__((aligned(16))) float s_wt[4 * 16 * FE16_MW];
+  __shared__ int64_t s_wstart[64];
+  const int wmax = p.mel_wmax;
+  const bool mel_table = wmax <= FE16_MW;
+  static_assert((4 * 16 * FE16_MW) % (64 * FE16_WAVES) == 0, "table fill");
+#pragma unroll
+  for (int k = 0; k < 4 * 16 * FE16_MW / (64 * FE16_WAVES); ++k)
+    s_wt[threadIdx.x + 64 * FE16_WAVES * k] = p.mel_tab[threadIdx.x + 64 * FE16_WAVES * k];
+  if (threadIdx.x < 64) s_wstart[threadIdx.x] = p.win_start[threadIdx.x];
+  __syncthreads();
+
+  const int total = p.n_clips * p.n_win * p.T;
+  const int L = (int)p.sig_len;
+  float* fb = s_fr[wave] + g * FE16_FRAME;   // this frame's LDS (transpose rows, then power)
+  // samples of frame fr: v[2 a + e] = x[pos0 + 32 a + 2 b + e]
+  auto load = [&](int fr, float* v) {
+    if (fr >= total) {
+#pragma unroll
+      for (int i = 0; i < 32; ++i) v[i] = 0.0f;
+      return;
+    }
+    const unsigned item = (unsigned)fr / (unsigned)p.T;
+    const int t = fr - (int)item * p.T;
+    const unsigned clip = item / (unsigned)p.n_win;
+    const int w = (int)(item - clip * (unsigned)p.n_win);
+    const int64_t wstart = s_wstart[w];
+    const int64_t src_off = (int64_t)clip * p.clip_stride + wstart;
+    const int64_t av64 = p.clip_len - wstart;
+    const int avail = av64 > L ? L : (int)av64;
+    const int pos0 = t * p.hop - N2;
+    if (!I16 && pos0 >= 0 && pos0 + NFFT <= avail && ((src_off + pos0) & 1) == 0) {
+      const float2* src = reinterpret_cast<const float2*>(p.audio + src_off + pos0) + b;
+#pragma unroll
+      for (int a = 0; a < 16; ++a) {
+        const float2 q = src[16 * a];
+        v[2 * a] = q.x;
+        v[2 * a + 1] = q.y;
+      }
+      return;
+    }
+#pragma unroll
+    for (int a = 0; a < 16; ++a)
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        int j = pos0 + 32 * a + 2 * b + e;
+        if (j < 0) j = -j;                           // reflect (F.pad mode='reflect')
+        if (j >= L) j = 2 * (L - 1) - j;
+        const bool ok = j < avail;                   // pad_truncate zeros
+        const int jc = ok ? j : 0;
+        if (I16)
+          v[2 * a + e] = ok ? (float)((double)p.audio_i16[src_off + jc] / 32767.0) : 0.0f;
+        else
+          v[2 * a + e] = ok ? p.audio[src_off + jc] : 0.0f;
+      }
+  };
+
+  const int ngroups = (total + 3) >> 2;
+  int gi = (int)blockIdx.x * FE16_WAVES + wave;
+  const int gstride = (int)gridDim.x * FE16_WAVES;
+  float v[32];
+  if (gi < ngroups) load(4 * gi + g, v);
+  for (; gi < ngroups; gi += gstride) {
+    const int fr = 4 * gi + g;
+    float2 x[16];
+#pragma unroll
+    for (int a = 0; a < 16; ++a) x[a] = make_float2(v[2 * a] * win[2 * a], v[2 * a + 1] * win[2 * a + 1]);
+    if (gi + gstride < ngroups) load(4 * (gi + gstride) + g, v);   // next group, in flight
+    // 1-2: DFT over a, twiddle W256^(b k1)
+    dft16(x);
+#pragma unroll
+    for (int k1 = 1; k1 < 16; ++k1) x[k1] = cmul(x[k1], tw1[k1]);
+    // 3: transpose (row b = lane, column k1) -> lane k1 reads column b
+#pragma unroll
+    for (int k1 = 0; k1 < 16; k1 += 2)
+      *reinterpret_cast<float4*>(fb + b * FE16_ROW + 2 * k1) = make_float4(x[k1].x, x[k1].y, x[k1 + 1].x, x[k1 + 1].y);
+    wave_lds_sync();
+#pragma unroll
+    for (int bb = 0; bb < 16; ++bb) x[bb] = *reinterpret_cast<const float2*>(fb + bb * FE16_ROW + 2 * b);
+    dft16(x);   // x[k2] = Z[b + 16 k2]
+    // 4: unpack pairs (k = b + 16 k2, N2 - k), k2 = 0..7 (+ k2 = 8 on lane 0:
+    // bin 128).  Partner lane (16 - b) & 15 holds Z[N2 - k] at its 15 - k2;
+    // lane 0 pairs with itself at (16 - k2) & 15.
+    const int partner = (g << 4) | ((16 - b) & 15);
+    wave_lds_sync();   // every lane's column reads done before power overwrites the rows
+    float2 bzs[8];   // all 16 permutes issued before any use (one latency)
+#pragma unroll
+    for (int k2 = 0; k2 < 8; ++k2) {
+      bzs[k2].x = __shfl(x[15 - k2].x, partner);
+      bzs[k2].y = __shfl(x[15 - k2].y, partner);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int k2 = 0; k2 < 9; ++k2) {
+      float2 bz;
+      if (k2 < 8) {
+        bz = b == 0 ? x[(16 - k2) & 15] : bzs[k2];
+      } else {
+        bz = x[8];
+      }
+      const float2 A = x[k2];
+      const float2 E2 = make_float2(A.x + bz.x, A.y - bz.y);   // 2 E
+      const float2 D = make_float2(A.x - bz.x, A.y + bz.y);    // A - conj(Z[N2 - k])
+      const float2 O2 = make_float2(D.y, -D.x);                // 2 O = -i D
+      const float2 WO = cmul(tw2[k2], O2);
+      const float2 Xa = cadd(E2, WO), Xb = csub(E2, WO);       // 2 X[k], 2 conj(X[N2 - k])
+      const int k = b + 16 * k2;
+      if (k2 < 8) {
+        fb[k] = (Xa.x * Xa.x + Xa.y * Xa.y) * 0.25f;
+        fb[N2 - k] = (Xb.x * Xb.x + Xb.y * Xb.y) * 0.25f;
+      } else if (b == 0) {
+        fb[N2 / 2] = (Xa.x * Xa.x + Xa.y * Xa.y) * 0.25f;
+      }
+    }
+    wave_lds_sync();
+    // 5: mel bands (bin order fma chains, the four bands interleaved so
+    // each step has 16 LDS reads in flight), dB, bn0
+    float accq[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    if (mel_table) {
+      for (int e = 0; e < wmax; e += 4) {
+        float pw[4][4];
+        float4 ww[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          ww[q] = *reinterpret_cast<const float4*>(s_wt + (q * 16 + b) * FE16_MW + e);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) pw[q][j] = fb[mlo[q] + e + j];
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          accq[q] = fmaf(pw[q][0], ww[q].x, accq[q]);
+          accq[q] = fmaf(pw[q][1], ww[q].y, accq[q]);
+          accq[q] = fmaf(pw[q][2], ww[q].z, accq[q]);
+          accq[q] = fmaf(pw[q][3], ww[q].w, accq[q]);
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float acc = accq[q];
+      if (mel_table) {
+      } else if (mel_in_lds) {
+        for (int i = o0[q]; i < o1[q]; i += 4) {
+          float pw[4], ww[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const bool ok = i + e < o1[q];
+            pw[e] = ok ? fb[mlo[q] + (i + e - o0[q])] : 0.f;
+            ww[e] = ok ? s_melw[i + e] : 0.f;
+          }
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (i + e < o1[q]) acc = fmaf(pw[e], ww[e], acc);
+        }
+      } else {
+        for (int i = o0[q]; i < o1[q]; ++i) acc = fmaf(fb[mlo[q] + (i - o0[q])], p.mel_w[i], acc);
+      }
+      float db = 10.0f * log10f(fmaxf(acc, 1e-10f));
+      db = (db - bmu[q]) * bsc[q] + bbi[q];
+      if (fr < total) p.out[(int64_t)fr * 64 + fe16_band(b, q)] = db;
+    }
+    wave_lds_sync();   // power reads done before the next group's transpose writes
+  }
+}
+
 // at most the resident workgroups of the chip; every wave walks several
 // frames, so the register prefetch of the next frame overlaps the current FFT
 // (launch facts per device: launch_info)
@@ -267,9 +543,28 @@ static void launch_logmel_t(const FrontendParams& p0, int64_t total, hipStream_t
   hipLaunchKernelGGL((logmel_kernel<NFFT, I16>), dim3((unsigned)blocks), dim3(64 * FE_WAVES), li.dyn, s, p);
 }
 
+// one wave per four frames; every wave walks several groups so the register
+// prefetch of the next group overlaps the current one
+template <bool I16>
+static void launch_logmel512(const FrontendParams& p0, int64_t total, hipStream_t s) {
+  const LaunchInfo li =
+      launch_info(reinterpret_cast<const void*>(logmel512_kernel<I16>), 64 * FE16_WAVES, fe_mel_lds<512>());
+  if (!li.ok) return;
+  FrontendParams p = p0;
+  p.mel_lds_floats = (int32_t)(li.dyn / 4);
+  const int64_t groups = (total + 3) / 4;
+  int64_t blocks = (groups + FE16_WAVES - 1) / FE16_WAVES;
+  // register-limited to 2 waves per SIMD (~215 VGPRs): two 4-wave workgroups
+  // per CU (82 KB of the 160 KB LDS; the occupancy query assumes 64 KB per CU
+  // and would say one)
+  blocks = std::min<int64_t>(blocks, (int64_t)li.ncu * 2);
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL((logmel512_kernel<I16>), dim3((unsigned)blocks), dim3(64 * FE16_WAVES), li.dyn, s, p);
+}
+
 void launch_logmel(const FrontendParams& p, int n_fft, hipStream_t s) {
   const int64_t total = (int64_t)p.n_clips * p.n_win * p.T;
-  if (total >= (int64_t)1 << 31 || p.sig_len >= (int64_t)1 << 31) return note_launch_error(hipErrorInvalidValue);
+  if (total >= ((int64_t)1 << 31) - 4 ||p.sig_len >= (int64_t)1 << 31) return note_launch_error(hipErrorInvalidValue);
   const bool i16 = p.audio_i16 != nullptr;
   switch (n_fft) {
     case 256:
@@ -277,8 +572,8 @@ void launch_logmel(const FrontendParams& p, int n_fft, hipStream_t s) {
       else launch_logmel_t<256, false>(p, total, s);
       break;
     case 512:
-      if (i16) launch_logmel_t<512, true>(p, total, s);
-      else launch_logmel_t<512, false>(p, total, s);
+      if (i16) launch_logmel512<true>(p, total, s);
+      else launch_logmel512<false>(p, total, s);
       break;
     case 1024:
       if (i16) launch_logmel_t<1024, true>(p, total, s);

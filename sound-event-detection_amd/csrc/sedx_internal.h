@@ -20,6 +20,10 @@
 namespace sedx {
 
 // ---- frontend -------------------------------------------------------------
+// logmel512_kernel: lane b of a frame's 16-lane row sums mel bands b, 31 - b,
+// 32 + b, 63 - b (slots q = 0..3, balanced widths) from a zero-padded table
+constexpr int FE16_MEL_MW = 36;
+inline int fe16_band_host(int b, int q) { return q == 0 ? b : q == 1 ? 31 - b : q == 2 ? 32 + b : 63 - b; }
 struct FrontendParams {
   const float* audio;       // base pointer (fp32 samples)
   const int16_t* audio_i16; // or int16 samples, dequantised x / 32767 on load (utilities.py:78-79)
@@ -37,6 +41,8 @@ struct FrontendParams {
   const int32_t* mel_off;   // [65] offsets into mel_w
   const int32_t* mel_lo;    // [64] first fft bin of each band
   int32_t mel_lds_floats;   // set by launch_logmel: LDS room for the packed mel weights
+  const float* mel_tab;     // [4][16][FE16_MEL_MW] band weights of slot q, lane b (n_fft 512 kernel)
+  int32_t mel_wmax;         // widest band rounded up to 4 (> FE16_MEL_MW: the per-band loop)
   const float* bn_scale;    // [64] bn0 folded
   const float* bn_mean;     // [64]
   const float* bn_bias;     // [64]
@@ -96,11 +102,15 @@ void launch_conv3x3(const float* in, int B, int T, int F, int Cin, int Cout,
 
 // Same contract as fp32 Winograd F(2x2, 3x3) (conv_wino.hip): U from
 // pack_conv_wino (wf = BN-folded weights [Cout][Cin][9] in float64);
-// F in {32, 16, 8}, Cout % 32 == 0.
+// F in {64, 32, 16, 8}, Cout % 32 == 0 (F = 64: block 1's conv2, fed by
+// launch_conv1_nhwc).
 void launch_conv3x3_wino(const float* in, int B, int T, int F, int Cin, int Cout,
                          const float* U, const float* bias, float* out, int epi,
                          const float* zero16, hipStream_t s);
 void pack_conv_wino(const double* wf, int Cin, int Cout, float* U);   // U: Cin * Cout * 16 floats
+// block 1's conv1 + BN + ReLU: X0 [B][T][64] -> [B][T][64][64] (w1 [64][9] folded, b1 [64])
+void launch_conv1_nhwc(const float* x0, int B, int T, const float* w1, const float* b1, float* out,
+                       hipStream_t s);
 
 // Same contract on bf16 MFMA with a 3-term hi/lo split (fp32-class accuracy).
 // wp = host-packed split weights [Cout/BN][Cin/16][9][BN][4 x 16 B] (BN = 64 if

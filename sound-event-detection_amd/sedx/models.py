@@ -221,6 +221,7 @@ class _SedModel(nn.Module):
         self._natives = {}
         self.precision = 'exact'
         self.pipelined = False
+        self.tuning = {}           # sedx_set_tuning knob -> value, applied to every handle
 
     def _config(self):
         cfg = _lib.SedxConfig()
@@ -259,6 +260,11 @@ class _SedModel(nn.Module):
             _lib.check(_lib.lib().sedx_set_precision(nat.h, _lib.PRECISION[self.precision]), nat.h,
                        'set_precision')
             nat.precision = self.precision
+        for knob, value in self.tuning.items():
+            if getattr(nat, 'tuning', {}).get(knob) != value:
+                _lib.check(_lib.lib().sedx_set_tuning(nat.h, knob, value), nat.h, 'set_tuning')
+                nat.tuning = dict(getattr(nat, 'tuning', {}))
+                nat.tuning[knob] = value
         if getattr(nat, 'pipelined', False) != self.pipelined:
             _lib.check(_lib.lib().sedx_set_pipelined(nat.h, int(self.pipelined)), nat.h, 'set_pipelined')
             nat.pipelined = self.pipelined
@@ -272,6 +278,11 @@ class _SedModel(nn.Module):
         if mode not in _lib.PRECISION:
             raise ValueError('precision must be one of %s' % sorted(_lib.PRECISION))
         self.precision = mode
+        return self
+
+    def set_tuning(self, knob, value):
+        """An implementation choice of the library (sedx_set_tuning: _lib.TUNE_*)."""
+        self.tuning[int(knob)] = int(value)
         return self
 
     def set_pipelined(self, on=True):
