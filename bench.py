@@ -59,17 +59,28 @@ PEAK_TF = {'exact': 157.3, 'winograd': 157.3, 'x3': 2500.0 / 3}
 PEAK_HBM_GBPS = 8000.0
 PEAK_FP64_TF = 78.6        # MI355X datasheet FP64 vector (not in MI355X_MICROARCH.md)
 DTYPE = {'exact': 'f32',
-         'winograd': 'f32 (conv blocks 2-4 as Winograd F(2x2,3x3): f32 transforms, f32 MFMA, f32 accumulate)',
+         'winograd': 'f32 (conv2 of block 1 and blocks 2-4 as Winograd F(2x2,3x3): f32 transforms, f32 MFMA, '
+                     'f32 accumulate)',
          'x3': 'bf16x3-split (3 bf16 MFMAs per f32 MAC: hi*hi + hi*lo + lo*hi, f32 accumulate)'}
 # Winograd F(2x2,3x3): 16 matrix-pipe multiplies per 2x2 output tile where the
-# direct conv does 36 (blocks 2-4 in 'winograd' mode; block 1 stays direct)
-WINO_STAGES = ('b2c1', 'b2c2', 'b3c1', 'b3c2', 'b4c1', 'b4c2')
+# direct conv does 36 ('winograd' mode: blocks 2-4, and block 1's conv2 unless
+# --wino-block1 0 keeps block 1 as the direct fused launch)
+WINO_BLOCK1 = True
 WINO_MUL = 16.0 / 36.0
+
+
+def wino_stages():
+    return (('b1c2',) if WINO_BLOCK1 else ()) + ('b2c1', 'b2c2', 'b3c1', 'b3c2', 'b4c1', 'b4c2')
 # conv stages of sedx_stage_times: (F, Cin, Cout, number of 2x poolings before it)
 CONV_STAGES = {'b1c2': (64, 64, 64, 0), 'b2c1': (32, 64, 128, 1), 'b2c2': (32, 128, 128, 1),
                'b3c1': (16, 128, 256, 2), 'b3c2': (16, 256, 256, 2), 'b4c1': (8, 256, 512, 3),
                'b4c2': (8, 512, 512, 3)}
 FRONTEND_BYTES_PER_CLIP = 160000 * 4 + 1001 * 64 * 4   # waveform in + X0 out
+# per 512-sample frame: 256-point complex FFT (5 N log2 N), real unpack
+# (~10 per bin), window, |X|^2 (3 per bin), mel (2 per band weight, 514 at
+# 16 kHz), dB + bn0 (~4 per band)
+FRONTEND_FLOPS_PER_FRAME = 5 * 256 * 8 + 10 * 257 + 512 + 3 * 257 + 2 * 514 + 4 * 64
+PEAK_VALU_F32_TF = 78.6    # non-packed f32 VALU (packed FP32 is excluded beside MFMA)
 
 
 def conv_flops(stage, B, T):
@@ -85,6 +96,7 @@ def build_model(name, device, preset=(16000, 512, 160, 64, 25, 7000), feature='l
     for k, v in synth.make_state_dict(name, seed=0).items():
         sd[k] = torch.from_numpy(v)
     m.load_state_dict(sd)
+    m.set_tuning(_lib.TUNE_WINO_BLOCK1, int(WINO_BLOCK1))
     return m.to(device).eval()
 
 
@@ -320,8 +332,10 @@ def stage_times_isolated(model, wave, dev, reps):
 PROFILE_SUMMARY = os.path.join(REPO, 'profiles', 'r02b_kernel_summary.json')
 
 
-# block 1's conv1 (Cin 1 -> 64) computed inside the b1c2 launch
-FUSED_BLOCK1 = {'x3': True, 'exact': True, 'winograd': True}
+# block 1's conv1 (Cin 1 -> 64) computed inside the b1c2 launch (winograd
+# mode with the Winograd block 1: its own launch, stage b1c1)
+def fused_block1(precision):
+    return precision != 'winograd' or not WINO_BLOCK1
 
 
 def conv_kernel_name(stage, precision):
@@ -331,7 +345,7 @@ def conv_kernel_name(stage, precision):
     bn = 64 if cout == 64 else 128
     if precision == 'x3':
         return 'sedx::conv3x3_x3_kernel<%d, %d, %d, %s>' % (F, bn, epi, 'true' if stage == 'b1c2' else 'false')
-    if precision == 'winograd' and stage in WINO_STAGES:
+    if precision == 'winograd' and stage in wino_stages():
         # 4 tile groups (8 waves) at the bench shapes
         return 'sedx::conv3x3_wino_kernel<%d, %d, 4>' % (F, epi)
     # exact: 8-wave 64x64 wave tiles at the bench shapes (4-wave / 32x32 only for small grids)
@@ -364,9 +378,9 @@ def roofline(stage_ms, B, precision, T=1001):
     # matrix-pipe FLOPs the launch executes (Winograd layers: 16/36 of the
     # direct conv's) — the roofline's numerator; the direct-conv equivalent
     # is reported beside it
-    mul = {st: (WINO_MUL if wino and st in WINO_STAGES else 1.0) for st in CONV_STAGES}
+    mul = {st: (WINO_MUL if wino and st in wino_stages() else 1.0) for st in CONV_STAGES}
     flops = conv_flops(dom, B, T) * mul[dom]
-    if dom == 'b1c2' and FUSED_BLOCK1[precision]:
+    if dom == 'b1c2' and fused_block1(precision):
         flops += 2.0 * B * T * 64 * 64 * 9      # conv1 (Cin 1 -> 64) computed inside the launch
     achieved = flops / (conv[dom] * 1e-3) / 1e12
     peak = PEAK_TF[precision]
@@ -378,8 +392,8 @@ def roofline(stage_ms, B, precision, T=1001):
     traffic, rocprof_ms, mfma_util, clock = profiled(kname) if (B, T) == (32, 1001) else (None,) * 4
     return {'bound': 'mfma', 'kernel': '%s (%s)' % (kname, dom),
             'arith': {'exact': 'fp32 MFMA v_mfma_f32_32x32x2_f32 (f32 in, f32 acc)',
-                      'winograd': 'fp32 MFMA v_mfma_f32_32x32x2_f32 (f32 in, f32 acc); blocks 2-4 Winograd '
-                                  'F(2x2,3x3), their FLOPs counted as executed (16/36 of direct)',
+                      'winograd': 'fp32 MFMA v_mfma_f32_32x32x2_f32 (f32 in, f32 acc); Winograd F(2x2,3x3) '
+                                  'layers (%s) counted as executed FLOPs (16/36 of direct)' % ', '.join(wino_stages()),
                       'x3': '3xbf16-split MFMA 32x32x16, f32 acc (peak = bf16 dense 2.5 PF / 3)'}[precision],
             'achieved': round(achieved, 2), 'peak': round(peak, 1), 'unit': 'TFLOP/s',
             'frac': round(achieved / peak, 4),
@@ -517,8 +531,9 @@ def main():
     dev = torch.device('cuda', local)
     torch.cuda.set_device(dev)
     name = MODEL_NAMES[args.model]
+    global WINO_BLOCK1
+    WINO_BLOCK1 = bool(args.wino_block1)
     model = build_model(name, dev)
-    model.set_tuning(_lib.TUNE_WINO_BLOCK1, args.wino_block1)
     B = args.batch
     wave = torch.from_numpy(synth.make_waveforms(B, 10.0, 16000, seed=1234 + rank)).to(dev)
 
@@ -553,10 +568,17 @@ def main():
         if extra['stage_ms_isolated'].get('frontend'):
             fe = extra['stage_ms_isolated']['frontend']
             extra['frontend_roofline'] = {
-                'bound': 'hbm', 'kernel': 'sedx::logmel_kernel<512, false>',
+                'bound': 'hbm', 'kernel': 'sedx::logmel512_kernel<false>',
                 'achieved': round(B * FRONTEND_BYTES_PER_CLIP / (fe * 1e-3) / 1e9, 1), 'peak': PEAK_HBM_GBPS,
                 'unit': 'GB/s', 'frac': round(B * FRONTEND_BYTES_PER_CLIP / (fe * 1e-3) / 1e9 / PEAK_HBM_GBPS, 4),
-                'ms_per_batch': fe, 'bytes_per_clip': FRONTEND_BYTES_PER_CLIP}
+                'ms_per_batch': fe, 'bytes_per_clip': FRONTEND_BYTES_PER_CLIP,
+                # the FFT's arithmetic intensity (~16 FLOP/B) is past the
+                # non-packed f32 VALU ridge (78.6 TF / 8 TB/s = 9.8): the
+                # VALU side, with algorithmic FLOPs (radix-2 count) per frame
+                'flops_per_frame': FRONTEND_FLOPS_PER_FRAME,
+                'valu_tflops': round(B * 1001 * FRONTEND_FLOPS_PER_FRAME / (fe * 1e-3) / 1e12, 2),
+                'valu_peak_tflops': PEAK_VALU_F32_TF,
+                'valu_frac': round(B * 1001 * FRONTEND_FLOPS_PER_FRAME / (fe * 1e-3) / 1e12 / PEAK_VALU_F32_TF, 4)}
         extra.update(events_side(model, wave))
         extra['latency_b1'] = latency_b1(model, dev)
         notes = {'x3': 'opt-in arithmetic (operands narrowed to 16 significant bits), same workload',

@@ -302,7 +302,8 @@ __device__ __forceinline__ void dft16(float2 (&x)[16]) {
 
 constexpr int FE16_WAVES = 4;
 constexpr int FE16_ROW = 36;                       // floats per transpose row (16 float2 + pad)
-constexpr int FE16_FRAME = 16 * FE16_ROW + 32;     // floats per frame (transpose, then power)
+constexpr int FE16_FRAME = 16 * FE16_ROW + 16;     // floats per frame (transpose, then power); 592 = 16 mod 64:
+                                                   // the four frames of a wave start 16 banks apart
 constexpr int FE16_MW = FE16_MEL_MW;               // widest mel band of the table path (bins, multiple of 4)
 __device__ __forceinline__ int fe16_band(int b, int q) { return q == 0 ? b : q == 1 ? 31 - b : q == 2 ? 32 + b : 63 - b; }
 
@@ -320,18 +321,27 @@ __global__ __launch_bounds__(64 * FE16_WAVES) void logmel512_kernel(FrontendPara
     for (int i = threadIdx.x; i < nnz; i += 64 * FE16_WAVES) s_melw[i] = p.mel_w[i];
 
   // per-lane constants: window of its 32 samples, step-2 twiddles W256^(b k1),
-  // unpack twiddles W512^(b + 16 k2), its four mel bands
+  // unpack twiddles W512^(b + 16 k2), its four mel bands.  The twiddle and
+  // window tables are staged through the (not yet used) frame buffers with
+  // coalesced loads, so each lane reads its constants from LDS
+  float* stage = &s_fr[0][0];
+  for (int i = threadIdx.x; i < NFFT; i += 64 * FE16_WAVES) {
+    reinterpret_cast<float2*>(stage)[i] = p.twiddle[i];
+    stage[2 * NFFT + i] = p.window[i];
+  }
+  __syncthreads();
   float win[32];
 #pragma unroll
   for (int a = 0; a < 16; ++a) {
-    win[2 * a] = p.window[32 * a + 2 * b];
-    win[2 * a + 1] = p.window[32 * a + 2 * b + 1];
+    const float2 wv = *reinterpret_cast<const float2*>(stage + 2 * NFFT + 32 * a + 2 * b);
+    win[2 * a] = wv.x;
+    win[2 * a + 1] = wv.y;
   }
   float2 tw1[16], tw2[9];
 #pragma unroll
-  for (int k1 = 0; k1 < 16; ++k1) tw1[k1] = p.twiddle[(2 * b * k1) & (NFFT - 1)];
+  for (int k1 = 0; k1 < 16; ++k1) tw1[k1] = reinterpret_cast<const float2*>(stage)[(2 * b * k1) & (NFFT - 1)];
 #pragma unroll
-  for (int k2 = 0; k2 < 9; ++k2) tw2[k2] = p.twiddle[b + 16 * k2];
+  for (int k2 = 0; k2 < 9; ++k2) tw2[k2] = reinterpret_cast<const float2*>(stage)[b + 16 * k2];
   int mlo[4], o0[4], o1[4];
   float bmu[4], bsc[4], bbi[4];
 #pragma unroll

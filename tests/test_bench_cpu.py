@@ -47,7 +47,7 @@ def test_roofline_exact_unfused_and_names(bench):
     stage = {s: 0.2 for s in bench.CONV_STAGES}
     stage['b1c2'] = 1.0
     e = bench.roofline(stage, 32, 'exact')
-    fused = bench.FUSED_BLOCK1['exact']
+    fused = bench.fused_block1('exact')
     flops = bench.conv_flops('b1c2', 32, 1001) + (2.0 * 32 * 1001 * 64 * 64 * 9 if fused else 0.0)
     assert e['flops_per_launch'] == flops
     assert e['kernel'].startswith(bench.conv_kernel_name('b1c2', 'exact'))
@@ -58,3 +58,23 @@ def test_cpu_info(bench):
     info = bench.cpu_info()
     assert info['host_logical_cpus'] >= 1
     assert 'cpu_model' in info
+
+
+def test_roofline_winograd_block1(bench):
+    """Winograd mode: b1c2 is a Winograd launch (executed FLOPs 16/36 of the
+    direct conv2, conv1 in its own b1c1 launch); with --wino-block1 0 it is
+    the direct fused launch again."""
+    stage = {s: 0.2 for s in bench.CONV_STAGES}
+    stage['b1c2'] = 1.0
+    stage['b1c1'] = 0.1
+    assert bench.WINO_BLOCK1
+    w = bench.roofline(stage, 32, 'winograd')
+    assert w['kernel'] == 'sedx::conv3x3_wino_kernel<64, 1, 4> (b1c2)'
+    assert w['flops_per_launch'] == bench.conv_flops('b1c2', 32, 1001) * 16.0 / 36.0
+    try:
+        bench.WINO_BLOCK1 = False
+        d = bench.roofline(stage, 32, 'winograd')
+        assert d['kernel'].startswith('sedx::conv3x3_kernel<64, 64, 1, true')
+        assert d['flops_per_launch'] == bench.conv_flops('b1c2', 32, 1001) + 2.0 * 32 * 1001 * 64 * 64 * 9
+    finally:
+        bench.WINO_BLOCK1 = True
