@@ -41,6 +41,7 @@ struct DevWeights {
   float* c1_wt = nullptr;
   float* c1_b = nullptr;
   float* zero = nullptr;   // 256 zero bytes (LDS-DMA source of out-of-clip halo pixels)
+  float* trash = nullptr;  // 32 KB write-only scratch (the Winograd kernel's dummy / out-of-range stores)
   float* wp[8] = {};    // packed conv weights: block k conv j -> index 2(k-1)+(j-1); [0] unused
   float* cb[8] = {};    // folded biases
   void* wx3[8] = {};    // split bf16 hi/lo packs for conv3x3_x3 (same indices)
@@ -372,14 +373,15 @@ sedx_status run_body(sedx_handle* h, int64_t B, const Geometry& g, float* ws, co
       launch_block1_fused_x3(nullptr, iB, c.T, A, w.c1_wt, w.c1_b, w.wx3[c.idx], w.cb[c.idx], c.out,
                              sched, s);
     else if (i == 0 && wb1)
-      launch_conv3x3_wino(A, iB, c.T, 64, 64, 64, w.wu[c.idx], w.cb[c.idx], c.out, EPI_POOL2, w.zero, s);
+      launch_conv3x3_wino(A, iB, c.T, 64, 64, 64, w.wu[c.idx], w.cb[c.idx], c.out, EPI_POOL2, w.zero, w.trash, s);
     else if (i == 0)
       launch_block1_exact(A, iB, c.T, w.c1_w, w.c1_b, w.wp[c.idx], w.cb[c.idx], c.out, w.zero, s);
     else if (x3)
       launch_conv3x3_x3(c.in, iB, c.T, c.F, c.cin, c.cout, w.wx3[c.idx], w.cb[c.idx], c.out, c.epi,
                         sched + i * CONV_SCHED_INTS, s);
     else if (h->precision == SEDX_PRECISION_WINOGRAD)
-      launch_conv3x3_wino(c.in, iB, c.T, c.F, c.cin, c.cout, w.wu[c.idx], w.cb[c.idx], c.out, c.epi, w.zero, s);
+      launch_conv3x3_wino(c.in, iB, c.T, c.F, c.cin, c.cout, w.wu[c.idx], w.cb[c.idx], c.out, c.epi, w.zero, w.trash,
+                          s);
     else
       launch_conv3x3(c.in, iB, c.T, c.F, c.cin, c.cout, w.wp[c.idx], w.cb[c.idx], c.out, c.epi, w.zero, s);
     const size_t px = c.epi == EPI_STORE ? (size_t)c.T * c.F : c.epi == EPI_POOL2 ? (size_t)(c.T / 2) * (c.F / 2)
@@ -868,6 +870,8 @@ sedx_status sedx_finalize_weights(sedx_handle* h) {
   add((void**)&W.c1_b, c1b.data(), c1b.size() * 4);
   std::vector<float> zeros(64, 0.f);
   add((void**)&W.zero, zeros.data(), zeros.size() * 4);
+  std::vector<float> trash(64 * 128, 0.f);
+  add((void**)&W.trash, trash.data(), trash.size() * 4);
   for (int i = 1; i < 8; ++i) {
     add((void**)&W.wp[i], packed[i].data(), packed[i].size() * 4);
     add((void**)&W.cb[i], cbias[i].data(), cbias[i].size() * 4);

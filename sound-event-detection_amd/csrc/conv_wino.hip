@@ -40,6 +40,8 @@
 // Every shape (TG = 4 / 2 / 1) performs the same operations in the same order
 // for each (tile, channel), so outputs do not depend on the batch size or the
 // shape chosen.
+#include <type_traits>
+
 #include "sedx_internal.h"
 
 namespace sedx {
@@ -66,9 +68,10 @@ struct WinoGeom {
   static constexpr int UPW = (U + WAVES - 1) / WAVES;
   static constexpr int VM_MIN = U / WAVES;           // units of the wave with the fewest
   static constexpr int XCH = WAVES * 8 * 4 * 64;     // floats: epilogue exchange, [wave][r 8][4][lane]
-  static constexpr int LDS_BYTES = 4 * (NBUF * BUF > XCH ? NBUF * BUF : XCH);
+  static constexpr int LDS_BYTES = 4 * (NBUF * BUF + XCH);   // ring, then the epilogue exchange
   static_assert(P % FT == 0, "whole tile rows per workgroup");
   static_assert(VM_MIN * (NBUF - 1) <= 63, "vmcnt field");
+  static_assert(LDS_BYTES <= (TG == 4 ? 160 : 80) * 1024, "LDS per workgroup (1 per CU at TG 4, else 2)");
 };
 
 // raw workgroup barrier behind "this wave's DMAs older than its N youngest
@@ -78,16 +81,19 @@ template <int N>
 __device__ __forceinline__ void wino_bar_n() {
   asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
 }
-template <int VM, int Y>
+// S: this wave's epilogue stores issued after the awaited chunk's DMA (a
+// persistent workgroup's previous tile; every store is issued, so the count
+// is exact)
+template <int VM, int Y, int S = 0>
 __device__ __forceinline__ void wino_bar(int younger) {
   if constexpr (Y > 0) {
     if (younger >= Y) {
-      wino_bar_n<VM * Y>();
+      wino_bar_n<VM * Y + S>();
       return;
     }
-    wino_bar<VM, Y - 1>(younger);
+    wino_bar<VM, Y - 1, S>(younger);
   } else {
-    wino_bar_n<0>();
+    wino_bar_n<S>();
   }
 }
 
@@ -103,7 +109,7 @@ template <int F, int EPI, int TG, int PH>
 __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, int T, int Cin, int Cout,
                                           const float* __restrict__ U, const float* __restrict__ bias,
                                           float* __restrict__ out, const float* __restrict__ zero16,
-                                          int tb_per_clip, int ngroups) {
+                                          float* __restrict__ trash, int tb_per_clip, int ngroups) {
   constexpr int ph = PH;
   using G = WinoGeom<F, TG>;
   constexpr int WAVES = G::WAVES;
@@ -114,18 +120,27 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
   const int lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int tg = wv % TG;   // tile group (waves tg, tg + TG: position halves 0, 1 — one SIMD)
-  // XCD-aware decode: workgroup id -> XCD id & 7; on one XCD, tile blocks in
-  // order, each with its channel groups consecutive
-  const int id = blockIdx.x;
-  const int xcd = id & 7, j = id >> 3;
-  const int jb = j / ngroups;
-  const int tb = jb * 8 + xcd;
-  const int ng = j - jb * ngroups;
-  if (tb >= B * tb_per_clip) return;   // padding of the tile blocks to a multiple of 8 (uniform)
-  const int b = tb / tb_per_clip;
-  const int tr0 = (tb - b * tb_per_clip) * G::TRW;   // first tile row
-  const int t0 = 2 * tr0;
-  const int n0 = ng * 32;
+  // Persistent: workgroup g takes items g, g + gridDim.x, ... (gridDim.x a
+  // multiple of 8, so every item of a workgroup is on its XCD).  XCD-aware
+  // item decode: item -> XCD id & 7; on one XCD, tile blocks in order, each
+  // with its channel groups consecutive.  Padding items (tile blocks rounded
+  // up to a multiple of 8) come last on their XCD.
+  auto decode = [&](int item, int& b_, int& t0_, int& n0_) -> bool {
+    const int xcd = item & 7, j = item >> 3;
+    const int jb = j / ngroups;
+    const int tb = jb * 8 + xcd;
+    if (tb >= B * tb_per_clip) return false;
+    b_ = tb / tb_per_clip;
+    t0_ = 2 * (tb - b_ * tb_per_clip) * G::TRW;   // first row (2 x first tile row)
+    n0_ = (j - jb * ngroups) * 32;
+    return true;
+  };
+  // this workgroup's 128 trash floats (spread: the dummy and out-of-range
+  // stores of different workgroups do not pile onto one cache line)
+  float* const tr_lane = trash + (blockIdx.x & 63) * 128 + lane;
+  int item = blockIdx.x;
+  int b = 0, t0 = 0, n0 = 0;
+  if (!decode(item, b, t0, n0)) return;   // uniform
   const int khalf = lane >> 5;
 
   // A side: this lane's tile (lane & 31) and channel pair (2 khalf, 2 khalf + 1).
@@ -142,44 +157,50 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
   // wave's positions 8 ph .. 8 ph + 7
   const int b_base = G::A_SZ + 8 * ph * 128 + khalf * 64 + 2 * (lane & 31);
 
-  // ---- LDS-DMA units of this wave (unit u -> wave u % WAVES) ----
-  const float* dsrc[G::UPW];
-  int64_t dstep[G::UPW];
+  // ---- LDS-DMA units of this wave (unit u -> wave u % WAVES): LDS offsets
+  // fixed, sources per item ----
   int dlds[G::UPW];
 #pragma unroll
   for (int k = 0; k < G::UPW; ++k) {
     const int u = wv + WAVES * k;
-    dsrc[k] = zero16;
-    dstep[k] = 0;
-    dlds[k] = 0;
-    if (u < G::UW) {
-      const int row = 4 * u + (lane >> 4);   // (p, h) row of 2 x 32 floats
-      dsrc[k] = U + (int64_t)row * 2 * Cout + 2 * n0 + 4 * (lane & 15);
-      dstep[k] = (int64_t)32 * 2 * Cout;
-      dlds[k] = G::A_SZ + 256 * u;
-    } else if (u < G::U) {
-      const int slot = 64 * (u - G::UW) + lane;
-      const int q = slot / Q, rem = slot - q * Q;
-      const int r = 2 * (rem / HC) + (q >> 1), c = 2 * (rem % HC) + (q & 1);
-      const int t = t0 - 1 + r, f = c - 1;
-      if (slot < G::PL && t >= 0 && t < T && f >= 0 && f < F) {
-        dsrc[k] = in + (((int64_t)b * T + t) * F + f) * Cin;
-        dstep[k] = KC;
+    dlds[k] = u < G::UW ? G::A_SZ + 256 * u : 256 * (u - G::UW);
+  }
+  // a unit's source as a 32-bit element offset (from U + 2 n0 for weight
+  // units, from in for halo units; -1: a pixel outside the clip, read from
+  // the zero block): one VGPR per unit (the launcher checks B T F Cin < 2^31)
+  auto desc = [&](int b_, int t0_, int (&off)[G::UPW]) {
+#pragma unroll
+    for (int k = 0; k < G::UPW; ++k) {
+      const int u = wv + WAVES * k;
+      off[k] = -1;
+      if (u < G::UW) {
+        const int row = 4 * u + (lane >> 4);   // (p, h) row of 2 x 32 floats
+        off[k] = row * 2 * Cout + 4 * (lane & 15);
+      } else if (u < G::U) {
+        const int slot = 64 * (u - G::UW) + lane;
+        const int q = slot / Q, rem = slot - q * Q;
+        const int r = 2 * (rem / HC) + (q >> 1), c = 2 * (rem % HC) + (q & 1);
+        const int t = t0_ - 1 + r, f = c - 1;
+        if (slot < G::PL && t >= 0 && t < T && f >= 0 && f < F) off[k] = ((b_ * T + t) * F + f) * Cin;
       }
-      dlds[k] = 256 * (u - G::UW);
     }
-  }
-#define SEDX_WG_DMA(chunk_, buf_)                                                                      \
-  {                                                                                                    \
-    _Pragma("unroll") for (int k = 0; k < G::UPW; ++k) {                                               \
-      if (wv + WAVES * k < G::U) {                                                                     \
-        const uint32_t m0_ = (uint32_t)(size_t)(__attribute__((address_space(3))) float*)(             \
-            smem + (buf_) * G::BUF + dlds[k]);                                                         \
-        sedx_glds16(dsrc[k] + (int64_t)(chunk_) * dstep[k], __builtin_amdgcn_readfirstlane(m0_));      \
-      }                                                                                                \
-    }                                                                                                  \
-    asm volatile("" ::: "memory");                                                                     \
-  }
+  };
+  auto dma = [&](const int (&off)[G::UPW], int n0_, int chunk_, int buf_) {
+#pragma unroll
+    for (int k = 0; k < G::UPW; ++k) {
+      const int u = wv + WAVES * k;
+      if (u < G::U) {
+        const uint32_t m0_ =
+            (uint32_t)(size_t)(__attribute__((address_space(3))) float*)(smem + buf_ * G::BUF + dlds[k]);
+        const float* src = u < G::UW ? U + 2 * n0_ + off[k] + (int64_t)chunk_ * (64 * Cout)
+                                     : (off[k] >= 0 ? in + off[k] + chunk_ * KC : zero16);
+        sedx_glds16(src, __builtin_amdgcn_readfirstlane(m0_));
+      }
+    }
+    asm volatile("" ::: "memory");
+  };
+  int doff[G::UPW];
+  desc(b, t0, doff);
 
   f32x16 acc[8];
 #pragma unroll
@@ -259,42 +280,32 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
 
   const int nchunks = Cin / KC;   // even (Cin % 8 == 0, checked by the launcher)
   constexpr int NB = G::NBUF;
+  // epilogue stores per wave (all issued: out-of-range ones go to trash)
+  constexpr int S = EPI == EPI_FMEAN ? 4 : EPI == EPI_POOL2 ? 8 : 32;
+  static_assert(G::VM_MIN * (NB - 2) + S <= 63, "vmcnt field");
 #pragma unroll
-  for (int c = 0; c < NB; ++c)
-    if (c < nchunks) SEDX_WG_DMA(c, c);
-  // chunk 0 landed: younger chunks 1 .. NB - 1 may be in flight
-  wino_bar<G::VM_MIN, NB - 1>(min(NB - 1, nchunks - 1));
+  for (int c = 0; c < NB; ++c) dma(doff, n0, c, c);   // nchunks >= 8 (launcher)
+  // S stores to trash: every item, the first included, then has S stores
+  // between its chunk NB - 1 and chunk NB DMAs (a later item: the previous
+  // item's epilogue), so all items wait alike
   {
-    float2 pd[3][4];
-    issue_reads(0, pd, ua);
-    transform(pd, va);
+    float* const vt = tr_lane;   // inline asm: exactly S global stores (never merged)
+    const float zf = 0.0f;
+#pragma unroll
+    for (int i = 0; i < S; ++i) asm volatile("global_store_dword %0, %1, off" ::"v"(vt), "v"(zf) : "memory");
   }
+  // chunk 0 landed: younger chunks 1 .. NB - 1 and the S stores may be in flight
+  wino_bar<G::VM_MIN, NB - 1, S>(NB - 1);
 
-  // top of chunk c: chunk c + 1 landed (c + 2 .. c + NB - 1 may be in
-  // flight) and every wave has consumed chunk c's buffer (its reads were
-  // waited for in the previous step), which then receives chunk c + NB.  On
-  // the last chunk the step's reads of the "next" buffer are unused.
-  int buf = 0;
-  for (int chunk = 0; chunk < nchunks; chunk += 2) {
-    const int b1 = buf == NB - 1 ? 0 : buf + 1, b2 = b1 == NB - 1 ? 0 : b1 + 1;
-    wino_bar<G::VM_MIN, NB - 2>(max(0, min(NB - 2, nchunks - chunk - 2)));
-    if (chunk + NB < nchunks) SEDX_WG_DMA(chunk + NB, buf);
-    step(va, ua, b1, vb, ubv);
-    wino_bar<G::VM_MIN, NB - 2>(max(0, min(NB - 2, nchunks - chunk - 3)));
-    if (chunk + 1 + NB < nchunks) SEDX_WG_DMA(chunk + 1 + NB, b1);
-    step(vb, ubv, b2, va, ua);
-    buf = b2;
-  }
-#undef SEDX_WG_DMA
-
-  // ---- epilogue.  Register r of every position tile = MFMA row
+  // ---- epilogue pieces.  Register r of every position tile = MFMA row
   // m = (r & 3) + 8 (r >> 2) + 4 khalf (tile 32 tg + m), column lane & 31.
   // Each wave reduces its V rows i to a partial Y = A^T M A: with
   // T_a[j] = sum_i A^T[a][i] M[i][j] over its rows (ph 0: T_0 = m0 + m1,
   // T_1 = m1; ph 1: T_0 = m2, T_1 = -m2 - m3), Y[a] = (T_a0 + T_a1 + T_a2,
   // T_a1 - T_a2 - T_a3).  Wave half h finishes registers 8 h .. 8 h + 7:
   // it hands its partial of the other half's registers over through LDS
-  // and sums Y_0 + Y_1 (in that order) for its own. ----
+  // (an exchange area of its own, after the ring, so the next item's chunks
+  // can already be landing) and sums Y_0 + Y_1 (in that order) for its own.
   auto partial = [&](int r, float y[4]) {
     float t[2][4];
 #pragma unroll
@@ -314,109 +325,224 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
       y[2 * a + 1] = (t[a][1] - t[a][2]) - t[a][3];
     }
   };
-  wino_bar_n<0>();   // every wave's last fragment reads done: the ring is free
-  float* xo = smem + wv * (8 * 4 * 64);   // this wave's exchange slots [r 8][4][lane]
-  const int ro = 8 * (1 - ph);            // registers the partner finishes
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    float y[4];
-    partial(ro + k, y);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) xo[(k * 4 + e) * 64 + lane] = y[e];
-  }
-  __syncthreads();
-  const float* xi = smem + (tg + TG * (1 - ph)) * (8 * 4 * 64);   // the partner's slots
-  const int n = n0 + (lane & 31);
-  const float bv = bias[n];
-  // full Y of register 8 ph + k (+ bias, ReLU), as y[a][b]
-  auto outtile = [&](int k, float y[2][2]) {
-    float mine[4];
-    partial(8 * ph + k, mine);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const float other = xi[(k * 4 + e) * 64 + lane];
-      const float s = PH == 0 ? mine[e] + other : other + mine[e];
-      y[e >> 1][e & 1] = fmaxf(s + bv, 0.0f);
+  float* const xo = smem + NB * G::BUF + wv * (8 * 4 * 64);                    // this wave's slots [r 8][4][lane]
+  const float* const xi = smem + NB * G::BUF + (tg + TG * (1 - ph)) * (8 * 4 * 64);   // the partner's
+
+  // top of chunk c: chunk c + 1 landed (c + 2 .. c + NB - 1 of the item
+  // sequence may be in flight) and every wave has consumed chunk c's buffer
+  // (its reads were waited for in the previous step), which then receives
+  // chunk c + NB — of this item, or of the next one over the last chunks.
+  // The next item's chunk 0 is read and transformed after the epilogue.
+  int buf = 0;
+  for (;;) {
+    const int nitem = item + (int)gridDim.x;
+    int nb_ = 0, nt0 = 0, nn0 = 0;
+    const bool has_next = decode(nitem, nb_, nt0, nn0);
+    const float bv = bias[n0 + (lane & 31)];   // loaded early: its wait must not drain the DMAs
+    {   // the item's chunk 0 (landed: the previous barrier waited for it)
+      float2 pd[3][4];
+      issue_reads(buf, pd, ua);
+      transform(pd, va);
     }
-  };
-  if constexpr (EPI == EPI_FMEAN) {
-    // F = 8: registers 4q .. 4q + 3 are the 4 tiles (bins 0-7) of tile row
-    // 8 tg + 2 q + khalf; torch.mean over the 8 bins
-    static_assert(F == 8, "freq-mean epilogue: F = 8");
 #pragma unroll
-    for (int qq = 0; qq < 2; ++qq) {
-      const int q = 2 * ph + qq;
-      float y[4][2][2];
+    for (int p = 0; p < 8; ++p)
 #pragma unroll
-      for (int jj = 0; jj < 4; ++jj) outtile(4 * qq + jj, y[jj]);
-      const int trl = 8 * tg + 2 * q + khalf;
-#pragma unroll
-      for (int a = 0; a < 2; ++a) {
-        float sum = 0.0f;
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) sum = (sum + y[jj][a][0]) + y[jj][a][1];
-        const int t = t0 + 2 * trl + a;
-        if (t < T) out[((int64_t)b * T + t) * Cout + n] = sum * (1.0f / F);
+      for (int r = 0; r < 16; ++r) acc[p][r] = 0.0f;
+    auto issue = [&](int g, int bf) {
+      if (g < nchunks) {
+        dma(doff, n0, g, bf);
+      } else if (has_next) {
+        int noff[G::UPW];
+        desc(nb_, nt0, noff);
+        dma(noff, nn0, g - nchunks, bf);
       }
-    }
-  } else {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int r = 8 * ph + k;
-      const int m = (r & 3) + 8 * (r >> 2) + 4 * khalf;
-      const int ptile = 32 * tg + m;
-      const int trl = ptile / FT, tf = ptile % FT;
-      float y[2][2];
-      outtile(k, y);
-      if constexpr (EPI == EPI_POOL2) {
-        const int To = T / 2;
-        const int to = tr0 + trl;
-        const float pv = (((y[0][0] + y[0][1]) + y[1][0]) + y[1][1]) * 0.25f;
-        if (to < To) out[(((int64_t)b * To + to) * (F / 2) + tf) * Cout + n] = pv;
+    };
+    // one chunk pair; LAST: the item's final pair, whose second step runs
+    // the MFMAs only (the next item's chunk 0 is read at the next item's top)
+    // MID: both DMAs of the pair are of this item and NB - 2 chunks are in
+    // flight behind each awaited one (no branches: the steady state)
+    auto pair = [&](int chunk, auto first_tag, auto last_tag, auto mid_tag) {
+      constexpr bool FIRST = decltype(first_tag)::value, LAST = decltype(last_tag)::value;
+      constexpr bool MID = decltype(mid_tag)::value;
+      const int b1 = buf == NB - 1 ? 0 : buf + 1, b2 = b1 == NB - 1 ? 0 : b1 + 1;
+      // chunks 1 and 2 of an item: the S stores (previous epilogue, or the
+      // prologue's) were issued after their DMAs
+      if constexpr (MID) {
+        wino_bar_n<G::VM_MIN * (NB - 2) + (FIRST ? S : 0)>();
+        dma(doff, n0, chunk + NB, buf);
+      } else {
+        wino_bar<G::VM_MIN, NB - 2, FIRST ? S : 0>(has_next ? NB - 2 : max(0, min(NB - 2, nchunks - chunk - 2)));
+        issue(chunk + NB, buf);
+      }
+      step(va, ua, b1, vb, ubv);
+      if constexpr (MID) {
+        wino_bar_n<G::VM_MIN * (NB - 2) + (FIRST ? S : 0)>();
+        dma(doff, n0, chunk + 1 + NB, b1);
+      } else {
+        wino_bar<G::VM_MIN, NB - 2, FIRST ? S : 0>(has_next ? NB - 2 : max(0, min(NB - 2, nchunks - chunk - 3)));
+        issue(chunk + 1 + NB, b1);
+      }
+      if constexpr (!LAST) {
+        step(vb, ubv, b2, va, ua);
       } else {
 #pragma unroll
+        for (int p = 0; p < 8; ++p) acc[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(vb[0][p], ubv[p].x, acc[p], 0, 0, 0);
+#pragma unroll
+        for (int p = 0; p < 8; ++p) acc[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(vb[1][p], ubv[p].y, acc[p], 0, 0, 0);
+      }
+      buf = b2;
+    };
+    // nchunks >= 8 (launcher): pair 0 and the middle pairs keep both DMAs in
+    // this item; the last two pairs reach into the next one
+    pair(0, std::true_type{}, std::false_type{}, std::true_type{});
+    for (int chunk = 2; chunk < nchunks - 4; chunk += 2)
+      pair(chunk, std::false_type{}, std::false_type{}, std::true_type{});
+    pair(nchunks - 4, std::false_type{}, std::false_type{}, std::false_type{});
+    pair(nchunks - 2, std::false_type{}, std::true_type{}, std::false_type{});
+
+#ifdef SEDX_WINO_ABL_NOEPI
+    {   // keep every accumulator (and so every MFMA) alive
+      float sink = 0.0f;
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sink += acc[q][r];
+      if (sink == 12345.678f) out[0] = sink;
+    }
+    return;
+#endif
+    // ---- epilogue ----
+    const int tr0 = t0 / 2;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float y[4];
+      partial(8 * (1 - ph) + k, y);   // registers the partner finishes
+#pragma unroll
+      for (int e = 0; e < 4; ++e) xo[(k * 4 + e) * 64 + lane] = y[e];
+    }
+    // LDS-only barrier (__syncthreads() would drain the next item's DMAs)
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    const int n = n0 + (lane & 31);
+    // full Y of register 8 ph + k (+ bias, ReLU), as y[a][b]
+    auto outtile = [&](int k, float y[2][2]) {
+      float mine[4];
+      partial(8 * ph + k, mine);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float other = xi[(k * 4 + e) * 64 + lane];
+        const float sm = PH == 0 ? mine[e] + other : other + mine[e];
+        y[e >> 1][e & 1] = fmaxf(sm + bv, 0.0f);
+      }
+    };
+    if constexpr (EPI == EPI_FMEAN) {
+      // F = 8: registers 4q .. 4q + 3 are the 4 tiles (bins 0-7) of tile row
+      // 8 tg + 2 q + khalf; torch.mean over the 8 bins
+      static_assert(F == 8, "freq-mean epilogue: F = 8");
+#pragma unroll
+      for (int qq = 0; qq < 2; ++qq) {
+        const int q = 2 * ph + qq;
+        float y[4][2][2];
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) outtile(4 * qq + jj, y[jj]);
+        const int trl = 8 * tg + 2 * q + khalf;
+#pragma unroll
         for (int a = 0; a < 2; ++a) {
+          float sum = 0.0f;
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) sum = (sum + y[jj][a][0]) + y[jj][a][1];
           const int t = t0 + 2 * trl + a;
-          if (t < T) {
-            float* o = out + (((int64_t)b * T + t) * F + 2 * tf) * Cout + n;
+          float* dst = t < T ? out + ((int64_t)b * T + t) * Cout + n : tr_lane;
+          *dst = sum * (1.0f / F);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int r = 8 * ph + k;
+        const int m = (r & 3) + 8 * (r >> 2) + 4 * khalf;
+        const int ptile = 32 * tg + m;
+        const int trl = ptile / FT, tf = ptile % FT;
+        float y[2][2];
+        outtile(k, y);
+        if constexpr (EPI == EPI_POOL2) {
+          const int To = T / 2;
+          const int to = tr0 + trl;
+          const float pv = (((y[0][0] + y[0][1]) + y[1][0]) + y[1][1]) * 0.25f;
+          float* dst = to < To ? out + (((int64_t)b * To + to) * (F / 2) + tf) * Cout + n : tr_lane;
+          *dst = pv;
+        } else {
+#pragma unroll
+          for (int a = 0; a < 2; ++a) {
+            const int t = t0 + 2 * trl + a;
+            float* o = t < T ? out + (((int64_t)b * T + t) * F + 2 * tf) * Cout + n : tr_lane;
+            const int64_t o1 = t < T ? Cout : 64;
             o[0] = y[a][0];
-            o[Cout] = y[a][1];
+            o[o1] = y[a][1];
           }
         }
       }
     }
+    if (!has_next) break;
+    // the partner's reads of this item's exchange slots finish before the
+    // next item's epilogue overwrites them: many barriers lie between
+    item = nitem;
+    b = nb_;
+    t0 = nt0;
+    n0 = nn0;
+    desc(b, t0, doff);
   }
 }
 
 template <int F, int EPI, int TG>
 __global__ __launch_bounds__(128 * TG, TG == 4 ? 1 : 2) void conv3x3_wino_kernel(
     const float* __restrict__ in, int B, int T, int Cin, int Cout, const float* __restrict__ U,
-    const float* __restrict__ bias, float* __restrict__ out, const float* __restrict__ zero16, int tb_per_clip,
-    int ngroups) {
+    const float* __restrict__ bias, float* __restrict__ out, const float* __restrict__ zero16,
+    float* __restrict__ trash, int tb_per_clip, int ngroups) {
   if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) < TG)
-    wino_body<F, EPI, TG, 0>(in, B, T, Cin, Cout, U, bias, out, zero16, tb_per_clip, ngroups);
+    wino_body<F, EPI, TG, 0>(in, B, T, Cin, Cout, U, bias, out, zero16, trash, tb_per_clip, ngroups);
   else
-    wino_body<F, EPI, TG, 1>(in, B, T, Cin, Cout, U, bias, out, zero16, tb_per_clip, ngroups);
+    wino_body<F, EPI, TG, 1>(in, B, T, Cin, Cout, U, bias, out, zero16, trash, tb_per_clip, ngroups);
 }
+
+static int wino_device_cus() {
+  int dev = 0, ncu = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  return ncu;
+}
+
+#ifndef SEDX_WINO_ITEMS
+#define SEDX_WINO_ITEMS 4
+#endif
+constexpr int WINO_ITEMS = SEDX_WINO_ITEMS;
 
 template <int F, int TG>
 static void launch_wino_w(const float* in, int B, int T, int Cin, int Cout, const float* U, const float* bias,
-                          float* out, int epi, const float* zero16, hipStream_t s) {
+                          float* out, int epi, const float* zero16, float* trash, hipStream_t s) {
   using G = WinoGeom<F, TG>;
   // tile rows of a clip: POOL2 drops an odd last row (floor), the others keep it
   const int trows = epi == EPI_POOL2 ? T / 2 : (T + 1) / 2;
   const int tb_per_clip = (trows + G::TRW - 1) / G::TRW;
   const int ngroups = Cout / 32;
   const int64_t tblocks = (int64_t)B * tb_per_clip;
-  const int64_t nwg = (tblocks + 7) / 8 * 8 * ngroups;
-  if (nwg > INT32_MAX || tblocks <= 0) return note_launch_error(hipErrorInvalidValue);
+  const int64_t nitems = (tblocks + 7) / 8 * 8 * ngroups;
+  if (nitems > INT32_MAX || tblocks <= 0 || (int64_t)B * T * F * Cin >= INT32_MAX)   // 32-bit DMA offsets
+    return note_launch_error(hipErrorInvalidValue);
+  // persistent workgroups: as many as are resident (1 per CU at TG 4, else
+  // 2), a multiple of 8 (XCD-aware item decode); each walks its items with
+  // the next item's first chunks landing during the current one's last
+  // ~WINO_ITEMS items per workgroup, but at least one resident round: the
+  // hardware dispatcher still balances the workgroups over the CUs (a CU
+  // shared with another stream's kernel finishes its workgroups later)
+  const int64_t resident = (int64_t)wino_device_cus() * (TG == 4 ? 1 : 2) / 8 * 8;
+  const int64_t per = (nitems + WINO_ITEMS - 1) / WINO_ITEMS;
+  const int64_t nwg = std::min<int64_t>(nitems, std::max<int64_t>(std::max<int64_t>(8, resident), (per + 7) / 8 * 8));
   dim3 grid((unsigned)nwg);
 #define SEDX_WG_LAUNCH(E)                                                                              \
   {                                                                                                    \
     auto* k_ = conv3x3_wino_kernel<F, E, TG>;                                                          \
     if (!launch_info(reinterpret_cast<const void*>(k_), G::THREADS, G::LDS_BYTES).ok) return;          \
     hipLaunchKernelGGL(k_, grid, dim3(G::THREADS), G::LDS_BYTES, s, in, B, T, Cin, Cout, U, bias, out, zero16, \
-                       tb_per_clip, ngroups);                                                          \
+                       trash, tb_per_clip, ngroups);                                                   \
     return;                                                                                            \
   }
   if constexpr (F == 8) {
@@ -430,36 +556,31 @@ static void launch_wino_w(const float* in, int B, int T, int Cin, int Cout, cons
   note_launch_error(hipErrorInvalidValue);
 }
 
-static int wino_device_cus() {
-  int dev = 0, ncu = 256;
-  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-  return ncu;
-}
 
 // 4 tile groups (128 tiles) when that gives every CU a workgroup, else 2,
 // else 1: the same per-wave work, bit-identical outputs
 template <int F>
 static void launch_wino_f(const float* in, int B, int T, int Cin, int Cout, const float* U, const float* bias,
-                          float* out, int epi, const float* zero16, hipStream_t s) {
+                          float* out, int epi, const float* zero16, float* trash, hipStream_t s) {
   const int64_t ncu = wino_device_cus();
   const int trows = epi == EPI_POOL2 ? T / 2 : (T + 1) / 2;
   auto wgs = [&](int trw) { return (int64_t)B * ((trows + trw - 1) / trw) * (Cout / 32); };
   if (wgs(WinoGeom<F, 4>::TRW) >= ncu)
-    launch_wino_w<F, 4>(in, B, T, Cin, Cout, U, bias, out, epi, zero16, s);
+    launch_wino_w<F, 4>(in, B, T, Cin, Cout, U, bias, out, epi, zero16, trash, s);
   else if (wgs(WinoGeom<F, 2>::TRW) >= ncu)
-    launch_wino_w<F, 2>(in, B, T, Cin, Cout, U, bias, out, epi, zero16, s);
+    launch_wino_w<F, 2>(in, B, T, Cin, Cout, U, bias, out, epi, zero16, trash, s);
   else
-    launch_wino_w<F, 1>(in, B, T, Cin, Cout, U, bias, out, epi, zero16, s);
+    launch_wino_w<F, 1>(in, B, T, Cin, Cout, U, bias, out, epi, zero16, trash, s);
 }
 
 void launch_conv3x3_wino(const float* in, int B, int T, int F, int Cin, int Cout, const float* U,
-                         const float* bias, float* out, int epi, const float* zero16, hipStream_t s) {
-  if (Cin % 8 != 0 || Cout % 32 != 0 || B <= 0 || T <= 0) return note_launch_error(hipErrorInvalidValue);
+                         const float* bias, float* out, int epi, const float* zero16, float* trash, hipStream_t s) {
+  if (Cin % 8 != 0 || Cin < 32 || Cout % 32 != 0 || B <= 0 || T <= 0) return note_launch_error(hipErrorInvalidValue);
   switch (F) {
-    case 64: launch_wino_f<64>(in, B, T, Cin, Cout, U, bias, out, epi, zero16, s); break;
-    case 32: launch_wino_f<32>(in, B, T, Cin, Cout, U, bias, out, epi, zero16, s); break;
-    case 16: launch_wino_f<16>(in, B, T, Cin, Cout, U, bias, out, epi, zero16, s); break;
-    case 8: launch_wino_f<8>(in, B, T, Cin, Cout, U, bias, out, epi, zero16, s); break;
+    case 64: launch_wino_f<64>(in, B, T, Cin, Cout, U, bias, out, epi, zero16, trash, s); break;
+    case 32: launch_wino_f<32>(in, B, T, Cin, Cout, U, bias, out, epi, zero16, trash, s); break;
+    case 16: launch_wino_f<16>(in, B, T, Cin, Cout, U, bias, out, epi, zero16, trash, s); break;
+    case 8: launch_wino_f<8>(in, B, T, Cin, Cout, U, bias, out, epi, zero16, trash, s); break;
     default: note_launch_error(hipErrorInvalidValue); break;
   }
 }

@@ -104,9 +104,11 @@ void launch_conv3x3(const float* in, int B, int T, int F, int Cin, int Cout,
 // pack_conv_wino (wf = BN-folded weights [Cout][Cin][9] in float64);
 // F in {64, 32, 16, 8}, Cout % 32 == 0 (F = 64: block 1's conv2, fed by
 // launch_conv1_nhwc).
+// trash: >= 64 x 128 floats of device scratch; out-of-range epilogue stores land
+// there (every store is issued, so the persistent kernel's counted waits are exact).
 void launch_conv3x3_wino(const float* in, int B, int T, int F, int Cin, int Cout,
                          const float* U, const float* bias, float* out, int epi,
-                         const float* zero16, hipStream_t s);
+                         const float* zero16, float* trash, hipStream_t s);
 void pack_conv_wino(const double* wf, int Cin, int Cout, float* U);   // U: Cin * Cout * 16 floats
 // block 1's conv1 + BN + ReLU: X0 [B][T][64] -> [B][T][64][64] (w1 [64][9] folded, b1 [64])
 void launch_conv1_nhwc(const float* x0, int B, int T, const float* w1, const float* b1, float* out,

@@ -31,6 +31,8 @@ int main(int argc, char** argv) {
   hipMalloc(&d_in, max_in * 4); hipMalloc(&d_o1, max_out * 4); hipMalloc(&d_o2, max_out * 4);
   hipMalloc(&d_bias, 512 * 4); hipMalloc(&d_wp, max_w * 4); hipMalloc(&d_u, max_w * 4);
   hipMalloc(&d_zero, 256); hipMemset(d_zero, 0, 256);
+  float* d_trash;
+  hipMalloc(&d_trash, 64 * 128 * 4);
   hipEvent_t e0, e1;
   hipEventCreate(&e0); hipEventCreate(&e1);
   std::mt19937 rng(7);
@@ -65,7 +67,7 @@ int main(int argc, char** argv) {
     hipMemset(d_o1, 0xff, nout * 4);
     hipMemset(d_o2, 0xff, nout * 4);
     auto direct = [&]() { sedx::launch_conv3x3(d_in, B, l.T, l.F, l.cin, l.cout, d_wp, d_bias, d_o1, l.epi, d_zero, 0); };
-    auto wino = [&]() { sedx::launch_conv3x3_wino(d_in, B, l.T, l.F, l.cin, l.cout, d_u, d_bias, d_o2, l.epi, d_zero, 0); };
+    auto wino = [&]() { sedx::launch_conv3x3_wino(d_in, B, l.T, l.F, l.cin, l.cout, d_u, d_bias, d_o2, l.epi, d_zero, d_trash, 0); };
     direct();
     wino();
     hipDeviceSynchronize();
