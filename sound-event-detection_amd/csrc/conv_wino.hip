@@ -400,17 +400,6 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
     pair(nchunks - 4, std::false_type{}, std::false_type{}, std::false_type{});
     pair(nchunks - 2, std::false_type{}, std::true_type{}, std::false_type{});
 
-#ifdef SEDX_WINO_ABL_NOEPI
-    {   // keep every accumulator (and so every MFMA) alive
-      float sink = 0.0f;
-#pragma unroll
-      for (int q = 0; q < 8; ++q)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) sink += acc[q][r];
-      if (sink == 12345.678f) out[0] = sink;
-    }
-    return;
-#endif
     // ---- epilogue ----
     const int tr0 = t0 / 2;
 #pragma unroll
