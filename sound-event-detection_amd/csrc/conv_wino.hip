@@ -61,7 +61,10 @@ struct WinoGeom {
   static constexpr int A_SZ = KC * PLP;              // floats: [pixel][4 ch]
   static constexpr int W_SZ = 16 * KC * 32;          // floats: [p][h][n 32][ks]
   static constexpr int BUF = A_SZ + W_SZ;
-  static constexpr int NBUF = 3;                     // ring depth (4 and 6 measured: no change)
+#ifndef SEDX_WINO_NBUF
+#define SEDX_WINO_NBUF 3
+#endif
+  static constexpr int NBUF = TG == 4 ? SEDX_WINO_NBUF : 3;   // ring depth
   static constexpr int UW = W_SZ / 256;              // 1-KiB DMA units per chunk
   static constexpr int UA = PLP / 64;
   static constexpr int U = UW + UA;

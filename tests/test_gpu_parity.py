@@ -495,3 +495,37 @@ def test_config5_transformer_b256():
         e = err(full[k][idx], ref[k].numpy())
         print('config 5 B=256', k, 'max|d| =', e)
         assert e <= TOL
+
+
+@pytest.mark.parametrize('wino_block1', [0, 1])
+def test_winograd_block1_knob(wino_block1):
+    """SEDX_TUNE_WINO_BLOCK1: block 1 as the Winograd F = 64 launch fed by the
+    separate conv1 launch (1, the default) or as the direct fused kernel (0);
+    both within the Winograd bar of the oracle at the headline batch, with
+    identical thresholded events, and an odd-length clip (partial last tile
+    row, pooled rows dropped by floor) as close."""
+    from sedx import _lib, inference
+    wave = synth.make_waveforms(32, seconds=10.0, sample_rate=16000, seed=99)
+    m = build(GRU).set_precision('winograd').set_tuning(_lib.TUNE_WINO_BLOCK1, wino_block1)
+    got = run(m, wave)
+    ex = run(build(GRU).set_precision('exact'), wave)
+    ref = O.forward(O.full_state(synth.make_state_dict(GRU, seed=SEEDS[GRU])), GRU, wave=wave)
+    e = err(got['framewise_output'], ref['framewise_output'].numpy())
+    print('wino_block1=%d vs oracle %.3g' % (wino_block1, e))
+    assert e <= 2e-5
+    params = {'sed_high_threshold': 0.5, 'sed_low_threshold': 0.3, 'n_smooth': 10, 'n_salt': 10}
+    assert inference.events_from_framewise(got['framewise_output'], params) == \
+        inference.events_from_framewise(ex['framewise_output'], params)
+    odd = synth.make_waveforms(3, seconds=7.33, sample_rate=16000, seed=5)
+    ref_o = O.forward(O.full_state(synth.make_state_dict(GRU, seed=SEEDS[GRU])), GRU, wave=odd)
+    assert err(run(m, odd)['framewise_output'], ref_o['framewise_output'].numpy()) <= 2e-5
+
+
+def test_wino_block1_knob_errors():
+    """A bad value for the knob is a loud error, not a silent fallback."""
+    from sedx import _lib
+    m = build(GRU)
+    nat = m.native(torch.device('cuda', 0))
+    L = _lib.lib()
+    assert L.sedx_set_tuning(nat.h, _lib.TUNE_WINO_BLOCK1, 2) != 0
+    assert L.sedx_set_tuning(nat.h, _lib.TUNE_WINO_BLOCK1, 1) == 0
