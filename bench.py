@@ -400,6 +400,12 @@ def roofline(stage_ms, B, precision, T=1001):
             'traffic': traffic, 'traffic_unit': 'bytes/launch (HBM, rocprofv3 PMC)',
             'traffic_source': os.path.relpath(PROFILE_SUMMARY, REPO) if traffic is not None else None,
             'flops_per_launch': flops, 'avg_launch_ms': conv[dom],
+            # the same launch priced at the reference's algorithmic FLOPs
+            # (the direct conv's 2 B T F Cout 9 Cin): what a
+            # direct conv would have to sustain for this launch time
+            'flops_per_launch_algorithmic': flops / mul[dom],
+            'achieved_algorithmic': round(flops / mul[dom] / (conv[dom] * 1e-3) / 1e12, 2),
+            'frac_algorithmic': round(flops / mul[dom] / (conv[dom] * 1e-3) / 1e12 / peak, 4),
             'avg_launch_ms_rocprof': rocprof_ms,
             'mfma_busy_frac_pmc': mfma_util, 'clock_ghz_pmc': clock,
             'timing': 'avg_launch_ms: HIP events on the launch stream over the timed region '
