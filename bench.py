@@ -589,7 +589,7 @@ def main():
         extra['latency_b1'] = latency_b1(model, dev)
         notes = {'x3': 'opt-in arithmetic (operands narrowed to 16 significant bits), same workload',
                  'exact': 'fp32, direct 3x3 conv everywhere (bit-reproducible reference arithmetic), same workload',
-                 'winograd': 'fp32, blocks 2-4 as Winograd F(2x2,3x3), same workload'}
+                 'winograd': 'fp32, block 1 conv2 and blocks 2-4 as Winograd F(2x2,3x3), same workload'}
         for other in [p for p in ('exact', 'winograd', 'x3') if p != args.precision]:
             model.set_precision(other)
             extra['latency_b1_%s' % other] = latency_b1(model, dev)

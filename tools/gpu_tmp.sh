@@ -1,3 +1,10 @@
-cd $GRAFT_REPO_ROOT
-RUN=1 VARIANTS="full nb4 i3" BATCHES=32 REPS=30 bash tools/gpu_wino.sh 2>&1 | grep -E "==|total" || exit $?
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread -k "wino" > gpurun_out/t_wino.log 2>&1; rc=$?; grep -E "passed|failed" gpurun_out/t_wino.log | tail -2; exit $rc
+#!/bin/bash
+# scratch A/B of bench flags (one GPU call)
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+i=0
+for a in "--streams 2" "--streams 3" "--streams 1" "--streams 2 --no-pipeline"; do
+  i=$((i+1))
+  timeout -k 10 300 python bench.py --steps 30 --warmup 3 --no-cpu-baseline --no-side $a > gpurun_out/ab_$i.log 2>&1 || exit $?
+  python -c "import json; d=json.loads([l for l in open('gpurun_out/ab_$i.log') if l.startswith('{')][-1]); print('$a', d['value'], d['ms_per_step'])"
+done
