@@ -568,12 +568,25 @@ static void launch_wino_f(const float* in, int B, int T, int Cin, int Cout, cons
 void launch_conv3x3_wino(const float* in, int B, int T, int F, int Cin, int Cout, const float* U,
                          const float* bias, float* out, int epi, const float* zero16, float* trash, hipStream_t s) {
   if (Cin % 8 != 0 || Cin < 32 || Cout % 32 != 0 || B <= 0 || T <= 0) return note_launch_error(hipErrorInvalidValue);
-  switch (F) {
-    case 64: launch_wino_f<64>(in, B, T, Cin, Cout, U, bias, out, epi, zero16, trash, s); break;
-    case 32: launch_wino_f<32>(in, B, T, Cin, Cout, U, bias, out, epi, zero16, trash, s); break;
-    case 16: launch_wino_f<16>(in, B, T, Cin, Cout, U, bias, out, epi, zero16, trash, s); break;
-    case 8: launch_wino_f<8>(in, B, T, Cin, Cout, U, bias, out, epi, zero16, trash, s); break;
-    default: note_launch_error(hipErrorInvalidValue); break;
+  // the kernel's DMA offsets are 32-bit: batches whose input passes 2^31
+  // elements run as several launches over whole clips (same per-clip work,
+  // so the outputs do not depend on the split)
+  const int64_t in_clip = (int64_t)T * F * Cin;
+  const int64_t out_clip = epi == EPI_STORE ? (int64_t)T * F * Cout
+                           : epi == EPI_POOL2 ? (int64_t)(T / 2) * (F / 2) * Cout : (int64_t)T * Cout;
+  const int64_t bmax = (INT32_MAX - 1) / in_clip;
+  if (bmax < 1) return note_launch_error(hipErrorInvalidValue);
+  for (int64_t b0 = 0; b0 < B; b0 += bmax) {
+    const int bs = (int)std::min<int64_t>(bmax, B - b0);
+    const float* in_s = in + b0 * in_clip;
+    float* out_s = out + b0 * out_clip;
+    switch (F) {
+      case 64: launch_wino_f<64>(in_s, bs, T, Cin, Cout, U, bias, out_s, epi, zero16, trash, s); break;
+      case 32: launch_wino_f<32>(in_s, bs, T, Cin, Cout, U, bias, out_s, epi, zero16, trash, s); break;
+      case 16: launch_wino_f<16>(in_s, bs, T, Cin, Cout, U, bias, out_s, epi, zero16, trash, s); break;
+      case 8: launch_wino_f<8>(in_s, bs, T, Cin, Cout, U, bias, out_s, epi, zero16, trash, s); break;
+      default: return note_launch_error(hipErrorInvalidValue);
+    }
   }
 }
 

@@ -529,3 +529,16 @@ def test_wino_block1_knob_errors():
     L = _lib.lib()
     assert L.sedx_set_tuning(nat.h, _lib.TUNE_WINO_BLOCK1, 2) != 0
     assert L.sedx_set_tuning(nat.h, _lib.TUNE_WINO_BLOCK1, 1) == 0
+
+
+def test_winograd_batch_past_32bit_offsets():
+    """A batch whose block-1 activation passes 2^31 elements (530 x 10 s clips:
+    530 x 1001 x 64 x 64) runs the Winograd layers as several launches over
+    whole clips; every clip's outputs stay bit-identical to running it alone."""
+    m = build(GRU).set_precision('winograd')
+    wave = synth.make_waveforms(530, seconds=10.0, sample_rate=16000, seed=77)
+    full = run(m, wave)
+    for i in (0, 264, 529):
+        one = run(m, wave[i:i + 1])
+        assert np.array_equal(one['framewise_output'][0], full['framewise_output'][i]), i
+    torch.cuda.empty_cache()
