@@ -868,7 +868,7 @@ sedx_status sedx_finalize_weights(sedx_handle* h) {
     for (int t = 0; t < 9; ++t) c1wt[t * 64 + o] = c1w[o * 9 + t];
   add((void**)&W.c1_wt, c1wt.data(), c1wt.size() * 4);
   add((void**)&W.c1_b, c1b.data(), c1b.size() * 4);
-  std::vector<float> zeros(64, 0.f);
+  std::vector<float> zeros(1024, 0.f);   // >= Cin + 4 floats: the Winograd halo DMA steps through it
   add((void**)&W.zero, zeros.data(), zeros.size() * 4);
   std::vector<float> trash(64 * 128, 0.f);
   add((void**)&W.trash, trash.data(), trash.size() * 4);

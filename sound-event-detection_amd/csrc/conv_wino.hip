@@ -202,8 +202,35 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
     }
     asm volatile("" ::: "memory");
   };
-  int doff[G::UPW];
-  desc(b, t0, doff);
+  // the current item's unit sources at chunk 0 (a chunk adds a uniform step:
+  // 64 Cout floats for weight units, KC for halo units — a halo lane outside
+  // the clip steps through the zero block, >= Cin + 4 floats)
+  const float* dptr[G::UPW];
+  auto ptrs = [&](const int (&off)[G::UPW], int n0_) {
+#pragma unroll
+    for (int k = 0; k < G::UPW; ++k) {
+      const int u = wv + WAVES * k;
+      dptr[k] = u < G::UW ? U + 2 * n0_ + off[k] : (off[k] >= 0 ? in + off[k] : zero16);
+    }
+  };
+  auto dma_cur = [&](int chunk_, int buf_) {
+#pragma unroll
+    for (int k = 0; k < G::UPW; ++k) {
+      const int u = wv + WAVES * k;
+      if (u < G::U) {
+        const uint32_t m0_ =
+            (uint32_t)(size_t)(__attribute__((address_space(3))) float*)(smem + buf_ * G::BUF + dlds[k]);
+        const int64_t stp = u < G::UW ? (int64_t)64 * Cout : KC;
+        sedx_glds16(dptr[k] + chunk_ * stp, __builtin_amdgcn_readfirstlane(m0_));
+      }
+    }
+    asm volatile("" ::: "memory");
+  };
+  {
+    int doff[G::UPW];
+    desc(b, t0, doff);
+    ptrs(doff, n0);
+  }
 
   f32x16 acc[8];
 #pragma unroll
@@ -287,7 +314,7 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
   constexpr int S = EPI == EPI_FMEAN ? 4 : EPI == EPI_POOL2 ? 8 : 32;
   static_assert(G::VM_MIN * (NB - 2) + S <= 63, "vmcnt field");
 #pragma unroll
-  for (int c = 0; c < NB; ++c) dma(doff, n0, c, c);   // nchunks >= 8 (launcher)
+  for (int c = 0; c < NB; ++c) dma_cur(c, c);   // nchunks >= 8 (launcher)
   // S stores to trash: every item, the first included, then has S stores
   // between its chunk NB - 1 and chunk NB DMAs (a later item: the previous
   // item's epilogue), so all items wait alike
@@ -353,7 +380,7 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
       for (int r = 0; r < 16; ++r) acc[p][r] = 0.0f;
     auto issue = [&](int g, int bf) {
       if (g < nchunks) {
-        dma(doff, n0, g, bf);
+        dma_cur(g, bf);
       } else if (has_next) {
         int noff[G::UPW];
         desc(nb_, nt0, noff);
@@ -372,7 +399,7 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
       // prologue's) were issued after their DMAs
       if constexpr (MID) {
         wino_bar_n<G::VM_MIN * (NB - 2) + (FIRST ? S : 0)>();
-        dma(doff, n0, chunk + NB, buf);
+        dma_cur(chunk + NB, buf);
       } else {
         wino_bar<G::VM_MIN, NB - 2, FIRST ? S : 0>(has_next ? NB - 2 : max(0, min(NB - 2, nchunks - chunk - 2)));
         issue(chunk + NB, buf);
@@ -380,7 +407,7 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
       step(va, ua, b1, vb, ubv);
       if constexpr (MID) {
         wino_bar_n<G::VM_MIN * (NB - 2) + (FIRST ? S : 0)>();
-        dma(doff, n0, chunk + 1 + NB, b1);
+        dma_cur(chunk + 1 + NB, b1);
       } else {
         wino_bar<G::VM_MIN, NB - 2, FIRST ? S : 0>(has_next ? NB - 2 : max(0, min(NB - 2, nchunks - chunk - 3)));
         issue(chunk + 1 + NB, b1);
@@ -481,7 +508,11 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
     b = nb_;
     t0 = nt0;
     n0 = nn0;
-    desc(b, t0, doff);
+    {
+      int doff[G::UPW];
+      desc(b, t0, doff);
+      ptrs(doff, n0);
+    }
   }
 }
 

@@ -104,7 +104,7 @@ void launch_conv3x3(const float* in, int B, int T, int F, int Cin, int Cout,
 // pack_conv_wino (wf = BN-folded weights [Cout][Cin][9] in float64);
 // F in {64, 32, 16, 8}, Cout % 32 == 0 (F = 64: block 1's conv2, fed by
 // launch_conv1_nhwc).
-// trash: >= 64 x 128 floats of device scratch; out-of-range epilogue stores land
+// zero16 here: >= Cin + 4 floats of zeros; trash: >= 64 x 128 floats of device scratch; out-of-range epilogue stores land
 // there (every store is issued, so the persistent kernel's counted waits are exact).
 void launch_conv3x3_wino(const float* in, int B, int T, int F, int Cin, int Cout,
                          const float* U, const float* bias, float* out, int epi,

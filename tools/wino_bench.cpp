@@ -30,7 +30,7 @@ int main(int argc, char** argv) {
   }
   hipMalloc(&d_in, max_in * 4); hipMalloc(&d_o1, max_out * 4); hipMalloc(&d_o2, max_out * 4);
   hipMalloc(&d_bias, 512 * 4); hipMalloc(&d_wp, max_w * 4); hipMalloc(&d_u, max_w * 4);
-  hipMalloc(&d_zero, 256); hipMemset(d_zero, 0, 256);
+  hipMalloc(&d_zero, 4096); hipMemset(d_zero, 0, 4096);
   float* d_trash;
   hipMalloc(&d_trash, 64 * 128 * 4);
   hipEvent_t e0, e1;
