@@ -175,8 +175,9 @@ sedx_status sedx_forward_windows_vote(sedx_handle* h, const float* d_audio, int6
  *                       (v_mfma_f32_32x32x2_f32 / fp32 FMA): the reference's
  *                       arithmetic (pytorch/models.py:614-615, :663-670),
  *                       direct 3x3 convolution.
- *  SEDX_PRECISION_WINOGRAD  fp32 throughout as EXACT, with the six conv
- *                       layers of blocks 2-4 computed by Winograd F(2x2,3x3):
+ *  SEDX_PRECISION_WINOGRAD  fp32 throughout as EXACT, with block 1's conv2
+ *                       (SEDX_TUNE_WINO_BLOCK1) and the six conv layers of
+ *                       blocks 2-4 computed by Winograd F(2x2,3x3):
  *                       input / weight / output transforms and the 16
  *                       element-wise GEMMs all in fp32 (weights transformed
  *                       in float64, rounded once), 2.25x fewer multiplies;
