@@ -116,6 +116,13 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
   constexpr int ph = PH;
   using G = WinoGeom<F, TG>;
   constexpr int WAVES = G::WAVES;
+  // unit u = wv + WAVES k of this wave: a weight unit, a halo unit, or none.
+  // Folded at compile time where k alone decides (UW a multiple of WAVES:
+  // k < UW / WAVES weight, else halo; k < U / WAVES always present), so the
+  // per-chunk DMA issue has no branches but the last unit's presence check
+  static_assert(G::UW % WAVES == 0, "weight units a multiple of the waves");
+  auto is_w = [&](int k) { return (k + 1) * WAVES <= G::UW; };
+  auto present = [&](int k, int wv_) { return (k + 1) * WAVES <= G::U || wv_ + WAVES * k < G::U; };
   constexpr int CS = G::CS, KC = G::KC, FT = G::FT;
   extern __shared__ __attribute__((aligned(16))) float smem[];   // G::LDS_BYTES (dynamic: > 64 KiB)
 
@@ -166,7 +173,7 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
 #pragma unroll
   for (int k = 0; k < G::UPW; ++k) {
     const int u = wv + WAVES * k;
-    dlds[k] = u < G::UW ? G::A_SZ + 256 * u : 256 * (u - G::UW);
+    dlds[k] = is_w(k) ? G::A_SZ + 256 * u : 256 * (u - G::UW);
   }
   // a unit's source as a 32-bit element offset (from U + 2 n0 for weight
   // units, from in for halo units; -1: a pixel outside the clip, read from
@@ -176,10 +183,10 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
     for (int k = 0; k < G::UPW; ++k) {
       const int u = wv + WAVES * k;
       off[k] = -1;
-      if (u < G::UW) {
+      if (is_w(k)) {
         const int row = 4 * u + (lane >> 4);   // (p, h) row of 2 x 32 floats
         off[k] = row * 2 * Cout + 4 * (lane & 15);
-      } else if (u < G::U) {
+      } else if (present(k, wv)) {
         const int slot = 64 * (u - G::UW) + lane;
         const int q = slot / Q, rem = slot - q * Q;
         const int r = 2 * (rem / HC) + (q >> 1), c = 2 * (rem % HC) + (q & 1);
@@ -192,10 +199,10 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
 #pragma unroll
     for (int k = 0; k < G::UPW; ++k) {
       const int u = wv + WAVES * k;
-      if (u < G::U) {
+      if (present(k, wv)) {
         const uint32_t m0_ =
             (uint32_t)(size_t)(__attribute__((address_space(3))) float*)(smem + buf_ * G::BUF + dlds[k]);
-        const float* src = u < G::UW ? U + 2 * n0_ + off[k] + (int64_t)chunk_ * (64 * Cout)
+        const float* src = is_w(k) ? U + 2 * n0_ + off[k] + (int64_t)chunk_ * (64 * Cout)
                                      : (off[k] >= 0 ? in + off[k] + chunk_ * KC : zero16);
         sedx_glds16(src, __builtin_amdgcn_readfirstlane(m0_));
       }
@@ -210,17 +217,17 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
 #pragma unroll
     for (int k = 0; k < G::UPW; ++k) {
       const int u = wv + WAVES * k;
-      dptr[k] = u < G::UW ? U + 2 * n0_ + off[k] : (off[k] >= 0 ? in + off[k] : zero16);
+      dptr[k] = is_w(k) ? U + 2 * n0_ + off[k] : (off[k] >= 0 ? in + off[k] : zero16);
     }
   };
   auto dma_cur = [&](int chunk_, int buf_) {
 #pragma unroll
     for (int k = 0; k < G::UPW; ++k) {
       const int u = wv + WAVES * k;
-      if (u < G::U) {
+      if (present(k, wv)) {
         const uint32_t m0_ =
             (uint32_t)(size_t)(__attribute__((address_space(3))) float*)(smem + buf_ * G::BUF + dlds[k]);
-        const int64_t stp = u < G::UW ? (int64_t)64 * Cout : KC;
+        const int64_t stp = is_w(k) ? (int64_t)64 * Cout : KC;
         sedx_glds16(dptr[k] + chunk_ * stp, __builtin_amdgcn_readfirstlane(m0_));
       }
     }
