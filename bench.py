@@ -10,8 +10,8 @@ per GPU: BASELINE.json configs[1]), inputs already resident in HBM, weights
 random-init with the reference architecture.  The headline computes in fp32
 throughout (no operand narrower than fp32): every GEMM on fp32 operands with
 fp32 accumulation (v_mfma_f32_32x32x2_f32, GRU recurrence on fp32 MFMA), block
-1's conv direct, blocks 2-4's convs as Winograd F(2x2,3x3) with fp32
-transforms (--precision winograd).  For
+1's conv2 and blocks 2-4's convs as Winograd F(2x2,3x3) with fp32 transforms
+(--precision winograd, the library's default arithmetic).  For
 N > 1 (launched by torch.distributed.run, one process per GPU) every rank
 runs its own shard of clips (weak scaling) and the framewise outputs are
 gathered to rank 0 over RCCL inside each step — the path's only collective.
@@ -19,7 +19,7 @@ Rank 0 prints ONE JSON line.
 
 At N = 1 the line also carries, each with its own roofline:
   value_exact         the same workload with the direct fp32 conv everywhere
-                      (bit-reproducible; the library's default arithmetic)
+                      (the reference's operation order; sedx_set_precision EXACT)
   value_x3            the same workload with the opt-in 3xbf16-split MFMA
   configs.config3     Cnn_9layers_Transformer_FrameAtt logmel 16k, B=32
   configs.config4     Cnn_9layers_Gru_FrameAtt gammatone 32k, B=32 (float64
@@ -126,6 +126,15 @@ def cpu_info():
             'host_physical_cores': len(cores) or None}
 
 
+def cpu_threads():
+    """Host CPUs this process may run on (the GPU box's lease pins a share of
+    the machine): the oracle runs one torch thread per CPU it may use."""
+    try:
+        return len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return os.cpu_count() or 1
+
+
 def cpu_baseline(name, model, dev, seconds, B=32):
     """Clip mode: the oracle forward on B=32 clips per iteration (1 warm-up,
     then timed iterations for ~``seconds``).  The same clips go through the
@@ -133,6 +142,7 @@ def cpu_baseline(name, model, dev, seconds, B=32):
     (frame_prediction_to_event_prediction_v2 on both sides) and the smallest
     distance of any oracle value to a threshold."""
     from oracle import sed_oracle as O
+    torch.set_num_threads(cpu_threads())
     sd = O.full_state(synth.make_state_dict(name, seed=0), '16k')
     wave = synth.make_waveforms(B, seconds=10.0, sample_rate=16000, seed=7)
     O.forward(sd, name, wave=wave[:2])  # warm-up (allocator, threads)
@@ -146,6 +156,7 @@ def cpu_baseline(name, model, dev, seconds, B=32):
             break
     rate = B * len(ts) / sum(ts)
     out = {'value': round(rate, 3), 'unit': 'clips/s', 'cores': torch.get_num_threads(), 'kind': 'port',
+           'cpus_allowed': cpu_threads(),
            'ms_per_clip_p50': round(statistics.median(ts) / B * 1e3, 2),
            'sample': '%d iterations of B=%d x 10 s clips (clip mode, %.1f s) through oracle/sed_oracle.py '
                      'forward (torch fp32, the reference op sequence) on %d host threads'
@@ -366,61 +377,83 @@ def profiled(kernel):
             round(util, 4) if util else None, round(clk, 3) if clk else None)
 
 
-def roofline(stage_ms, B, precision, T=1001):
-    """MFMA roofline of the dominant conv launch: algorithmic FLOPs per launch
-    (2 B T F Cout 9 Cin, + the fused block-1 conv1 2 B T 64 64 9 for b1c2) over
-    its HIP-event launch time in the timed region.  Profile-derived fields
-    (traffic, rocprof time, MFMA busy) come from the committed summary of the
-    B=32, 10 s shapes only."""
-    conv = {s: stage_ms[s] for s in CONV_STAGES}
+def roofline(stage_ms, B, precision, T=1001, iso_ms=None):
+    """MFMA roofline of the dominant conv launch.
+
+    achieved = FLOPs the launch executes on the matrix pipe (direct conv:
+    2 B T F Cout 9 Cin, + the fused block-1 conv1 2 B T 64 64 9 for b1c2;
+    Winograd layers: 16/36 of the direct conv's) / its launch time, with the
+    launch time from HIP events on the launch stream measured live in this
+    run ONE BATCH AT A TIME (``iso_ms``: sedx_set_profiling mode 1; the
+    rocprofv3 summary of the same single-stream work is committed under
+    profiles/ and must agree).  The same launch's interval inside the
+    two-stream timed region (it then shares the chip with the previous
+    batch's GRU / head) is reported beside it (``*_timed_region``), and the
+    direct-conv-equivalent rate (what a direct conv would need for this time;
+    can exceed the peak for Winograd) as ``direct_conv_equiv_tflops``.
+    Profile-derived fields (traffic, rocprof time, MFMA busy) come from the
+    committed summary of the B=32, 10 s shapes only."""
+    conv = {s_: stage_ms[s_] for s_ in CONV_STAGES}
     dom = max(conv, key=conv.get)
     wino = precision == 'winograd'
-    # matrix-pipe FLOPs the launch executes (Winograd layers: 16/36 of the
-    # direct conv's) — the roofline's numerator; the direct-conv equivalent
-    # is reported beside it
     mul = {st: (WINO_MUL if wino and st in wino_stages() else 1.0) for st in CONV_STAGES}
     flops = conv_flops(dom, B, T) * mul[dom]
     if dom == 'b1c2' and fused_block1(precision):
         flops += 2.0 * B * T * 64 * 64 * 9      # conv1 (Cin 1 -> 64) computed inside the launch
-    achieved = flops / (conv[dom] * 1e-3) / 1e12
     peak = PEAK_TF[precision]
+    t_iso = iso_ms.get(dom) if iso_ms else None
+    t = t_iso if t_iso else conv[dom]
+    achieved = flops / (t * 1e-3) / 1e12
     conv1 = 2.0 * B * T * 64 * 64 * 9
     total = sum(conv_flops(st, B, T) * mul[st] for st in CONV_STAGES) + conv1
     total_direct = sum(conv_flops(st, B, T) for st in CONV_STAGES) + conv1
     conv_ms = sum(conv.values()) + stage_ms.get('b1c1', 0.0)
     kname = conv_kernel_name(dom, precision)
     traffic, rocprof_ms, mfma_util, clock = profiled(kname) if (B, T) == (32, 1001) else (None,) * 4
-    return {'bound': 'mfma', 'kernel': '%s (%s)' % (kname, dom),
-            'arith': {'exact': 'fp32 MFMA v_mfma_f32_32x32x2_f32 (f32 in, f32 acc)',
-                      'winograd': 'fp32 MFMA v_mfma_f32_32x32x2_f32 (f32 in, f32 acc); Winograd F(2x2,3x3) '
-                                  'layers (%s) counted as executed FLOPs (16/36 of direct)' % ', '.join(wino_stages()),
-                      'x3': '3xbf16-split MFMA 32x32x16, f32 acc (peak = bf16 dense 2.5 PF / 3)'}[precision],
-            'achieved': round(achieved, 2), 'peak': round(peak, 1), 'unit': 'TFLOP/s',
-            'frac': round(achieved / peak, 4),
-            'traffic': traffic, 'traffic_unit': 'bytes/launch (HBM, rocprofv3 PMC)',
-            'traffic_source': os.path.relpath(PROFILE_SUMMARY, REPO) if traffic is not None else None,
-            'flops_per_launch': flops, 'avg_launch_ms': conv[dom],
-            # the same launch priced at the reference's algorithmic FLOPs
-            # (SURVEY §8(d): the direct conv's 2 B T F Cout 9 Cin): what a
-            # direct conv would have to sustain for this launch time
-            'flops_per_launch_algorithmic': flops / mul[dom],
-            'achieved_algorithmic': round(flops / mul[dom] / (conv[dom] * 1e-3) / 1e12, 2),
-            'frac_algorithmic': round(flops / mul[dom] / (conv[dom] * 1e-3) / 1e12 / peak, 4),
-            'avg_launch_ms_rocprof': rocprof_ms,
-            'mfma_busy_frac_pmc': mfma_util, 'clock_ghz_pmc': clock,
-            'timing': 'avg_launch_ms: HIP events on the launch stream over the timed region '
-                      '(one event set per forward, all steps averaged); avg_launch_ms_rocprof: '
-                      'rocprofv3 --kernel-trace --stats of this bench (--streams 1 --no-side), committed summary',
-            'conv_stack_tflops': round(total / (conv_ms * 1e-3) / 1e12, 2),
-            'conv_stack_frac': round(total / (conv_ms * 1e-3) / 1e12 / peak, 4),
-            'conv_stack_direct_equiv_tflops': round(total_direct / (conv_ms * 1e-3) / 1e12, 2),
-            'conv_stack_ms': round(conv_ms, 4)}
+    direct = flops / mul[dom]
+    out = {'bound': 'mfma', 'kernel': '%s (%s)' % (kname, dom),
+           'arith': {'exact': 'fp32 MFMA v_mfma_f32_32x32x2_f32 (f32 in, f32 acc)',
+                     'winograd': 'fp32 MFMA v_mfma_f32_32x32x2_f32 (f32 in, f32 acc); Winograd F(2x2,3x3) '
+                                 'layers (%s) counted as executed FLOPs (16/36 of direct)' % ', '.join(wino_stages()),
+                     'x3': '3xbf16-split MFMA 32x32x16, f32 acc (peak = bf16 dense 2.5 PF / 3)'}[precision],
+           'achieved': round(achieved, 2), 'peak': round(peak, 1), 'unit': 'TFLOP/s',
+           'frac': round(achieved / peak, 4),
+           'traffic': traffic, 'traffic_unit': 'bytes/launch (HBM, rocprofv3 PMC)',
+           'traffic_source': os.path.relpath(PROFILE_SUMMARY, REPO) if traffic is not None else None,
+           'flops_per_launch': flops, 'avg_launch_ms': round(t, 4),
+           'timing': ('avg_launch_ms: HIP events on the launch stream, one batch at a time, measured live in this '
+                      'run (sedx_set_profiling 1)' if t_iso else
+                      'avg_launch_ms: HIP events on the launch stream over the timed region'),
+           'avg_launch_ms_timed_region': conv[dom],
+           'achieved_timed_region': round(flops / (conv[dom] * 1e-3) / 1e12, 2),
+           'frac_timed_region': round(flops / (conv[dom] * 1e-3) / 1e12 / peak, 4),
+           'timed_region_note': 'the launch interval inside the two-stream timed region (one event set per '
+                                'forward, all steps averaged): it shares the chip with the previous batch\'s '
+                                'GRU / head and the next batch\'s frontend',
+           'avg_launch_ms_rocprof': rocprof_ms,
+           'frac_rocprof': round(flops / (rocprof_ms * 1e-3) / 1e12 / peak, 4) if rocprof_ms else None,
+           'mfma_busy_frac_pmc': mfma_util, 'clock_ghz_pmc': clock,
+           'rocprof_source': ('rocprofv3 --kernel-trace --stats of bench.py --streams 1 --no-side, %s'
+                              % os.path.relpath(PROFILE_SUMMARY, REPO)) if rocprof_ms else None,
+           # the reference's algorithmic FLOPs (SURVEY §8(d): the direct conv's)
+           # over the same time: a rate, not a roofline fraction (> peak for
+           # Winograd, which executes 16/36 of the multiplies)
+           'flops_per_launch_direct_conv': direct,
+           'direct_conv_equiv_tflops': round(direct / (t * 1e-3) / 1e12, 2),
+           'conv_stack_tflops': round(total / (conv_ms * 1e-3) / 1e12, 2),
+           'conv_stack_frac': round(total / (conv_ms * 1e-3) / 1e12 / peak, 4),
+           'conv_stack_direct_equiv_tflops': round(total_direct / (conv_ms * 1e-3) / 1e12, 2),
+           'conv_stack_ms': round(conv_ms, 4)}
+    return out
 
 
 # ---------------------------------------------------------------------------
 # legs
 # ---------------------------------------------------------------------------
-def clip_leg(model, wave, args, world, rank, dev, precision):
+def clip_leg(model, wave, args, world, rank, dev, precision, isolated=False):
+    """Throughput + per-stage timed-region times + device p50/p99; with
+    ``isolated`` also the per-stage times one batch at a time (the roofline's
+    launch time)."""
     model.set_precision(precision)
     B = wave.shape[0]
 
@@ -432,7 +465,8 @@ def clip_leg(model, wave, args, world, rank, dev, precision):
 
     value, elapsed, stage_ms = measure(step, args, world, dev, model, B)
     p50, p99 = latency(step, B, max(5, min(args.steps, 20)))
-    return value, elapsed, stage_ms, p50, p99
+    iso = stage_times_isolated(model, wave, dev, max(3, min(args.steps, 10))) if isolated else None
+    return value, elapsed, stage_ms, p50, p99, iso
 
 
 def gamma_leg(args, dev, precision):
@@ -450,6 +484,9 @@ def gamma_leg(args, dev, precision):
             m(inference.gamma_features(m, audio))
 
     value, elapsed, stage_ms = measure(step, args, 1, dev, m, B)
+    with torch.no_grad():
+        feats = inference.gamma_features(m, audio)
+    iso = stage_times_isolated(m, feats, dev, max(3, min(args.steps, 10)))
     # gamma frontend alone, timed with torch events on the current stream (its
     # kernels are launched on that stream)
     for _ in range(2):
@@ -469,7 +506,7 @@ def gamma_leg(args, dev, precision):
                         '(float64 gammatone features + forward)' % B,
             'value': round(value, 2), 'unit': 'clips/s', 'dtype': DTYPE[precision] + '; gammatone frontend f64',
             'ms_per_step': round(elapsed / args.steps * 1e3, 4),
-            'roofline': roofline(stage_ms, B, precision, T=T),
+            'roofline': roofline(stage_ms, B, precision, T=T, iso_ms=iso),
             'gamma_frontend': {'ms_per_batch': round(fe_ms, 4), 'bound': 'fp64',
                                'achieved': round(flops / (fe_ms * 1e-3) / 1e12, 3), 'peak': PEAK_FP64_TF,
                                'unit': 'TFLOP/s (f64)', 'frac': round(flops / (fe_ms * 1e-3) / 1e12 / PEAK_FP64_TF, 4),
@@ -543,9 +580,12 @@ def main():
     B = args.batch
     wave = torch.from_numpy(synth.make_waveforms(B, 10.0, 16000, seed=1234 + rank)).to(dev)
 
+    side = world == 1 and rank == 0 and not args.no_side and args.mode == 'clip'
+    iso_ms = None
     if args.mode == 'clip':
-        value, elapsed, stage_ms, p50_dev, p99_dev = clip_leg(model, wave, args, world, rank, dev, args.precision)
-        roof = roofline(stage_ms, B, args.precision)
+        value, elapsed, stage_ms, p50_dev, p99_dev, iso_ms = clip_leg(model, wave, args, world, rank, dev,
+                                                                     args.precision, isolated=side)
+        roof = roofline(stage_ms, B, args.precision, iso_ms=iso_ms)
     else:
         model.set_precision(args.precision)
         wl = window_leg(model, wave, args, dev, args.precision)
@@ -560,17 +600,8 @@ def main():
     p50, p99 = latency(h2h, B, max(5, min(args.steps, 20))) if args.mode == 'clip' else (None, None)
 
     extra = {}
-    if world == 1 and rank == 0 and not args.no_side and args.mode == 'clip':
-        extra['stage_ms_isolated'] = stage_times_isolated(model, wave, dev, max(3, min(args.steps, 10)))
-        if roof is not None:
-            # the same launch one batch at a time (no other batch's GRU / head /
-            # frontend sharing the chip): the kernel's own rate beside the
-            # timed-region figure above
-            dom = roof['kernel'].rsplit('(', 1)[-1].rstrip(')')
-            iso = extra['stage_ms_isolated'].get(dom)
-            if iso:
-                roof['avg_launch_ms_isolated'] = iso
-                roof['frac_isolated'] = round(roof['flops_per_launch'] / (iso * 1e-3) / 1e12 / roof['peak'], 4)
+    if side:
+        extra['stage_ms_isolated'] = iso_ms
         if extra['stage_ms_isolated'].get('frontend'):
             fe = extra['stage_ms_isolated']['frontend']
             extra['frontend_roofline'] = {
@@ -594,24 +625,24 @@ def main():
             model.set_precision(other)
             extra['latency_b1_%s' % other] = latency_b1(model, dev)
             model.set_precision(args.precision)
-            v2, e2, st2, p2, _ = clip_leg(model, wave, args, 1, 0, dev, other)
+            v2, e2, st2, p2, _, iso2 = clip_leg(model, wave, args, 1, 0, dev, other, isolated=True)
             extra['value_%s' % other] = {'value': round(v2, 2), 'unit': 'clips/s', 'dtype': DTYPE[other],
                                          'ms_per_step': round(e2 / args.steps * 1e3, 4),
                                          'ms_per_clip_p50_device': round(p2, 4),
-                                         'roofline': roofline(st2, B, other), 'stage_ms': st2,
+                                         'roofline': roofline(st2, B, other, iso_ms=iso2), 'stage_ms': st2,
                                          'note': notes[other]}
         model.set_precision(args.precision)
         cfgs = {}
         if args.model == 'gru':
             trf = build_model(MODEL_NAMES['transformer'], dev)
-            v3, e3, st3, p3, _ = clip_leg(trf, wave, args, 1, 0, dev, args.precision)
+            v3, e3, st3, p3, _, iso3 = clip_leg(trf, wave, args, 1, 0, dev, args.precision, isolated=True)
             cfgs['config3'] = {'workload': 'Cnn_9layers_Transformer_FrameAtt logmel 16k, %d x 10 s clips '
                                            'per step (clip mode)' % B,
                                'metric': METRICS['transformer'],
                                'value': round(v3, 2), 'unit': 'clips/s', 'dtype': DTYPE[args.precision],
                                'ms_per_step': round(e3 / args.steps * 1e3, 4),
                                'ms_per_clip_p50_device': round(p3, 4),
-                               'roofline': roofline(st3, B, args.precision), 'stage_ms': st3}
+                               'roofline': roofline(st3, B, args.precision, iso_ms=iso3), 'stage_ms': st3}
             del trf
         cfgs['config4'] = gamma_leg(args, dev, args.precision)
         cfgs['window_mode'] = window_leg(model, wave, args, dev, args.precision)
@@ -646,6 +677,8 @@ def main():
             'ms_per_clip_p50_device': round(p50_dev, 4) if p50_dev is not None else None,
             'ms_per_clip_p99_device': round(p99_dev, 4) if p99_dev is not None else None,
             'roofline': roof, 'cpu_baseline': cpu, 'stage_ms': stage_ms,
+            # the libsedx.so this run loaded (SEDX_PKG selects another build for A/B runs)
+            'library': os.path.relpath(_lib.LIB_PATH, REPO), 'library_version': _lib.lib().sedx_version().decode(),
         }
         line.update(extra)
         if cpu:

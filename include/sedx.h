@@ -171,11 +171,11 @@ sedx_status sedx_forward_windows_vote(sedx_handle* h, const float* d_audio, int6
 /* Arithmetic of the GEMM-shaped work: the 9-layer conv stack (96.8 % of the
  * FLOPs), the GRU input projection and recurrence, the MHA projections and
  * the AttBlock projection.
- *  SEDX_PRECISION_EXACT (default) fp32 operands, fp32 accumulation
+ *  SEDX_PRECISION_EXACT  fp32 operands, fp32 accumulation
  *                       (v_mfma_f32_32x32x2_f32 / fp32 FMA): the reference's
  *                       arithmetic (pytorch/models.py:614-615, :663-670),
  *                       direct 3x3 convolution.
- *  SEDX_PRECISION_WINOGRAD  fp32 throughout as EXACT, with block 1's conv2
+ *  SEDX_PRECISION_WINOGRAD (default)  fp32 throughout as EXACT, with block 1's conv2
  *                       (SEDX_TUNE_WINO_BLOCK1) and the six conv layers of
  *                       blocks 2-4 computed by Winograd F(2x2,3x3):
  *                       input / weight / output transforms and the 16

@@ -40,7 +40,7 @@ struct DevWeights {
   float* c1_w = nullptr;
   float* c1_wt = nullptr;
   float* c1_b = nullptr;
-  float* zero = nullptr;   // 256 zero bytes (LDS-DMA source of out-of-clip halo pixels)
+  float* zero = nullptr;   // ZERO_BLOCK_FLOATS zeros (LDS-DMA source of out-of-clip halo pixels)
   float* trash = nullptr;  // 32 KB write-only scratch (the Winograd kernel's dummy / out-of-range stores)
   float* wp[8] = {};    // packed conv weights: block k conv j -> index 2(k-1)+(j-1); [0] unused
   float* cb[8] = {};    // folded biases
@@ -85,7 +85,7 @@ struct sedx_handle {
   void* ws = nullptr;        // cached workspace
   size_t ws_bytes = 0;
   // optional per-stage timing (sedx_set_profiling): events at stage boundaries
-  int precision = SEDX_PRECISION_EXACT;   // GEMM arithmetic (sedx_set_precision)
+  int precision = SEDX_PRECISION_WINOGRAD;   // GEMM arithmetic (sedx_set_precision; the default is fp32 Winograd)
   int gru_kernel = SEDX_GRU_KERNEL_COOP;   // sedx_set_tuning
   int gru_handoff = SEDX_GRU_HANDOFF_AUTO;
   int wino_block1 = 1;                     // SEDX_TUNE_WINO_BLOCK1
@@ -101,6 +101,11 @@ struct sedx_handle {
   bool pipelined = false;
   bool conv_done_recorded = false;
   hipEvent_t conv_done = nullptr;
+  // host-mapped word the GRU kernel ORs a failure code into when a bounded
+  // hand-off spin times out (that forward's outputs are NaN); the next
+  // forward / sedx_stage_times turns it into SEDX_EHIP
+  unsigned* gru_err_host = nullptr;
+  unsigned* gru_err_dev = nullptr;
   hipEvent_t ev[SEDX_N_STAGES + 1] = {};
   bool ev_recorded[SEDX_N_STAGES + 1] = {};
   // profiling mode 2 (accumulate): every forward takes its own event set from
@@ -181,8 +186,6 @@ sedx_status fail(sedx_handle* h, sedx_status st, const char* fmt, ...) {
       return fail(h, SEDX_EHIP, "%s failed: %s", #expr, hipGetErrorString(e_));         \
   } while (0)
 
-// errors of the launches just issued: preparation failures noted by
-// launch_info (sedx_internal.h) first, then the runtime's launch error
 // sedx_set_capture: stage `stage` just wrote `n` floats at `src`
 void capture(sedx_handle* h, int stage, const float* src, size_t n, hipStream_t s) {
   if (h->cap_stage != stage || !h->cap_buf) return;
@@ -191,11 +194,23 @@ void capture(sedx_handle* h, int stage, const float* src, size_t n, hipStream_t 
     note_launch_error(hipErrorInvalidValue);
 }
 
+// errors of the launches just issued: preparation failures noted by
+// launch_info (sedx_internal.h) first, then the runtime's launch error
 sedx_status launch_status(sedx_handle* h) {
   const hipError_t pe = take_launch_error();
   if (pe != hipSuccess) return fail(h, SEDX_EHIP, "kernel launch preparation failed: %s", hipGetErrorString(pe));
   const hipError_t le = hipGetLastError();
   if (le != hipSuccess) return fail(h, SEDX_EHIP, "kernel launch failed: %s", hipGetErrorString(le));
+  return SEDX_OK;
+}
+
+// a GRU hand-off of an earlier forward timed out (its outputs were NaN)
+sedx_status check_async_error(sedx_handle* h) {
+  if (!h->gru_err_host) return SEDX_OK;
+  const unsigned code = __atomic_exchange_n(h->gru_err_host, 0u, __ATOMIC_ACQ_REL);
+  if (code)
+    return fail(h, SEDX_EHIP, "a GRU recurrence hand-off of an earlier forward timed out (code %u): its "
+                              "outputs were NaN", code);
   return SEDX_OK;
 }
 
@@ -413,7 +428,7 @@ sedx_status run_body(sedx_handle* h, int64_t B, const Geometry& g, float* ws, co
       launch_gru(G, iB, (int)g.T3, w.whhT, w.bhh, Hs, s);
     else
       launch_gru_coop(G, iB, (int)g.T3, w.whh, w.bhh, Hs, LG + align_up((size_t)M * h->nac), !x3,
-                      h->gru_handoff == SEDX_GRU_HANDOFF_AUTO, s);
+                      h->gru_handoff == SEDX_GRU_HANDOFF_AUTO, h->gru_err_dev, s);
   } else {
     linear(S, w.wqkv, w.wqkv_x3, 1536, 128, w.bqkv, G, 0);
     launch_mha(G, iB, (int)g.T3, O, s);
@@ -433,7 +448,7 @@ sedx_status run_body(sedx_handle* h, int64_t B, const Geometry& g, float* ws, co
 struct WinGeom {
   int n_win = 0;
   int64_t win_samples = 0;
-  int64_t start[64];
+  std::vector<int64_t> start;   // sample offset of every window (the device table repeats this sequence)
   int64_t clip_len = 0;     // valid samples backing each clip
   int step = 0, interval = 0, sd = 0;
   int64_t Tw = 0, N = 0;
@@ -452,9 +467,13 @@ sedx_status window_geometry(const sedx_handle* h, int64_t L_clip, float sample_d
   const double duration = (double)L_clip / sr;
   double start = 0.0, end = 0.0;
   int n = 0;
+  wg->start.clear();
+  // unbounded like the reference's loop; the window count is limited only by
+  // the 32-bit item indexing of the launches (checked by the callers per batch)
   while (end <= duration) {
-    if (n >= 64) return fail(hm, SEDX_EINVAL, "more than 64 windows per clip");
-    wg->start[n++] = (int64_t)(start * sr);
+    if (n >= (1 << 24)) return fail(hm, SEDX_EINVAL, "too many windows per clip");
+    wg->start.push_back((int64_t)(start * sr));
+    ++n;
     start += ov;
     end = start + sd;
   }
@@ -497,7 +516,9 @@ T* carve(char*& p, size_t n) {
 // ============================================================================
 extern "C" {
 
-const char* sedx_version(void) { return "sedx 0.2 (gfx950: fp32 MFMA exact + 3xbf16-split MFMA)"; }
+const char* sedx_version(void) {
+  return "sedx 0.3 (gfx950: fp32 MFMA exact direct conv | fp32 Winograd F(2x2,3x3) | 3xbf16-split MFMA)";
+}
 
 sedx_status sedx_set_precision(sedx_handle* h, int32_t mode) {
   if (!h) return SEDX_EINVAL;
@@ -577,6 +598,7 @@ void sedx_destroy(sedx_handle* h) {
     if (h->conv_done) (void)hipEventDestroy(h->conv_done);
     if (h->blob) (void)hipFree(h->blob);
     if (h->ws) (void)hipFree(h->ws);
+    if (h->gru_err_host) (void)hipHostFree(h->gru_err_host);
   }
   delete h;
 }
@@ -868,7 +890,7 @@ sedx_status sedx_finalize_weights(sedx_handle* h) {
     for (int t = 0; t < 9; ++t) c1wt[t * 64 + o] = c1w[o * 9 + t];
   add((void**)&W.c1_wt, c1wt.data(), c1wt.size() * 4);
   add((void**)&W.c1_b, c1b.data(), c1b.size() * 4);
-  std::vector<float> zeros(1024, 0.f);   // >= Cin + 4 floats: the Winograd halo DMA steps through it
+  std::vector<float> zeros(ZERO_BLOCK_FLOATS, 0.f);   // >= Cin + 4 floats: the Winograd halo DMA steps through it
   add((void**)&W.zero, zeros.data(), zeros.size() * 4);
   std::vector<float> trash(64 * 128, 0.f);
   add((void**)&W.trash, trash.data(), trash.size() * 4);
@@ -925,6 +947,15 @@ sedx_status sedx_finalize_weights(sedx_handle* h) {
     off += (it.bytes + 255) & ~size_t(255);
   }
   HIP_TRY(h, hipMemcpy(h->blob, host.data(), total, hipMemcpyHostToDevice));
+  if (!h->gru_err_host) {
+    void* p = nullptr;
+    HIP_TRY(h, hipHostMalloc(&p, 64, hipHostMallocMapped | hipHostMallocCoherent));
+    h->gru_err_host = static_cast<unsigned*>(p);
+    *h->gru_err_host = 0;
+    void* d = nullptr;
+    HIP_TRY(h, hipHostGetDevicePointer(&d, p, 0));
+    h->gru_err_dev = static_cast<unsigned*>(d);
+  }
   h->finalized = true;
   return SEDX_OK;
 }
@@ -967,6 +998,7 @@ sedx_status sedx_stage_times(sedx_handle* h, float* ms, int32_t capacity, int32_
   *n_stages = SEDX_N_STAGES;
   if (!h->profiling) return fail(h, SEDX_ESTATE, "profiling is off");
   DeviceGuard dg(h->device);
+  if (sedx_status e = check_async_error(h)) return e;
   if (h->profiling == 2) {
     fold_ev_pool(h);
     for (int i = 0; i < SEDX_N_STAGES; ++i) {
@@ -1009,6 +1041,7 @@ static sedx_status forward_wave(sedx_handle* h, const float* d_wave, const int16
                                 void* d_workspace, size_t workspace_bytes, void* stream) {
   if (!h) return SEDX_EINVAL;
   if (!h->finalized) return fail(h, SEDX_ESTATE, "weights not finalised");
+  if (sedx_status e = check_async_error(h)) return e;
   if (h->cfg.feature_type != SEDX_FEATURE_LOGMEL)
     return fail(h, SEDX_EINVAL, "gamma models take features: use sedx_forward_features");
   if ((!d_wave && !d_wave16) || !d_framewise || !d_clipwise || B <= 0)
@@ -1032,7 +1065,7 @@ static sedx_status forward_wave(sedx_handle* h, const float* d_wave, const int16
   p.clip_stride = L;
   p.n_clips = (int32_t)B;
   p.n_win = 1;
-  p.win_start[0] = 0;
+  p.win_start = nullptr;
   p.clip_len = L;
   p.sig_len = L;
   p.T = (int32_t)g.T;
@@ -1074,6 +1107,7 @@ sedx_status sedx_forward_features(sedx_handle* h, const float* d_feat, int64_t B
                                   void* d_workspace, size_t workspace_bytes, void* stream) {
   if (!h) return SEDX_EINVAL;
   if (!h->finalized) return fail(h, SEDX_ESTATE, "weights not finalised");
+  if (sedx_status e = check_async_error(h)) return e;
   if (!d_feat || !d_framewise || !d_clipwise || B <= 0 || T <= 0)
     return fail(h, SEDX_EINVAL, "null pointer or empty batch");
   const Geometry g = geometry_from_T(h, T);
@@ -1095,6 +1129,7 @@ sedx_status sedx_gamma_features(sedx_handle* h, const float* d_audio, int64_t B,
                                 size_t workspace_bytes, void* stream) {
   if (!h) return SEDX_EINVAL;
   if (!h->finalized) return fail(h, SEDX_ESTATE, "weights not finalised");
+  if (sedx_status e = check_async_error(h)) return e;
   if (h->cfg.feature_type != SEDX_FEATURE_GAMMA)
     return fail(h, SEDX_EINVAL, "handle was not created with feature_type=gamma");
   if (L < h->g_nfft) return fail(h, SEDX_EINVAL, "clip shorter than the gammatone FFT");
@@ -1135,8 +1170,13 @@ sedx_status sedx_gamma_features(sedx_handle* h, const float* d_audio, int64_t B,
 }
 
 sedx_status sedx_gamma_workspace_size(const sedx_handle* h, int64_t B, int64_t L, size_t* bytes) {
-  if (!h || !bytes || B <= 0) return SEDX_EINVAL;
-  if (h->cfg.feature_type != SEDX_FEATURE_GAMMA || !h->finalized || L < h->g_nfft) return SEDX_EINVAL;
+  if (!h) return SEDX_EINVAL;
+  sedx_handle* hm = const_cast<sedx_handle*>(h);   // sedx_last_error's message only
+  if (!bytes || B <= 0) return fail(hm, SEDX_EINVAL, "null size pointer or empty batch");
+  if (h->cfg.feature_type != SEDX_FEATURE_GAMMA)
+    return fail(hm, SEDX_EINVAL, "handle was not created with feature_type=gamma");
+  if (!h->finalized) return fail(hm, SEDX_ESTATE, "weights not finalised");
+  if (L < h->g_nfft) return fail(hm, SEDX_EINVAL, "clip shorter than the gammatone FFT");
   *bytes = gamma_workspace_bytes(B, 1 + (L - h->g_nfft) / h->g_hop, h->g_nfft);
   return SEDX_OK;
 }
@@ -1157,9 +1197,10 @@ sedx_status sedx_window_geometry(const sedx_handle* h, int64_t L_clip, float sam
 static size_t window_ws_bytes(const sedx_handle* h, int64_t n_clips, const WinGeom& wg) {
   const int64_t items = n_clips * wg.n_win;
   const WsLayout l = ws_layout(h, items, wg.g);
-  // + per-window framewise, clipwise and (vote mode) the f64 binarisation thresholds
+  // + per-window framewise, clipwise, (vote mode) the f64 binarisation
+  // thresholds and the window table (int64 per window)
   const size_t extra = (size_t)items * (wg.Tw * h->cfg.classes_num + h->cfg.classes_num) + 2 * h->cfg.classes_num +
-                       256;
+                       2 * (size_t)wg.n_win + 4 * 64;
   return l.total_bytes + extra * sizeof(float);
 }
 
@@ -1170,6 +1211,7 @@ static sedx_status forward_windows_impl(sedx_handle* h, const float* d_audio, in
                                         void* d_workspace, size_t workspace_bytes, void* stream) {
   if (!h) return SEDX_EINVAL;
   if (!h->finalized) return fail(h, SEDX_ESTATE, "weights not finalised");
+  if (sedx_status e = check_async_error(h)) return e;
   if (h->cfg.feature_type != SEDX_FEATURE_LOGMEL)
     return fail(h, SEDX_EINVAL, "windowed inference needs a logmel model");
   if (!d_audio || !d_merged || n_clips <= 0) return fail(h, SEDX_EINVAL, "null pointer or empty batch");
@@ -1192,13 +1234,15 @@ static sedx_status forward_windows_impl(sedx_handle* h, const float* d_audio, in
   float* fw = ws + l.total_bytes / sizeof(float);
   float* clip = fw + align_up((size_t)items * wg.Tw * C);
   double* vthr = reinterpret_cast<double*>(clip + align_up((size_t)items * C));
+  int64_t* wstart = reinterpret_cast<int64_t*>(reinterpret_cast<float*>(vthr) + align_up(2 * (size_t)C));
+  launch_window_starts(wg.n_win, (double)overlap_value, h->cfg.sample_rate, wstart, s);
   if (h_vote_thres) HIP_TRY(h, hipMemcpyAsync(vthr, h_vote_thres, C * sizeof(double), hipMemcpyHostToDevice, s));
   FrontendParams p{};
   p.audio = d_audio;
   p.clip_stride = L_clip;
   p.n_clips = (int32_t)n_clips;
   p.n_win = wg.n_win;
-  for (int i = 0; i < wg.n_win; ++i) p.win_start[i] = wg.start[i];
+  p.win_start = wstart;
   p.clip_len = wg.clip_len;
   p.sig_len = wg.win_samples;
   p.T = (int32_t)wg.g.T;

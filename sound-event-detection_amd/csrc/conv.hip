@@ -574,12 +574,15 @@ void launch_conv3x3(const float* in, int B, int T, int F, int Cin, int Cout, con
   switch (F) {
     case 32:
       if (Cout % 128 == 0) launch_f_bn<32, 128, false>(in, B, T, Cin, Cout, wp, bias, out, epi, nullptr, nullptr, zero16, s);
+      else note_launch_error(hipErrorInvalidValue);   // never leave the output unwritten silently
       break;
     case 16:
       if (Cout % 128 == 0) launch_f_bn<16, 128, false>(in, B, T, Cin, Cout, wp, bias, out, epi, nullptr, nullptr, zero16, s);
+      else note_launch_error(hipErrorInvalidValue);   // never leave the output unwritten silently
       break;
     case 8:
       if (Cout % 128 == 0) launch_f_bn<8, 128, false>(in, B, T, Cin, Cout, wp, bias, out, epi, nullptr, nullptr, zero16, s);
+      else note_launch_error(hipErrorInvalidValue);   // never leave the output unwritten silently
       break;
     default:
       note_launch_error(hipErrorInvalidValue);

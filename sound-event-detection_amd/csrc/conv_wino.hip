@@ -198,7 +198,6 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
   auto dma = [&](const int (&off)[G::UPW], int n0_, int chunk_, int buf_) {
 #pragma unroll
     for (int k = 0; k < G::UPW; ++k) {
-      const int u = wv + WAVES * k;
       if (present(k, wv)) {
         const uint32_t m0_ =
             (uint32_t)(size_t)(__attribute__((address_space(3))) float*)(smem + buf_ * G::BUF + dlds[k]);
@@ -216,14 +215,12 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
   auto ptrs = [&](const int (&off)[G::UPW], int n0_) {
 #pragma unroll
     for (int k = 0; k < G::UPW; ++k) {
-      const int u = wv + WAVES * k;
       dptr[k] = is_w(k) ? U + 2 * n0_ + off[k] : (off[k] >= 0 ? in + off[k] : zero16);
     }
   };
   auto dma_cur = [&](int chunk_, int buf_) {
 #pragma unroll
     for (int k = 0; k < G::UPW; ++k) {
-      const int u = wv + WAVES * k;
       if (present(k, wv)) {
         const uint32_t m0_ =
             (uint32_t)(size_t)(__attribute__((address_space(3))) float*)(smem + buf_ * G::BUF + dlds[k]);
@@ -605,7 +602,10 @@ static void launch_wino_f(const float* in, int B, int T, int Cin, int Cout, cons
 
 void launch_conv3x3_wino(const float* in, int B, int T, int F, int Cin, int Cout, const float* U,
                          const float* bias, float* out, int epi, const float* zero16, float* trash, hipStream_t s) {
-  if (Cin % 8 != 0 || Cin < 32 || Cout % 32 != 0 || B <= 0 || T <= 0) return note_launch_error(hipErrorInvalidValue);
+  // halo lanes outside the clip step through the zero block by the chunk's
+  // channel offset: it must hold Cin + 4 floats
+  if (Cin % 8 != 0 || Cin < 32 || Cout % 32 != 0 || B <= 0 || T <= 0 || Cin + 4 > ZERO_BLOCK_FLOATS)
+    return note_launch_error(hipErrorInvalidValue);
   // the kernel's DMA offsets are 32-bit: batches whose input passes 2^31
   // elements run as several launches over whole clips (same per-clip work,
   // so the outputs do not depend on the split)

@@ -152,7 +152,7 @@ __global__ __launch_bounds__(64 * FE_WAVES) void logmel_kernel(FrontendParams p)
     const int t = fr - (int)item * p.T;
     const unsigned clip = item / (unsigned)p.n_win;
     const int w = (int)(item - clip * (unsigned)p.n_win);
-    const int64_t wstart = p.win_start[w];
+    const int64_t wstart = p.win_start ? p.win_start[w] : 0;
     const int64_t src_off = (int64_t)clip * p.clip_stride + wstart;
     const int64_t av64 = p.clip_len - wstart;        // samples of this item backed by audio
     const int avail = av64 > L ? L : (int)av64;       // (j < L always)
@@ -356,16 +356,14 @@ __global__ __launch_bounds__(64 * FE16_WAVES) void logmel512_kernel(FrontendPara
   }
   // band weights per (slot q, lane b), zero-padded to the widest band rounded
   // to 4 (host table; fma(P, 0, acc) == acc exactly for finite P, so the
-  // padded chain gives the band's own bits); window offsets of the items
+  // padded chain gives the band's own bits)
   __shared__ __attribute__((aligned(16))) float s_wt[4 * 16 * FE16_MW];
-  __shared__ int64_t s_wstart[64];
   const int wmax = p.mel_wmax;
   const bool mel_table = wmax <= FE16_MW;
   static_assert((4 * 16 * FE16_MW) % (64 * FE16_WAVES) == 0, "table fill");
 #pragma unroll
   for (int k = 0; k < 4 * 16 * FE16_MW / (64 * FE16_WAVES); ++k)
     s_wt[threadIdx.x + 64 * FE16_WAVES * k] = p.mel_tab[threadIdx.x + 64 * FE16_WAVES * k];
-  if (threadIdx.x < 64) s_wstart[threadIdx.x] = p.win_start[threadIdx.x];
   __syncthreads();
 
   const int total = p.n_clips * p.n_win * p.T;
@@ -382,7 +380,7 @@ __global__ __launch_bounds__(64 * FE16_WAVES) void logmel512_kernel(FrontendPara
     const int t = fr - (int)item * p.T;
     const unsigned clip = item / (unsigned)p.n_win;
     const int w = (int)(item - clip * (unsigned)p.n_win);
-    const int64_t wstart = s_wstart[w];
+    const int64_t wstart = p.win_start ? p.win_start[w] : 0;   // window table (any length), L2-resident
     const int64_t src_off = (int64_t)clip * p.clip_stride + wstart;
     const int64_t av64 = p.clip_len - wstart;
     const int avail = av64 > L ? L : (int)av64;

@@ -85,6 +85,14 @@ struct GruSync {                      // zeroed every launch
   unsigned long long stamps[8];       // SEDX_GRU_STAMPS diagnostic builds only
   unsigned mode;                      // 1 = XCD-local protocol was used by pair 0
 };
+// a bounded spin timed out: the launch's own flag word and the handle's
+// host-mapped word (sedx_forward* returns SEDX_EHIP on the next call)
+__device__ __forceinline__ void gru_fail(GruSync* sync, unsigned* host_err, unsigned code) {
+  atomicOr(&sync->err, code);
+  if (host_err) __hip_atomic_fetch_or(host_err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ bool gru_dead(const int* s_err) { return *reinterpret_cast<const volatile int*>(s_err) != 0; }
+
 #ifdef SEDX_GRU_STAMPS
 #define GRU_STAMP(i)                                                                    \
   if (tid == 0 && pair == 0 && p == 0) {                                                \
@@ -101,7 +109,8 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
                                                        const float* __restrict__ whh,
                                                        const float* __restrict__ bhh,
                                                        float* __restrict__ H, float* X,
-                                                       GruSync* sync, int nslots, int allow_fast) {
+                                                       GruSync* sync, int nslots, int allow_fast,
+                                                       unsigned* host_err) {
   __shared__ uint4 Aimg[16 * 32 * 4];          // h_{s-1} hi/lo, [kstep][clip][4 slots]
   // partial gate pre-activations: K quarters (x3) / eighths (exact: two
   // independent chains per wave, summed in order in the gate phase)
@@ -130,7 +139,7 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
     while (g_ld(&sync->ready[pair][0]) < 8u) {
       __builtin_amdgcn_s_sleep(1);
       if (++spins > GRU_SPIN) {
-        atomicOr(&sync->err, 1u);
+        gru_fail(sync, host_err, 1u);
         s_err = 1;
         break;
       }
@@ -219,13 +228,16 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
           gi[i][0] = gi[i][1] = gi[i][2] = 0.f;
         }
       }
+      // after a timed-out spin (s_err) no later wait is attempted: the
+      // workgroup runs its remaining steps on NaN instead of timing out again
+      // at every step
       if (!VALU && gs > 0) {
         if (fast) {
           if (tid < 8) {
             unsigned spins = 0;
-            while (g_ld(Fl + tid * 16) < (unsigned)gs) {
+            while (!gru_dead(&s_err) && g_ld(Fl + tid * 16) < (unsigned)gs) {
               if (++spins > GRU_SPIN) {
-                atomicOr(&sync->err, 2u);
+                gru_fail(sync, host_err, 2u);
                 s_err = 1;
                 break;
               }
@@ -234,10 +246,10 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
         } else if (tid == 0) {
           const unsigned target = 8u * (unsigned)gs;
           unsigned spins = 0;
-          while (g_ld(C) < target) {
+          while (!gru_dead(&s_err) && g_ld(C) < target) {
             __builtin_amdgcn_s_sleep(1);
             if (++spins > GRU_SPIN) {
-              atomicOr(&sync->err, 1u);
+              gru_fail(sync, host_err, 1u);
               s_err = 1;
               break;
             }
@@ -264,9 +276,9 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
           const int it = tid + 768 * k;
           if (it < nc * 256) {
             unsigned spins = 0;
-            while ((unsigned)(w[k] >> 32) != (unsigned)gs) {
+            while (!gru_dead(&s_err) && (unsigned)(w[k] >> 32) != (unsigned)gs) {
               if (++spins > GRU_SPIN) {
-                atomicOr(&sync->err, 4u);
+                gru_fail(sync, host_err, 4u);
                 s_err = 1;
                 break;
               }
@@ -474,7 +486,7 @@ size_t gru_coop_workspace_bytes(int B) {
 }
 
 void launch_gru_coop(const float* G, int B, int T, const float* whh, const float* bhh, float* H,
-                     void* ws, bool exact, bool allow_fast, hipStream_t s) {
+                     void* ws, bool exact, bool allow_fast, unsigned* host_err, hipStream_t s) {
   const int ngroups = (B + 31) / 32;
   const int nslots = ngroups < GRU_MAX_SLOTS ? ngroups : GRU_MAX_SLOTS;
   GruSync* sync = static_cast<GruSync*>(ws);
@@ -486,13 +498,13 @@ void launch_gru_coop(const float* G, int B, int T, const float* whh, const float
   (void)hipMemsetAsync(sync, 0, sync_bytes + (valu ? (size_t)2 * 2 * GRU_VALU_CLIPS * 256 * 8 : 0), s);
   if (valu)
     launch_kernel(gru_coop_kernel<true, true>, dim3(64), 768, s, G, B, T, whh, bhh, H, X, sync, nslots,
-                  allow_fast ? 1 : 0);
+                  allow_fast ? 1 : 0, host_err);
   else if (exact)
     launch_kernel(gru_coop_kernel<true, false>, dim3(64), 768, s, G, B, T, whh, bhh, H, X, sync, nslots,
-                  allow_fast ? 1 : 0);
+                  allow_fast ? 1 : 0, host_err);
   else
     launch_kernel(gru_coop_kernel<false, false>, dim3(64), 768, s, G, B, T, whh, bhh, H, X, sync, nslots,
-                  allow_fast ? 1 : 0);
+                  allow_fast ? 1 : 0, host_err);
 }
 
 }  // namespace sedx

@@ -30,7 +30,8 @@ struct FrontendParams {
   int64_t clip_stride;      // samples between clips
   int32_t n_clips;          // items = n_clips * n_win
   int32_t n_win;            // windows per clip (1 in clip mode)
-  int64_t win_start[64];    // sample offset of each window (by value; n_win <= 64)
+  const int64_t* win_start; // [n_win] device table of window sample offsets
+                            // (launch_window_starts); nullptr: every item starts at 0
   int64_t clip_len;         // valid samples per clip (beyond => zeros; pad_truncate)
   int64_t sig_len;          // samples per item fed to the STFT (L or window length)
   int32_t T;                // frames per item = sig_len / hop + 1
@@ -89,6 +90,9 @@ void launch_block1_exact(const float* xpad, int B, int T, const float* w1, const
                          const float* bias, float* out, const float* zero16, hipStream_t s);
 
 enum ConvEpi { EPI_STORE = 0, EPI_POOL2 = 1, EPI_FMEAN = 2 };
+// floats in the handle's device zero block (the halo DMA's source for pixels
+// outside the clip; the Winograd DMA walks it by up to Cin + 4 floats)
+constexpr int ZERO_BLOCK_FLOATS = 1024;
 constexpr int CONV_SCHED_INTS = 256;   // per conv launch: 8 tile-claim counters, 128 B apart
 // 3x3 conv (pad 1) + folded BN + ReLU (+ epilogue), implicit GEMM on fp32 MFMA.
 //  in [B][T][F][Cin] -> EPI_STORE: [B][T][F][Cout], EPI_POOL2: [B][T/2][F/2][Cout],
@@ -247,8 +251,10 @@ void launch_gru(const float* G, int B, int T, const float* whhT, const float* bh
 size_t gru_coop_workspace_bytes(int B);
 // exact: fp32 MFMA (else the x3 bf16 split); allow_fast: XCD-local hand-off
 // when the placement allows it (else always the global protocol).
+// host_err (nullable): host-mapped word OR-ed with the failure code when a
+// bounded hand-off spin times out (outputs of that launch are then NaN).
 void launch_gru_coop(const float* G, int B, int T, const float* whh, const float* bhh, float* H,
-                     void* ws, bool exact, bool allow_fast, hipStream_t s);
+                     void* ws, bool exact, bool allow_fast, unsigned* host_err, hipStream_t s);
 
 // MHA core: QKV [B][T][1536] (q|k|v, head h = cols 64h..64h+63) -> O [B][T][512]
 void launch_mha(const float* QKV, int B, int T, float* O, hipStream_t s);
@@ -267,6 +273,11 @@ void launch_transpose_btd(const float* E, int B, int T, int D, float* out, hipSt
 // summed, no avg_merge division (main_strong.py:1082-1097).
 void launch_merge(const float* fw, int n_clips, int n_win, int Tw, int C, int step, int N,
                   int interval, int sd, const double* vote_thr, float* merged, hipStream_t s);
+// window sample offsets of predict.py's loop (:297-338): start = 0, then
+// start += overlap_value in float64, offset = int(start * sr) — the host's
+// sequence (api.cpp window_geometry), recomputed on the device so the table
+// of any length needs no host buffer that outlives the call
+void launch_window_starts(int n_win, double overlap_value, int sample_rate, int64_t* starts, hipStream_t s);
 
 // ---- events (events.hip) --------------------------------------------------
 struct EventArgs {

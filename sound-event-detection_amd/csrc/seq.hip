@@ -458,9 +458,13 @@ __global__ __launch_bounds__(256) void merge_kernel(const float* __restrict__ fw
     const int64_t c = cf / N;
     float s = 0.f;
     bool first = true;
-    for (int w = 0; w < n_win; ++w) {
+    // windows covering frame f: w * step <= f < w * step + Tw, ascending
+    // (the incremental merge's addition order); O(Tw / step) per frame for any
+    // number of windows
+    const int w_lo = f >= Tw ? (f - Tw) / step + 1 : 0;
+    const int w_hi = min(n_win - 1, f / step);
+    for (int w = w_lo; w <= w_hi; ++w) {
       const int lf = f - w * step;
-      if (lf < 0 || lf >= Tw) continue;
       float v = fw[((c * n_win + w) * Tw + lf) * C + k];
       // binarize_pred: float64 0/1 (the comparison of a float32 element with
       // a float64 threshold is made in float64); sums of 0/1 are exact in f32
@@ -482,6 +486,19 @@ __global__ __launch_bounds__(256) void merge_kernel(const float* __restrict__ fw
     }
     merged[i] = d > 1 ? s / (float)d : s;
   }
+}
+
+__global__ void window_starts_kernel(int n_win, double ov, int sr, int64_t* __restrict__ starts) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  double start = 0.0;                 // predict.py:281, :302, :335-336 (float64 running sum)
+  for (int w = 0; w < n_win; ++w) {
+    starts[w] = (int64_t)(start * (double)sr);
+    start += ov;
+  }
+}
+
+void launch_window_starts(int n_win, double overlap_value, int sample_rate, int64_t* starts, hipStream_t s) {
+  hipLaunchKernelGGL(window_starts_kernel, dim3(1), dim3(64), 0, s, n_win, overlap_value, sample_rate, starts);
 }
 
 void launch_merge(const float* fw, int n_clips, int n_win, int Tw, int C, int step, int N,

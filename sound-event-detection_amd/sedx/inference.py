@@ -280,9 +280,17 @@ class GraphedForward:
 
     def __init__(self, model, example, warmup=3):
         import torch
+        if getattr(model, 'pipelined', False):
+            # a pipelined handle makes every forward wait on the previous
+            # forward's conv-done event, recorded outside any capture: that
+            # wait cannot be captured (and would leave the event half recorded)
+            raise RuntimeError('GraphedForward needs model.set_pipelined(False)')
         self.model = model
         self.static_in = example.detach().clone()
         self.stream = torch.cuda.Stream(example.device)
+        # the warm-up forwards on the side stream read static_in, whose clone
+        # was queued on the current stream
+        self.stream.wait_stream(torch.cuda.current_stream(example.device))
         with torch.no_grad(), torch.cuda.stream(self.stream):
             for _ in range(warmup):          # first launches set up per-device launch facts
                 model(self.static_in)

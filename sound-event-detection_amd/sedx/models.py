@@ -20,6 +20,8 @@ Usage mirrors the reference call sites (pytorch/predict.py:229-242, 311-313):
 """
 import ctypes
 import math
+import threading
+import weakref
 
 import numpy as np
 import torch
@@ -168,7 +170,7 @@ class _Native(object):
         self.h = h
         self.device_index = device_index
         self.signature = None
-        self.precision = 'exact'   # the library default
+        self.precision = 'winograd'   # the library default (sedx_set_precision)
 
     def load(self, state_dict):
         L = _lib.lib()
@@ -191,6 +193,28 @@ class _Native(object):
 
 def _ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+class _HandleCache(dict):
+    """device index -> _Native, shared by a model and its DataParallel
+    replicas.  ``torch.nn.DataParallel`` (pytorch/predict.py:239,
+    pytorch/main_strong.py:541) re-replicates the module on every forward
+    (``Module._replicate_for_data_parallel``: a shallow ``__dict__`` copy, so
+    this object is shared) and hands each replica parameters freshly broadcast
+    to its device, i.e. new ``data_ptr``s every call.  The replicas' weights
+    are copies of the source module's, so a replica's handle is keyed on the
+    SOURCE module's parameters (``source``) and the per-device handle is
+    packed once, not once per call.  ``lock`` serialises handle creation and
+    packing across DataParallel's per-device threads.  Copies and pickles of
+    a model start with an empty cache (a handle owns device memory)."""
+
+    def __init__(self, owner=None):
+        super().__init__()
+        self.lock = threading.Lock()
+        self.source = weakref.ref(owner) if owner is not None else None
+
+    def __reduce__(self):
+        return (_HandleCache, ())
 
 
 class _SedModel(nn.Module):
@@ -218,8 +242,8 @@ class _SedModel(nn.Module):
         self.conv_block2 = ConvBlock(64, 128)
         self.conv_block3 = ConvBlock(128, 256)
         self.conv_block4 = ConvBlock(256, 512)
-        self._natives = {}
-        self.precision = 'exact'
+        self._natives = _HandleCache(self)
+        self.precision = 'winograd'
         self.pipelined = False
         self.tuning = {}           # sedx_set_tuning knob -> value, applied to every handle
 
@@ -242,19 +266,35 @@ class _SedModel(nn.Module):
         return tuple((k, v.data_ptr(), v._version, tuple(v.shape))
                      for k, v in self.state_dict(keep_vars=True).items())
 
+    def _weights_source(self):
+        """The module whose parameters a handle is packed from: the source
+        module for a DataParallel replica (its own parameters are broadcast
+        copies of the source's, re-made every call), else the module itself."""
+        if getattr(self, '_is_replica', False):
+            ref = getattr(self._natives, 'source', None)
+            src = ref() if ref is not None else None
+            if src is not None:
+                return src
+        return self
+
     def native(self, device):
         """The libsedx handle for ``device`` with the current weights packed."""
         if device.type != 'cuda':
             raise RuntimeError('sedx runs on HIP devices only (got a %s tensor); there is no CPU '
                                'fallback' % device.type)
         idx = device.index if device.index is not None else torch.cuda.current_device()
+        with self._natives.lock:
+            return self._native_locked(idx)
+
+    def _native_locked(self, idx):
         nat = self._natives.get(idx)
         if nat is None:
             nat = _Native(self._config(), idx)
             self._natives[idx] = nat
-        sig = self._signature()
+        src = self._weights_source()
+        sig = src._signature()
         if nat.signature != sig:
-            nat.load(self.state_dict())
+            nat.load(src.state_dict())
             nat.signature = sig
         if nat.precision != self.precision:
             _lib.check(_lib.lib().sedx_set_precision(nat.h, _lib.PRECISION[self.precision]), nat.h,
@@ -272,9 +312,11 @@ class _SedModel(nn.Module):
 
     def set_precision(self, mode):
         """GEMM arithmetic (conv stack, GRU / MHA projections and recurrence,
-        AttBlock projection): 'exact' (default; fp32 operands and
-        accumulation, the reference's arithmetic) or 'x3' (opt-in;
-        3xbf16-split MFMA, fp32 accumulate, ~1e-6 from fp32)."""
+        AttBlock projection): 'winograd' (default; fp32 operands, transforms
+        and accumulation, block 1's conv2 and blocks 2-4 as Winograd
+        F(2x2,3x3): error vs float64 at or below the direct conv's), 'exact'
+        (fp32 direct convolution, the reference's operation order) or 'x3'
+        (opt-in; 3xbf16-split MFMA, fp32 accumulate, ~1e-6 from fp32)."""
         if mode not in _lib.PRECISION:
             raise ValueError('precision must be one of %s' % sorted(_lib.PRECISION))
         self.precision = mode
@@ -300,11 +342,12 @@ class _SedModel(nn.Module):
             pass  # ignored in eval, as in the reference (models.py:647-661)
 
     def output_geometry(self, length):
-        nat = self._natives.get(next(iter(self._natives))) if self._natives else None
         L = _lib.lib()
-        if nat is None:
-            nat = _Native(self._config(), torch.cuda.current_device() if torch.cuda.is_available() else 0)
-            self._natives[nat.device_index] = nat
+        with self._natives.lock:
+            nat = self._natives.get(next(iter(self._natives))) if self._natives else None
+            if nat is None:
+                nat = _Native(self._config(), torch.cuda.current_device() if torch.cuda.is_available() else 0)
+                self._natives[nat.device_index] = nat
         fr, sl = ctypes.c_int64(), ctypes.c_int64()
         _lib.check(L.sedx_output_geometry(nat.h, int(length), ctypes.byref(fr), ctypes.byref(sl)),
                    nat.h, 'output_geometry')

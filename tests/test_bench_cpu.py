@@ -78,3 +78,27 @@ def test_roofline_winograd_block1(bench):
         assert d['flops_per_launch'] == bench.conv_flops('b1c2', 32, 1001) + 2.0 * 32 * 1001 * 64 * 64 * 9
     finally:
         bench.WINO_BLOCK1 = True
+
+
+def test_roofline_fracs_are_fractions(bench):
+    """The launch time behind ``frac`` is the isolated HIP-event time when the
+    run measured it; every ``frac*`` field is executed FLOPs over the matrix
+    peak (<= 1 for any launch time the hardware can reach), and the Winograd
+    layers' direct-conv equivalent is a rate, not a fraction."""
+    T = 1001
+    stage = {s: 0.3 for s in bench.CONV_STAGES}
+    # fastest physically possible b1c2: executed FLOPs at exactly the peak
+    ex = bench.conv_flops('b1c2', 32, T) * 16.0 / 36.0
+    t_peak = ex / 157.3e12 * 1e3
+    stage['b1c2'] = t_peak * 1.3
+    iso = dict(stage, b1c2=t_peak * 1.05)
+    w = bench.roofline(stage, 32, 'winograd', iso_ms=iso)
+    assert w['avg_launch_ms'] == round(iso['b1c2'], 4) and 'one batch at a time' in w['timing']
+    assert w['avg_launch_ms_timed_region'] == stage['b1c2']
+    for k, v in w.items():
+        if k.startswith('frac') and v is not None:
+            assert 0 < v <= 1.0, (k, v)
+    assert w['direct_conv_equiv_tflops'] > w['peak']      # Winograd: more than a direct conv could do
+    assert not any(k.endswith('_algorithmic') for k in w)
+    t = bench.roofline(stage, 32, 'winograd')              # no isolated pass: the timed region
+    assert t['avg_launch_ms'] == round(stage['b1c2'], 4)

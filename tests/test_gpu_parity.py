@@ -272,6 +272,41 @@ def test_windowed_and_events(model, golden_dir):
             pytest.fail('event mismatch (%s), min |x - high| = %g' % (which, margin))
 
 
+@pytest.mark.parametrize('case', ['5_1', '6_05'])
+def test_long_file_windowed(model, golden_dir, case):
+    """predict.py over a whole long file (183 windows of 5 s at 1 s stride over
+    187.37 s; 131 windows of 6 s at 0.5 s over 71.3 s): every window in one
+    native batch, the merge + avg_merge of any window count, and the events,
+    against goldens the reference produced (oracle/make_golden_long.py)."""
+    from sedx import inference
+    mt, m = model
+    ev = json.load(open(os.path.join(golden_dir, 'long_events.json')))
+    c = ev['cases'][case]
+    g = np.load(os.path.join(golden_dir, 'long_%s.npz' % case))[mt]
+    audio = synth.make_waveforms(1, seconds=c['samples'] / 16000., sample_rate=16000, seed=c['seed'])
+    assert audio.shape[1] == c['samples']
+    nw, _, nf = inference.window_geometry(m, c['samples'], c['sample_duration'], c['overlap_value'])
+    assert nw == len(O.window_starts(c['samples'] / 16000., c['sample_duration'], c['overlap_value'])) > 64
+    assert nf == g.shape[1]
+    merged = inference.predict_windows(m, torch.from_numpy(audio).cuda(), c['sample_duration'],
+                                       c['overlap_value'], pad_clip=False)
+    got = merged.cpu().numpy()
+    assert np.isfinite(got).all()
+    e = err(got, g)
+    print(mt, 'long', case, nw, 'windows, merged', got.shape, 'max|d| =', e)
+    assert e <= TOL
+    for which in ('default', 'synthetic'):
+        params = ev['params_' + which]
+        exp = c[mt][which]
+        for ev_got in (inference.events_from_framewise(merged, params),          # GPU events
+                       inference.events_from_framewise(got, params)):            # host C++ events
+            if ev_got != exp:
+                hi = np.broadcast_to(np.asarray(params['sed_high_threshold'], np.float64), (25,))
+                margin = np.min(np.abs(g[0].astype(np.float64) - hi[None, :]))
+                pytest.fail('%s %s event mismatch (%s): %d vs %d events, min |x - high| = %g'
+                            % (mt, case, which, len(ev_got), len(exp), margin))
+
+
 def test_windowed_multi_clip_matches_single(model):
     from sedx import inference
     mt, m = model
@@ -542,3 +577,47 @@ def test_winograd_batch_past_32bit_offsets():
         one = run(m, wave[i:i + 1])
         assert np.array_equal(one['framewise_output'][0], full['framewise_output'][i]), i
     torch.cuda.empty_cache()
+
+
+def _replicate(mod):
+    """What torch.nn.parallel.replicate hands each device's thread: every
+    module replicated, parameters / buffers broadcast copies (new storage)."""
+    r = mod._replicate_for_data_parallel()
+    r._parameters = {k: (p.detach().clone() if p is not None else None) for k, p in mod._parameters.items()}
+    r._buffers = {k: (b.clone() if b is not None else None) for k, b in mod._buffers.items()}
+    r._modules = {k: _replicate(c) for k, c in mod._modules.items()}
+    return r
+
+
+@pytest.mark.parametrize('mt', [GRU, TRF])
+def test_dataparallel_call_site(mt, monkeypatch):
+    """The reference's own call site wraps the model in DataParallel
+    unconditionally (pytorch/predict.py:239-242, main_strong.py:541): the
+    wrapped model gives the bare model's outputs bit for bit, and replicas
+    with broadcast parameter copies (the >1-GPU case) reuse the packed
+    per-device handle instead of re-packing the weights every call."""
+    from sedx import models
+    m = build(mt)
+    wave = synth.make_waveforms(4, seconds=10.0, sample_rate=16000, seed=21)
+    bare = run(m, wave)
+    loads = []
+    orig = models._Native.load
+
+    def counting_load(self, sd):
+        loads.append(1)
+        return orig(self, sd)
+
+    monkeypatch.setattr(models._Native, 'load', counting_load)
+    dp = torch.nn.DataParallel(m, device_ids=[0])
+    dp.to('cuda')
+    dp.eval()
+    for _ in range(2):
+        out = run(dp, wave)
+        for k in ('framewise_output', 'clipwise_output', 'embedding'):
+            assert np.array_equal(out[k], bare[k]), k
+    for _ in range(3):
+        r = _replicate(m)
+        out = run(r, wave)
+        for k in ('framewise_output', 'clipwise_output', 'embedding'):
+            assert np.array_equal(out[k], bare[k]), k
+    assert loads == []

@@ -79,6 +79,19 @@ def test_native_events_match_golden_events(golden_dir):
             assert got == ev[mt][which]
 
 
+def test_native_events_match_long_file_goldens(golden_dir):
+    """Host C++ events over the reference's long-file merges (183 / 131
+    windows, 18,700 / 7,100 frames; oracle/make_golden_long.py)."""
+    from sedx import inference
+    ev = json.load(open(os.path.join(golden_dir, 'long_events.json')))
+    for case, c in ev['cases'].items():
+        g = np.load(os.path.join(golden_dir, 'long_%s.npz' % case))
+        for mt in ('Cnn_9layers_Gru_FrameAtt', 'Cnn_9layers_Transformer_FrameAtt'):
+            for which in ('default', 'synthetic'):
+                got = inference.events_from_framewise(g[mt], ev['params_' + which])
+                assert got == c[mt][which], (case, mt, which)
+
+
 def test_events_random_vs_oracle():
     from sedx import inference
     rng = np.random.default_rng(3)
@@ -119,3 +132,63 @@ def test_no_packed_fp32_in_any_kernel():
     r = subprocess.run(['make', '-s', '-C', pkg, '-j8', 'isa-check'], capture_output=True, text=True, timeout=900)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert 'no packed FP32 VALU' in r.stdout
+
+
+def test_dataparallel_replicas_reuse_the_source_handle(monkeypatch):
+    """torch.nn.DataParallel (pytorch/predict.py:239) re-replicates the model on
+    every forward, each replica holding freshly broadcast parameter copies
+    (new data_ptrs).  The handle cache is shared with the replicas and keyed
+    on the SOURCE module's parameters, so a replica does not re-pack the
+    weights (no sedx_load_param); an in-place update of the source does."""
+    import copy
+    import io
+    from sedx import models, synth
+
+    loads = []
+
+    class FakeNative(object):          # stands in for the libsedx handle (no GPU here)
+        def __init__(self, cfg, idx):
+            self.device_index, self.signature, self.precision, self.h = idx, None, 'exact', None
+
+        def load(self, sd):
+            loads.append(len(sd))
+
+    monkeypatch.setattr(models, '_Native', FakeNative)
+    mt = 'Cnn_9layers_Gru_FrameAtt'
+    m = getattr(models, mt)(16000, 512, 160, 64, 25, 7000, 25, 'logmel')
+    sd = m.state_dict()
+    for k, v in synth.make_state_dict(mt, seed=0).items():
+        sd[k] = torch.from_numpy(v)
+    m.load_state_dict(sd)
+    m.eval()
+    dev = torch.device('cuda', 0)
+    m.native(dev)
+    assert len(loads) == 1
+    m.native(dev)
+    assert len(loads) == 1
+    def replicate(mod):
+        """torch.nn.parallel.replicate for one device without a GPU: every
+        module replicated, parameters and buffers broadcast copies (same
+        values, new storage)"""
+        r = mod._replicate_for_data_parallel()
+        r._parameters = {k: (p.detach().clone() if p is not None else None) for k, p in mod._parameters.items()}
+        r._buffers = {k: (b.clone() if b is not None else None) for k, b in mod._buffers.items()}
+        r._modules = {k: replicate(c) for k, c in mod._modules.items()}
+        return r
+
+    for _ in range(3):                 # one replica per DataParallel call
+        r = replicate(m)
+        assert r._natives is m._natives and r._weights_source() is m
+        assert r._signature() != m._signature()
+        assert r.native(dev) is m._natives[0]
+    assert len(loads) == 1
+    with torch.no_grad():
+        m.conv_block2.conv1.weight.mul_(1.0)   # in-place update of the source
+    replicate(m).native(dev)
+    assert len(loads) == 2
+    # copies / pickles start with their own empty cache
+    c = copy.deepcopy(m)
+    assert isinstance(c._natives, models._HandleCache) and len(c._natives) == 0
+    assert c._weights_source() is c
+    buf = io.BytesIO()
+    torch.save(m, buf)

@@ -77,6 +77,33 @@ def test_windowed_and_events(golden_dir, mt):
         assert got == ev[mt][which]
 
 
+@pytest.mark.parametrize('mt', [GRU, TRF])
+def test_long_file_windowed(golden_dir, mt):
+    """Long files (predict.py's unbounded loop, oracle/make_golden_long.py):
+    the oracle's window count and merged length match the reference golden,
+    the oracle reproduces the 131-window 6 s / 0.5 s merge, and its events
+    match the reference's on both long goldens."""
+    ev = json.load(open(os.path.join(golden_dir, 'long_events.json')))
+    for case, c in sorted(ev['cases'].items()):
+        g = np.load(os.path.join(golden_dir, 'long_%s.npz' % case))[mt]
+        secs = c['samples'] / 16000.
+        starts = O.window_starts(secs, c['sample_duration'], c['overlap_value'])
+        step = int(100 * c['overlap_value'])
+        assert len(starts) > 64
+        # N = Tw + (n_win - 1) * step, Tw = a window's framewise length
+        # (models.py:678-681: 8 * T3, the GRU's padded to a multiple of 100)
+        tw = 8 * ((((100 * c['sample_duration'] + 1) // 2) // 2) // 2)
+        if mt == GRU:
+            tw = O.roundup(tw)
+        assert g.shape[1] == tw + (len(starts) - 1) * step
+        if case == '6_05':   # 131 batch-1 forwards: ~4-8 s on the CPU
+            audio = synth.make_waveforms(1, seconds=secs, sample_rate=16000, seed=c['seed'])[0]
+            merged = O.predict_windows(_sd(mt), mt, audio, 16000, c['sample_duration'], c['overlap_value'])
+            _close(merged, g, 1e-5, 'long_' + case)
+        for which in ('default', 'synthetic'):
+            assert O.events_from_framewise(g, ev['params_' + which]) == c[mt][which], (case, which)
+
+
 def test_merge_kat(golden_dir):
     g = np.load(os.path.join(golden_dir, 'merge_kat.npz'))
     for key in g.files:

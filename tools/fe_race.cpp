@@ -208,7 +208,7 @@ int main(int argc, char** argv) {
   float* d_audio = (float*)up(audio.data(), audio.size() * 4);
   sedx::FrontendParams p{};
   p.audio = d_audio;
-  p.clip_stride = L; p.n_clips = B; p.n_win = 1; p.win_start[0] = 0; p.clip_len = L; p.sig_len = L;
+  p.clip_stride = L; p.n_clips = B; p.n_win = 1; p.win_start = nullptr; p.clip_len = L; p.sig_len = L;
   p.T = T; p.hop = hop;
   p.twiddle = (const float2*)up(tw.data(), tw.size() * 4);
   p.window = (const float*)up(win.data(), win.size() * 4);
