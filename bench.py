@@ -39,6 +39,7 @@ import sys
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
+T_START = time.perf_counter()
 # SEDX_PKG: an alternative build of the package (A/B runs of kernel variants)
 for _p in (REPO, os.environ.get('SEDX_PKG') or os.path.join(REPO, 'sound-event-detection_amd')):
     if _p not in sys.path:
@@ -126,13 +127,45 @@ def cpu_info():
             'host_physical_cores': len(cores) or None}
 
 
-def cpu_threads():
-    """Host CPUs this process may run on (the GPU box's lease pins a share of
-    the machine): the oracle runs one torch thread per CPU it may use."""
+def cpu_quota():
+    """CPUs granted by the cgroup CPU quota (cgroup v2 cpu.max or v1
+    cfs_quota/period), None when unlimited or unreadable."""
     try:
-        return len(os.sched_getaffinity(0))
+        with open('/sys/fs/cgroup/cpu.max') as f:
+            q, per = f.read().split()[:2]
+        if q != 'max':
+            return max(1, -(-int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    try:
+        with open('/sys/fs/cgroup/cpu/cpu.cfs_quota_us') as f:
+            q = int(f.read())
+        with open('/sys/fs/cgroup/cpu/cpu.cfs_period_us') as f:
+            per = int(f.read())
+        if q > 0:
+            return max(1, -(-q // per))
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def cpu_threads():
+    """Host CPUs this process may use: its affinity set, capped by the cgroup
+    CPU quota (the GPU box's lease grants a share of a large machine whose
+    affinity set shows every CPU): the oracle runs one torch thread per CPU
+    it may use."""
+    try:
+        n = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
-        return os.cpu_count() or 1
+        n = os.cpu_count() or 1
+    q = cpu_quota()
+    return min(n, q) if q else n
+
+
+def progress(msg):
+    """One line on stderr per bench leg (the JSON record is the only stdout
+    line): a long run shows it is alive."""
+    print('[bench %.0fs] %s' % (time.perf_counter() - T_START, msg), file=sys.stderr, flush=True)
 
 
 def cpu_baseline(name, model, dev, seconds, B=32):
@@ -156,7 +189,8 @@ def cpu_baseline(name, model, dev, seconds, B=32):
             break
     rate = B * len(ts) / sum(ts)
     out = {'value': round(rate, 3), 'unit': 'clips/s', 'cores': torch.get_num_threads(), 'kind': 'port',
-           'cpus_allowed': cpu_threads(),
+           'cpus_affinity': len(os.sched_getaffinity(0)) if hasattr(os, 'sched_getaffinity') else None,
+           'cpu_quota': cpu_quota(),
            'ms_per_clip_p50': round(statistics.median(ts) / B * 1e3, 2),
            'sample': '%d iterations of B=%d x 10 s clips (clip mode, %.1f s) through oracle/sed_oracle.py '
                      'forward (torch fp32, the reference op sequence) on %d host threads'
@@ -582,6 +616,8 @@ def main():
 
     side = world == 1 and rank == 0 and not args.no_side and args.mode == 'clip'
     iso_ms = None
+    if rank == 0:
+        progress('headline leg (%s, %s mode, B=%d, %d steps)' % (args.precision, args.mode, B, args.steps))
     if args.mode == 'clip':
         value, elapsed, stage_ms, p50_dev, p99_dev, iso_ms = clip_leg(model, wave, args, world, rank, dev,
                                                                      args.precision, isolated=side)
@@ -616,12 +652,14 @@ def main():
                 'valu_tflops': round(B * 1001 * FRONTEND_FLOPS_PER_FRAME / (fe * 1e-3) / 1e12, 2),
                 'valu_peak_tflops': PEAK_VALU_F32_TF,
                 'valu_frac': round(B * 1001 * FRONTEND_FLOPS_PER_FRAME / (fe * 1e-3) / 1e12 / PEAK_VALU_F32_TF, 4)}
+        progress('events + latency_b1')
         extra.update(events_side(model, wave))
         extra['latency_b1'] = latency_b1(model, dev)
         notes = {'x3': 'opt-in arithmetic (operands narrowed to 16 significant bits), same workload',
                  'exact': 'fp32, direct 3x3 conv everywhere (bit-reproducible reference arithmetic), same workload',
                  'winograd': 'fp32, block 1 conv2 and blocks 2-4 as Winograd F(2x2,3x3), same workload'}
         for other in [p for p in ('exact', 'winograd', 'x3') if p != args.precision]:
+            progress('value_%s leg' % other)
             model.set_precision(other)
             extra['latency_b1_%s' % other] = latency_b1(model, dev)
             model.set_precision(args.precision)
@@ -634,6 +672,7 @@ def main():
         model.set_precision(args.precision)
         cfgs = {}
         if args.model == 'gru':
+            progress('config3 (Transformer) leg')
             trf = build_model(MODEL_NAMES['transformer'], dev)
             v3, e3, st3, p3, _, iso3 = clip_leg(trf, wave, args, 1, 0, dev, args.precision, isolated=True)
             cfgs['config3'] = {'workload': 'Cnn_9layers_Transformer_FrameAtt logmel 16k, %d x 10 s clips '
@@ -644,15 +683,19 @@ def main():
                                'ms_per_clip_p50_device': round(p3, 4),
                                'roofline': roofline(st3, B, args.precision, iso_ms=iso3), 'stage_ms': st3}
             del trf
+        progress('config4 (gammatone 32k) leg')
         cfgs['config4'] = gamma_leg(args, dev, args.precision)
+        progress('window-mode leg')
         cfgs['window_mode'] = window_leg(model, wave, args, dev, args.precision)
         model.set_precision(args.precision)
         extra['configs'] = cfgs
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        progress('cpu baseline (%d threads)' % cpu_threads())
         cpu = cpu_baseline(name, model, dev, args.cpu_seconds, B)
         if args.mode == 'clip' and not args.no_side:
+            progress('cpu baseline, window mode')
             cpu['window_mode'] = cpu_baseline_window(name, min(args.cpu_seconds, 10.0))
 
     if rank == 0:

@@ -41,6 +41,7 @@
 namespace sedx {
 
 typedef float f32x16_g __attribute__((ext_vector_type(16)));
+typedef float f32x4_g __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8_g __attribute__((ext_vector_type(8)));
 
 typedef __bf16 bf16x2_g __attribute__((ext_vector_type(2)));
@@ -63,6 +64,16 @@ __device__ __forceinline__ void g_split8(const float* v, uint4& hi, uint4& lo) {
 // correctly at both ends
 __device__ __forceinline__ float g_sigmoid(float x) { return __frcp_rn(1.0f + __expf(-x)); }
 __device__ __forceinline__ float g_tanh(float x) { return 2.0f * __frcp_rn(1.0f + __expf(-2.0f * x)) - 1.0f; }
+// one GRU cell (ATen gate order r, z, n; h' = n + z (h - n)); gh* = the
+// recurrent pre-activations with b_hh added, gi* = x W_ih^T + b_ih.  Every
+// recurrence kernel calls this one function, so their gate arithmetic (and
+// its fma contraction) is the same instruction sequence
+__device__ __forceinline__ float gru_cell(float gir, float giz, float gin, float ghr, float ghz, float ghn, float hp) {
+  const float r = g_sigmoid(gir + ghr);
+  const float z = g_sigmoid(giz + ghz);
+  const float n = g_tanh(gin + r * ghn);
+  return n + z * (hp - n);
+}
 __device__ __forceinline__ unsigned g_ld(const unsigned* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // sc1
 }
@@ -426,11 +437,9 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
             ghr += br;
             ghz += bz;
             ghn += bn;
-            const float r = g_sigmoid(gi[i][0] + ghr);
-            const float z = g_sigmoid(gi[i][1] + ghz);
-            const float n = g_tanh(gi[i][2] + r * ghn);
             const float hp = VALU ? hreg[i] : hprev[c][u];
-            hvs[i] = s_err ? __builtin_nanf("") : n + z * (hp - n);   // NaN propagates to every slice
+            const float hn = gru_cell(gi[i][0], gi[i][1], gi[i][2], ghr, ghz, ghn, hp);
+            hvs[i] = s_err ? __builtin_nanf("") : hn;   // NaN propagates to every slice
           }
           float* xp = dst + c * 256 + 32 * p + u;
           if (c >= nc) {
@@ -480,21 +489,242 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
 #endif
 }
 
+// ---------------------------------------------------------------------------
+// Batched exact recurrence on 16-clip groups (launches of more than
+// GRU_VALU_CLIPS clips), data-tagged hand-off.
+// Per (16-clip group, direction) NS workgroups ("slices") own U = 256 / NS
+// hidden units = 3 U gate rows each, their W_hh rows resident in VGPRs as
+// v_mfma_f32_16x16x4_f32 A fragments.  Per step:
+//   sweep    h_{t-1} [16 clips][256] arrives as 8-byte granules {tag = step
+//            + 1, value}, each written by ONE sc1 store and swept with sc1
+//            loads until its tag matches (cdna_hip_programming.md Guideline
+//            16 R2: the data is the flag: no drain, flag, poll or fence),
+//            into an LDS image whose k order is permuted so a lane's whole
+//            chain is two ds_read_b128;
+//   product  12 waves = 3 gates x 4 K-quarters, each two independent chains
+//            (K eighths 2 kq, 2 kq + 1) of 8 MFMAs per 16-row tile;
+//   gates    the eight partials summed in K order + b_hh, gru_cell, the new
+//            h published as granules (double-buffered by step parity) and
+//            stored to H.
+// 16-clip groups halve the bytes every slice sweeps per step against the
+// 32-clip kernel (16 KB of h, 32 KB of granules) and NS = 16 slices halve
+// each slice's serial product.
+// Arithmetic contract shared by every exact kernel of this file: per (gate
+// row, clip) eight partials, each the in-order fma chain over its 32 k from
+// 0 (v_mfma_f32_16x16x4_f32 is the in-order fma chain over its four k, and
+// v_mfma_f32_32x32x2_f32 over its two: tools/mfma16_f32_semantics.cpp,
+// tools/mfma_f32_semantics.cpp), summed p0 + p1 + ... + p7, then gru_cell:
+// the outputs are bit-identical to the 32-clip MFMA and the small-batch VALU
+// kernels.
+constexpr int GRU_HS_LD = 260;     // h image row stride (floats): b128 fragment reads conflict-free
+constexpr int GRU_PLD = 17;        // partial rows (16 clips + pad)
+template <int NS>
+constexpr size_t gru_tag_lds() {
+  return (size_t)16 * GRU_HS_LD * 4 + (size_t)8 * 3 * (256 / NS) * GRU_PLD * 4;
+}
+// position of k in the h image: k = 32 e + 4 s + q -> 32 e + 8 q + s
+__device__ __forceinline__ int gru_hperm(int k) { return (k & ~31) | ((k & 3) << 3) | ((k >> 2) & 7); }
+
+template <int NS>
+__global__ __launch_bounds__(768) void gru_tag_kernel(const float* __restrict__ G, int B, int T,
+                                                      const float* __restrict__ whh,
+                                                      const float* __restrict__ bhh, float* __restrict__ H,
+                                                      unsigned long long* X, GruSync* sync, int nslots,
+                                                      unsigned* host_err) {
+  constexpr int U = 256 / NS;          // hidden units per slice
+  constexpr int RT = U / 16;           // 16-row tiles per gate
+  static_assert(U % 16 == 0, "slice rows");
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* Hs = smem;                              // [16 clips][GRU_HS_LD] h_{t-1}, k permuted
+  float* part = smem + 16 * GRU_HS_LD;           // [8 eighths][3 gates][U units][GRU_PLD]
+  __shared__ int s_err;                          // a bounded spin timed out: outputs become NaN
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int pair = blockIdx.x & 7;               // dispatch residue -> one XCD (observed; speed only)
+  const int p = blockIdx.x >> 3;                 // slice 0..NS-1
+  const int slot = pair >> 1, dir = pair & 1;
+  if (slot >= nslots) return;                    // whole workgroup exits (uniform)
+  const int ngroups = (B + 15) / 16;
+  const int g = wave % 3, kq = wave / 3, q = lane >> 4, m16 = lane & 15;
+  if (tid == 0) s_err = 0;
+
+  // W_hh -> A fragments: A[m][kk] = W_hh[g 256 + U p + 16 rt + m][32 e + 4 s + kk], lane = (kk, m)
+  float Wf[RT][2][8];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int ci = 0; ci < 2; ++ci) {
+      const float* wrow = whh + ((int64_t)dir * 768 + g * 256 + U * p + 16 * rt + m16) * 256 + 32 * (2 * kq + ci) + q;
+#pragma unroll
+      for (int st = 0; st < 8; ++st) Wf[rt][ci][st] = wrow[4 * st];
+    }
+  // gate phase: thread = (unit gu, clip gc)
+  const bool gate_thr = tid < 16 * U;
+  const int gu = tid >> 4, gc = tid & 15;
+  float br = 0.f, bz = 0.f, bn = 0.f;
+  if (gate_thr) {
+    br = bhh[dir * 768 + U * p + gu];
+    bz = bhh[dir * 768 + 256 + U * p + gu];
+    bn = bhh[dir * 768 + 512 + U * p + gu];
+  }
+  unsigned long long* Xp = X + (int64_t)pair * 2 * 16 * 256;
+  __syncthreads();
+
+  int j = 0;
+  for (int grp = slot; grp < ngroups; grp += nslots, ++j) {
+    const int c0 = grp * 16;
+    const int nc = min(16, B - c0);
+    float hreg = 0.f;                            // this thread's h_{t-1} (own slice: same (clip, unit) every step)
+    auto load_gi = [&](int s_, float& a, float& b, float& c) {
+      const int t_ = dir ? T - 1 - s_ : s_;
+      if (gate_thr && gc < nc) {
+        const float* gp = G + ((int64_t)(c0 + gc) * T + t_) * 1536 + dir * 768 + U * p + gu;
+        a = gp[0];
+        b = gp[256];
+        c = gp[512];
+      } else {
+        a = b = c = 0.f;
+      }
+    };
+    float gi0, gi1, gi2;
+    load_gi(0, gi0, gi1, gi2);
+    for (int s = 0; s < T; ++s) {
+      const int gs = j * T + s;                  // step of this pair; tags / parities are gs-based
+      const int t = dir ? T - 1 - s : s;
+      float nx0 = 0.f, nx1 = 0.f, nx2 = 0.f;
+      if (s + 1 < T) load_gi(s + 1, nx0, nx1, nx2);   // next step's inputs, in flight across this one
+      // ---- sweep.  Also at a group's first step (values discarded): a
+      // slice may publish step gs only after it has seen every slice's gs - 1,
+      // which is what keeps the parity double buffer from being overwritten
+      // while a slower slice still sweeps it
+      if (gs > 0) {
+        const unsigned long long* src = Xp + ((gs - 1) & 1) * 16 * 256;
+        constexpr int NGR = (16 * 256 + 767) / 768;
+        unsigned long long w[NGR];
+#pragma unroll
+        for (int k = 0; k < NGR; ++k) {
+          const int it = tid + 768 * k;
+          w[k] = it < nc * 256 ? __hip_atomic_load(src + it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+        }
+#pragma unroll
+        for (int k = 0; k < NGR; ++k) {
+          const int it = tid + 768 * k;
+          if (it < nc * 256) {
+            unsigned spins = 0;
+            while (!gru_dead(&s_err) && (unsigned)(w[k] >> 32) != (unsigned)gs) {
+              if (++spins > GRU_SPIN) {
+                gru_fail(sync, host_err, 4u);
+                s_err = 1;
+                break;
+              }
+              w[k] = __hip_atomic_load(src + it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            if (s > 0) Hs[(it >> 8) * GRU_HS_LD + gru_hperm(it & 255)] = __uint_as_float((unsigned)w[k]);
+          }
+        }
+      }
+      if (s == 0)
+        for (int i = tid; i < 16 * GRU_HS_LD; i += 768) Hs[i] = 0.f;
+      __syncthreads();
+      // ---- recurrent product: lane (q, m16) reads clip m16's k = 32 e + 4 s + q, s = 0..7
+      {
+        const float* hrow = Hs + m16 * GRU_HS_LD + 8 * q;
+        const float4 a0 = *reinterpret_cast<const float4*>(hrow + 32 * (2 * kq));
+        const float4 a1 = *reinterpret_cast<const float4*>(hrow + 32 * (2 * kq) + 4);
+        const float4 b0 = *reinterpret_cast<const float4*>(hrow + 32 * (2 * kq + 1));
+        const float4 b1 = *reinterpret_cast<const float4*>(hrow + 32 * (2 * kq + 1) + 4);
+        const float h0[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+        const float h1[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+          f32x4_g acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int st = 0; st < 8; ++st) {
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Wf[rt][0][st], h0[st], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(Wf[rt][1][st], h1[st], acc1, 0, 0, 0);
+          }
+          // D[m][n]: lane (q, n = m16) register i holds row 4 q + i
+          float* p0 = part + ((2 * kq) * 3 + g) * U * GRU_PLD + (16 * rt + 4 * q) * GRU_PLD + m16;
+          float* p1 = p0 + 3 * U * GRU_PLD;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            p0[i * GRU_PLD] = acc0[i];
+            p1[i * GRU_PLD] = acc1[i];
+          }
+        }
+      }
+      __syncthreads();
+      // ---- gates, publish
+      if (gate_thr) {
+        float hv = 0.f;
+        if (gc < nc) {
+          const float* pp = part + gu * GRU_PLD + gc;
+          constexpr int GS = U * GRU_PLD;        // gate stride; eighth stride 3 GS
+          float ghr = pp[0], ghz = pp[GS], ghn = pp[2 * GS];
+#pragma unroll
+          for (int e = 1; e < 8; ++e) {          // partials in K order
+            ghr += pp[3 * GS * e];
+            ghz += pp[3 * GS * e + GS];
+            ghn += pp[3 * GS * e + 2 * GS];
+          }
+          ghr += br;
+          ghz += bz;
+          ghn += bn;
+          const float hn = gru_cell(gi0, gi1, gi2, ghr, ghz, ghn, hreg);
+          hv = s_err ? __builtin_nanf("") : hn;  // NaN propagates to every slice
+          __hip_atomic_store(Xp + (gs & 1) * 16 * 256 + gc * 256 + U * p + gu,
+                             ((unsigned long long)(gs + 1) << 32) | __float_as_uint(hv), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+          H[((int64_t)(c0 + gc) * T + t) * 512 + dir * 256 + U * p + gu] = hv;
+        }
+        hreg = hv;
+      }
+      gi0 = nx0;
+      gi1 = nx1;
+      gi2 = nx2;
+    }
+  }
+}
+
 size_t gru_coop_workspace_bytes(int B) {
   (void)B;
+  // sync block, then the exchange space: 32-clip kernel 8 pairs x 2 parities
+  // x 32 x 256 floats; tagged kernel 8 pairs x 2 parities x 16 x 256 granules
+  // (the same 512 KB)
+  static_assert((size_t)8 * 2 * 16 * 256 * 8 == (size_t)8 * 2 * 32 * 256 * 4, "exchange space");
   return ((sizeof(GruSync) + 255) & ~size_t(255)) + (size_t)8 * 2 * 32 * 256 * 4;
 }
 
+template <int NS>
+static void launch_gru_tag(const float* G, int B, int T, const float* whh, const float* bhh, float* H, GruSync* sync,
+                           unsigned long long* X, size_t sync_bytes, unsigned* host_err, hipStream_t s) {
+  const int ngroups = (B + 15) / 16;
+  const int nslots = ngroups < GRU_MAX_SLOTS ? ngroups : GRU_MAX_SLOTS;
+  const LaunchInfo li = launch_info(reinterpret_cast<const void*>(gru_tag_kernel<NS>), 768, gru_tag_lds<NS>());
+  if (!li.ok) return;
+  // sync block + the granules of the pairs in use (every tag 0)
+  (void)hipMemsetAsync(sync, 0, sync_bytes + (size_t)2 * nslots * 2 * 16 * 256 * 8, s);
+  hipLaunchKernelGGL(gru_tag_kernel<NS>, dim3(8 * NS), dim3(768), li.dyn, s, G, B, T, whh, bhh, H, X, sync, nslots,
+                     host_err);
+}
+
 void launch_gru_coop(const float* G, int B, int T, const float* whh, const float* bhh, float* H,
-                     void* ws, bool exact, bool allow_fast, unsigned* host_err, hipStream_t s) {
+                     void* ws, bool exact, bool allow_fast, int variant, unsigned* host_err, hipStream_t s) {
+  GruSync* sync = static_cast<GruSync*>(ws);
+  const size_t sync_bytes = (sizeof(GruSync) + 255) & ~size_t(255);
+  float* X = reinterpret_cast<float*>(static_cast<char*>(ws) + sync_bytes);
+  const bool valu = exact && B <= GRU_VALU_CLIPS;
+  if (exact && !valu && variant != 2) {
+    auto* Xg = reinterpret_cast<unsigned long long*>(X);
+    if (variant == 1)
+      launch_gru_tag<8>(G, B, T, whh, bhh, H, sync, Xg, sync_bytes, host_err, s);
+    else
+      launch_gru_tag<16>(G, B, T, whh, bhh, H, sync, Xg, sync_bytes, host_err, s);
+    return;
+  }
   const int ngroups = (B + 31) / 32;
   const int nslots = ngroups < GRU_MAX_SLOTS ? ngroups : GRU_MAX_SLOTS;
-  GruSync* sync = static_cast<GruSync*>(ws);
-  float* X = reinterpret_cast<float*>(static_cast<char*>(ws) + ((sizeof(GruSync) + 255) & ~size_t(255)));
   // one fill launch: the sync block rounded to 256 B (the exchange buffers
   // start there) and, for the tagged hand-off, its granules (every tag 0)
-  const size_t sync_bytes = (sizeof(GruSync) + 255) & ~size_t(255);
-  const bool valu = exact && B <= GRU_VALU_CLIPS;
   (void)hipMemsetAsync(sync, 0, sync_bytes + (valu ? (size_t)2 * 2 * GRU_VALU_CLIPS * 256 * 8 : 0), s);
   if (valu)
     launch_kernel(gru_coop_kernel<true, true>, dim3(64), 768, s, G, B, T, whh, bhh, H, X, sync, nslots,

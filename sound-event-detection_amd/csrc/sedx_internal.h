@@ -253,8 +253,10 @@ size_t gru_coop_workspace_bytes(int B);
 // when the placement allows it (else always the global protocol).
 // host_err (nullable): host-mapped word OR-ed with the failure code when a
 // bounded hand-off spin times out (outputs of that launch are then NaN).
+// variant (exact, B > 8): 0 the 16-clip data-tagged kernel with 16 slices,
+// 1 the same with 8 slices, 2 the 32-clip flag hand-off kernel (x3 always).
 void launch_gru_coop(const float* G, int B, int T, const float* whh, const float* bhh, float* H,
-                     void* ws, bool exact, bool allow_fast, unsigned* host_err, hipStream_t s);
+                     void* ws, bool exact, bool allow_fast, int variant, unsigned* host_err, hipStream_t s);
 
 // MHA core: QKV [B][T][1536] (q|k|v, head h = cols 64h..64h+63) -> O [B][T][512]
 void launch_mha(const float* QKV, int B, int T, float* O, hipStream_t s);

@@ -37,12 +37,27 @@ int main(int argc, char** argv) {
   hipMemcpy(Bb, hb.data(), hb.size() * 4, hipMemcpyHostToDevice);
   hipEvent_t e0, e1;
   hipEventCreate(&e0); hipEventCreate(&e1);
+  // variants: 0 = tagged 16-clip groups x 16 slices, 1 = tagged x 8 slices,
+  // 2 = the 32-clip flag kernel (fast = XCD-local hand-off allowed)
+  std::vector<float> ref;
   for (int exact = 1; exact >= 0; --exact)
+    for (int variant = 0; variant < 3; ++variant)
     for (int fast = 0; fast < 2; ++fast) {
-      sedx::launch_gru_coop(G, B, T, W, Bb, H, ws, exact, fast, 0);
+      if ((!exact || variant < 2) && !fast) continue;
+      if (!exact && variant < 2) continue;
+      sedx::launch_gru_coop(G, B, T, W, Bb, H, ws, exact, fast, variant, nullptr, 0);
       hipDeviceSynchronize();
+      if (exact) {   // every exact variant must give the same bits
+        std::vector<float> out((size_t)B * T * 512);
+        hipMemcpy(out.data(), H, out.size() * 4, hipMemcpyDeviceToHost);
+        if (ref.empty()) ref = out;
+        size_t bad = 0;
+        for (size_t i = 0; i < out.size(); ++i) bad += out[i] != ref[i] && !(out[i] != out[i] && ref[i] != ref[i]);
+        printf("B=%d exact variant %d fast %d: %zu of %zu outputs differ from variant 0\n", B, variant, fast, bad,
+               out.size());
+      }
       hipEventRecord(e0, 0);
-      for (int r = 0; r < reps; ++r) sedx::launch_gru_coop(G, B, T, W, Bb, H, ws, exact, fast, 0);
+      for (int r = 0; r < reps; ++r) sedx::launch_gru_coop(G, B, T, W, Bb, H, ws, exact, fast, variant, nullptr, 0);
       hipEventRecord(e1, 0);
       hipEventSynchronize(e1);
       float ms = 0;
@@ -50,9 +65,9 @@ int main(int argc, char** argv) {
       Sync sy;
       hipMemcpy(&sy, ws, sizeof(Sync), hipMemcpyDeviceToHost);
       const double tot = (double)(sy.stamps[0] + sy.stamps[1] + sy.stamps[2] + sy.stamps[3]);
-      printf("B=%d %s %s: mode=%u err=%u  %.3f ms/launch  %.2f us/step | wait %.0f%% gather %.0f%% product %.0f%% "
+      printf("B=%d v%d %s %s: mode=%u err=%u  %.3f ms/launch  %.2f us/step | wait %.0f%% gather %.0f%% product %.0f%% "
              "gates+publish %.0f%% (s_memtime ticks/step %.0f)\n",
-             B, exact ? "exact" : "x3", fast ? "auto" : "global", sy.mode, sy.err, ms / reps, ms / reps * 1e3 / T,
+             B, variant, exact ? "exact" : "x3", fast ? "auto" : "global", sy.mode, sy.err, ms / reps, ms / reps * 1e3 / T,
              100 * sy.stamps[0] / tot, 100 * sy.stamps[1] / tot, 100 * sy.stamps[2] / tot, 100 * sy.stamps[3] / tot,
              tot / T);
     }
