@@ -598,6 +598,8 @@ def main():
                     help='headline only (no x3 / config 3 / config 4 / window legs, no latency_b1): '
                          'profiling passes use it so per-kernel rocprof averages cover only the headline')
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
+    ap.add_argument('--gru-kernel', choices=['coop', 'coop32', 'tag8', 'simple'], default='coop',
+                    help='GRU recurrence kernel (SEDX_TUNE_GRU_KERNEL; A/B runs)')
     ap.add_argument('--wino-block1', type=int, choices=[0, 1], default=1,
                     help='winograd precision: block 1 as Winograd too (1, default) or direct fused (0)')
     args = ap.parse_args()
@@ -611,6 +613,9 @@ def main():
     global WINO_BLOCK1
     WINO_BLOCK1 = bool(args.wino_block1)
     model = build_model(name, dev)
+    gk = {'coop': 0, 'simple': 1, 'coop32': 2, 'tag8': 3}[args.gru_kernel]
+    if gk:
+        model.set_tuning(_lib.TUNE_GRU_KERNEL, gk)
     B = args.batch
     wave = torch.from_numpy(synth.make_waveforms(B, 10.0, 16000, seed=1234 + rank)).to(dev)
 

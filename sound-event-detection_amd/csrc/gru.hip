@@ -491,24 +491,34 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
 
 // ---------------------------------------------------------------------------
 // Batched exact recurrence on 16-clip groups (launches of more than
-// GRU_VALU_CLIPS clips), data-tagged hand-off.
+// GRU_VALU_CLIPS clips), data-tagged hand-off straight into MFMA operands.
 // Per (16-clip group, direction) NS workgroups ("slices") own U = 256 / NS
-// hidden units = 3 U gate rows each, their W_hh rows resident in VGPRs as
+// hidden units = 3 U gate rows each.  8 waves, wave e = K eighth e (k = 32 e
+// .. 32 e + 31), holding W_hh[its slice's 3 U rows][its 32 k] as
 // v_mfma_f32_16x16x4_f32 A fragments.  Per step:
-//   sweep    h_{t-1} [16 clips][256] arrives as 8-byte granules {tag = step
-//            + 1, value}, each written by ONE sc1 store and swept with sc1
-//            loads until its tag matches (cdna_hip_programming.md Guideline
-//            16 R2: the data is the flag: no drain, flag, poll or fence),
-//            into an LDS image whose k order is permuted so a lane's whole
-//            chain is two ds_read_b128;
-//   product  12 waves = 3 gates x 4 K-quarters, each two independent chains
-//            (K eighths 2 kq, 2 kq + 1) of 8 MFMAs per 16-row tile;
-//   gates    the eight partials summed in K order + b_hh, gru_cell, the new
-//            h published as granules (double-buffered by step parity) and
-//            stored to H.
-// 16-clip groups halve the bytes every slice sweeps per step against the
-// 32-clip kernel (16 KB of h, 32 KB of granules) and NS = 16 slices halve
-// each slice's serial product.
+//   sweep    lane (q, n) needs h_{t-1}[clip n][k = 32 e + 4 s + q], s = 0..7:
+//            exactly its B operands.  Every h value travels as one 8-byte
+//            granule {tag = step + 1, value} written by ONE sc1 store; the
+//            lane loads its 8 granules with sc1 loads and re-polls until
+//            every tag matches (cdna_hip_programming.md Guideline 16 R2: the
+//            data is the flag) — no flag, fence, LDS image or barrier in
+//            front of the product, and a wave starts as soon as the 4
+//            slices of its K eighth have published;
+//   product  3 gates x RT row tiles independent chains of 8 MFMAs (K order)
+//            -> LDS partials, double-buffered by step parity;
+//   barrier  (the step's only one)
+//   gates    thread (unit, clip): the eight partials summed in K order +
+//            b_hh, gru_cell, the new h published as a granule (double-
+//            buffered by step parity) and stored to H.
+// Per step a slice moves 32 KB of granules (16 clips x 256 x 8 B) and runs
+// 3 U x 16 x 256 MACs on the matrix pipe.
+// Hazards: part[parity] of step s + 2 is written after the step s + 1
+// barrier, which every gate thread reaches after its step-s reads; a slice
+// publishes step gs only after each of its waves saw gs - 1 from every slice
+// of its K eighth, and every slice's gs - 1 granules after it saw all of
+// gs - 2 (its gate inputs), so the parity buffers are never overwritten
+// while read.  Group boundaries keep the sweep (values discarded) for the
+// same reason.
 // Arithmetic contract shared by every exact kernel of this file: per (gate
 // row, clip) eight partials, each the in-order fma chain over its 32 k from
 // 0 (v_mfma_f32_16x16x4_f32 is the in-order fma chain over its four k, and
@@ -516,46 +526,42 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
 // tools/mfma_f32_semantics.cpp), summed p0 + p1 + ... + p7, then gru_cell:
 // the outputs are bit-identical to the 32-clip MFMA and the small-batch VALU
 // kernels.
-constexpr int GRU_HS_LD = 260;     // h image row stride (floats): b128 fragment reads conflict-free
 constexpr int GRU_PLD = 17;        // partial rows (16 clips + pad)
 template <int NS>
 constexpr size_t gru_tag_lds() {
-  return (size_t)16 * GRU_HS_LD * 4 + (size_t)8 * 3 * (256 / NS) * GRU_PLD * 4;
+  return (size_t)2 * 8 * 3 * (256 / NS) * GRU_PLD * 4;
 }
-// position of k in the h image: k = 32 e + 4 s + q -> 32 e + 8 q + s
-__device__ __forceinline__ int gru_hperm(int k) { return (k & ~31) | ((k & 3) << 3) | ((k >> 2) & 7); }
 
 template <int NS>
-__global__ __launch_bounds__(768) void gru_tag_kernel(const float* __restrict__ G, int B, int T,
+__global__ __launch_bounds__(512) void gru_tag_kernel(const float* __restrict__ G, int B, int T,
                                                       const float* __restrict__ whh,
                                                       const float* __restrict__ bhh, float* __restrict__ H,
                                                       unsigned long long* X, GruSync* sync, int nslots,
                                                       unsigned* host_err) {
   constexpr int U = 256 / NS;          // hidden units per slice
   constexpr int RT = U / 16;           // 16-row tiles per gate
-  static_assert(U % 16 == 0, "slice rows");
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* Hs = smem;                              // [16 clips][GRU_HS_LD] h_{t-1}, k permuted
-  float* part = smem + 16 * GRU_HS_LD;           // [8 eighths][3 gates][U units][GRU_PLD]
+  constexpr int PB = 8 * 3 * U * GRU_PLD;   // floats per partial buffer
+  static_assert(U % 16 == 0 && 16 * U <= 512, "slice rows");
+  extern __shared__ __attribute__((aligned(16))) float smem[];   // part[2][8 eighths][3 gates][U][GRU_PLD]
   __shared__ int s_err;                          // a bounded spin timed out: outputs become NaN
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, e = tid >> 6;
   const int pair = blockIdx.x & 7;               // dispatch residue -> one XCD (observed; speed only)
   const int p = blockIdx.x >> 3;                 // slice 0..NS-1
   const int slot = pair >> 1, dir = pair & 1;
   if (slot >= nslots) return;                    // whole workgroup exits (uniform)
   const int ngroups = (B + 15) / 16;
-  const int g = wave % 3, kq = wave / 3, q = lane >> 4, m16 = lane & 15;
+  const int q = lane >> 4, n16 = lane & 15;
   if (tid == 0) s_err = 0;
 
   // W_hh -> A fragments: A[m][kk] = W_hh[g 256 + U p + 16 rt + m][32 e + 4 s + kk], lane = (kk, m)
-  float Wf[RT][2][8];
+  float Wf[3][RT][8];
 #pragma unroll
-  for (int rt = 0; rt < RT; ++rt)
+  for (int g = 0; g < 3; ++g)
 #pragma unroll
-    for (int ci = 0; ci < 2; ++ci) {
-      const float* wrow = whh + ((int64_t)dir * 768 + g * 256 + U * p + 16 * rt + m16) * 256 + 32 * (2 * kq + ci) + q;
+    for (int rt = 0; rt < RT; ++rt) {
+      const float* wrow = whh + ((int64_t)dir * 768 + g * 256 + U * p + 16 * rt + n16) * 256 + 32 * e + q;
 #pragma unroll
-      for (int st = 0; st < 8; ++st) Wf[rt][ci][st] = wrow[4 * st];
+      for (int st = 0; st < 8; ++st) Wf[g][rt][st] = wrow[4 * st];
     }
   // gate phase: thread = (unit gu, clip gc)
   const bool gate_thr = tid < 16 * U;
@@ -590,81 +596,88 @@ __global__ __launch_bounds__(768) void gru_tag_kernel(const float* __restrict__ 
     for (int s = 0; s < T; ++s) {
       const int gs = j * T + s;                  // step of this pair; tags / parities are gs-based
       const int t = dir ? T - 1 - s : s;
+      // ---- sweep: this lane's B operands of step gs (h of gs - 1)
+      float hb[8];
+      if (gs > 0 && n16 < nc) {
+        const unsigned long long* src = Xp + ((gs - 1) & 1) * 16 * 256 + n16 * 256 + 32 * e + q;
+        unsigned long long w[8];
+        // poll ONE granule with back-off until it carries this step's tag,
+        // then read the other seven (a slice writes all its granules within a
+        // few cycles) and re-poll only stragglers: 8x fewer polling loads than
+        // sweeping all of them, which other kernels on the chip share the L2
+        // and fabric with
+        unsigned spins = 0;
+        w[0] = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        while ((unsigned)(w[0] >> 32) != (unsigned)gs && !gru_dead(&s_err)) {
+          __builtin_amdgcn_s_sleep(1);
+          if (++spins > GRU_SPIN) {
+            gru_fail(sync, host_err, 4u);
+            s_err = 1;
+            break;
+          }
+          w[0] = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+#pragma unroll
+        for (int st = 1; st < 8; ++st)
+          w[st] = __hip_atomic_load(src + 4 * st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (;;) {
+          bool ok = true;
+#pragma unroll
+          for (int st = 0; st < 8; ++st) ok &= (unsigned)(w[st] >> 32) == (unsigned)gs;
+          if (ok || gru_dead(&s_err)) break;
+          __builtin_amdgcn_s_sleep(1);
+          if (++spins > GRU_SPIN) {
+            gru_fail(sync, host_err, 4u);
+            s_err = 1;
+            break;
+          }
+#pragma unroll
+          for (int st = 0; st < 8; ++st)
+            if ((unsigned)(w[st] >> 32) != (unsigned)gs)
+              w[st] = __hip_atomic_load(src + 4 * st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+#pragma unroll
+        for (int st = 0; st < 8; ++st) hb[st] = s > 0 ? __uint_as_float((unsigned)w[st]) : 0.f;
+      } else {
+#pragma unroll
+        for (int st = 0; st < 8; ++st) hb[st] = 0.f;
+      }
       float nx0 = 0.f, nx1 = 0.f, nx2 = 0.f;
       if (s + 1 < T) load_gi(s + 1, nx0, nx1, nx2);   // next step's inputs, in flight across this one
-      // ---- sweep.  Also at a group's first step (values discarded): a
-      // slice may publish step gs only after it has seen every slice's gs - 1,
-      // which is what keeps the parity double buffer from being overwritten
-      // while a slower slice still sweeps it
-      if (gs > 0) {
-        const unsigned long long* src = Xp + ((gs - 1) & 1) * 16 * 256;
-        constexpr int NGR = (16 * 256 + 767) / 768;
-        unsigned long long w[NGR];
+      // ---- recurrent product: 3 RT independent chains over this eighth's 32 k
+      f32x4_g acc[3][RT];
 #pragma unroll
-        for (int k = 0; k < NGR; ++k) {
-          const int it = tid + 768 * k;
-          w[k] = it < nc * 256 ? __hip_atomic_load(src + it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
-        }
+      for (int g = 0; g < 3; ++g)
 #pragma unroll
-        for (int k = 0; k < NGR; ++k) {
-          const int it = tid + 768 * k;
-          if (it < nc * 256) {
-            unsigned spins = 0;
-            while (!gru_dead(&s_err) && (unsigned)(w[k] >> 32) != (unsigned)gs) {
-              if (++spins > GRU_SPIN) {
-                gru_fail(sync, host_err, 4u);
-                s_err = 1;
-                break;
-              }
-              w[k] = __hip_atomic_load(src + it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            if (s > 0) Hs[(it >> 8) * GRU_HS_LD + gru_hperm(it & 255)] = __uint_as_float((unsigned)w[k]);
-          }
-        }
-      }
-      if (s == 0)
-        for (int i = tid; i < 16 * GRU_HS_LD; i += 768) Hs[i] = 0.f;
-      __syncthreads();
-      // ---- recurrent product: lane (q, m16) reads clip m16's k = 32 e + 4 s + q, s = 0..7
-      {
-        const float* hrow = Hs + m16 * GRU_HS_LD + 8 * q;
-        const float4 a0 = *reinterpret_cast<const float4*>(hrow + 32 * (2 * kq));
-        const float4 a1 = *reinterpret_cast<const float4*>(hrow + 32 * (2 * kq) + 4);
-        const float4 b0 = *reinterpret_cast<const float4*>(hrow + 32 * (2 * kq + 1));
-        const float4 b1 = *reinterpret_cast<const float4*>(hrow + 32 * (2 * kq + 1) + 4);
-        const float h0[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-        const float h1[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+        for (int rt = 0; rt < RT; ++rt) acc[g][rt] = f32x4_g{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int rt = 0; rt < RT; ++rt) {
-          f32x4_g acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+      for (int st = 0; st < 8; ++st)
 #pragma unroll
-          for (int st = 0; st < 8; ++st) {
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Wf[rt][0][st], h0[st], acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(Wf[rt][1][st], h1[st], acc1, 0, 0, 0);
-          }
-          // D[m][n]: lane (q, n = m16) register i holds row 4 q + i
-          float* p0 = part + ((2 * kq) * 3 + g) * U * GRU_PLD + (16 * rt + 4 * q) * GRU_PLD + m16;
-          float* p1 = p0 + 3 * U * GRU_PLD;
+        for (int g = 0; g < 3; ++g)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            p0[i * GRU_PLD] = acc0[i];
-            p1[i * GRU_PLD] = acc1[i];
-          }
-        }
-      }
+          for (int rt = 0; rt < RT; ++rt)
+            acc[g][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(Wf[g][rt][st], hb[st], acc[g][rt], 0, 0, 0);
+      // D[m][n]: lane (q, n) register i holds row 4 q + i
+      float* pw = smem + (s & 1) * PB + e * 3 * U * GRU_PLD + (4 * q) * GRU_PLD + n16;
+#pragma unroll
+      for (int g = 0; g < 3; ++g)
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) pw[(g * U + 16 * rt + i) * GRU_PLD] = acc[g][rt][i];
       __syncthreads();
       // ---- gates, publish
       if (gate_thr) {
         float hv = 0.f;
         if (gc < nc) {
-          const float* pp = part + gu * GRU_PLD + gc;
+          const float* pp = smem + (s & 1) * PB + gu * GRU_PLD + gc;
           constexpr int GS = U * GRU_PLD;        // gate stride; eighth stride 3 GS
           float ghr = pp[0], ghz = pp[GS], ghn = pp[2 * GS];
 #pragma unroll
-          for (int e = 1; e < 8; ++e) {          // partials in K order
-            ghr += pp[3 * GS * e];
-            ghz += pp[3 * GS * e + GS];
-            ghn += pp[3 * GS * e + 2 * GS];
+          for (int k8 = 1; k8 < 8; ++k8) {       // partials in K order
+            ghr += pp[3 * GS * k8];
+            ghz += pp[3 * GS * k8 + GS];
+            ghn += pp[3 * GS * k8 + 2 * GS];
           }
           ghr += br;
           ghz += bz;
@@ -699,11 +712,11 @@ static void launch_gru_tag(const float* G, int B, int T, const float* whh, const
                            unsigned long long* X, size_t sync_bytes, unsigned* host_err, hipStream_t s) {
   const int ngroups = (B + 15) / 16;
   const int nslots = ngroups < GRU_MAX_SLOTS ? ngroups : GRU_MAX_SLOTS;
-  const LaunchInfo li = launch_info(reinterpret_cast<const void*>(gru_tag_kernel<NS>), 768, gru_tag_lds<NS>());
+  const LaunchInfo li = launch_info(reinterpret_cast<const void*>(gru_tag_kernel<NS>), 512, gru_tag_lds<NS>());
   if (!li.ok) return;
   // sync block + the granules of the pairs in use (every tag 0)
   (void)hipMemsetAsync(sync, 0, sync_bytes + (size_t)2 * nslots * 2 * 16 * 256 * 8, s);
-  hipLaunchKernelGGL(gru_tag_kernel<NS>, dim3(8 * NS), dim3(768), li.dyn, s, G, B, T, whh, bhh, H, X, sync, nslots,
+  hipLaunchKernelGGL(gru_tag_kernel<NS>, dim3(8 * NS), dim3(512), li.dyn, s, G, B, T, whh, bhh, H, X, sync, nslots,
                      host_err);
 }
 
