@@ -589,7 +589,8 @@ def main():
     ap.add_argument('--no-pipeline', action='store_true',
                     help='streams > 1 without ordering the conv stacks (A/B of sedx_set_pipelined)')
     ap.add_argument('--model', choices=list(MODEL_NAMES), default='gru')
-    ap.add_argument('--mode', choices=['clip', 'window'], default='clip')
+    ap.add_argument('--mode', choices=['clip', 'window', 'gamma'], default='clip',
+                    help="gamma: BASELINE config 4 alone (profiling passes of the gammatone leg)")
     # headline: fp32 with the Winograd conv for blocks 2-4 (the exact direct
     # conv and the opt-in x3 arithmetic are reported beside it)
     ap.add_argument('--precision', choices=list(PEAK_TF), default='winograd')
@@ -598,7 +599,7 @@ def main():
                     help='headline only (no x3 / config 3 / config 4 / window legs, no latency_b1): '
                          'profiling passes use it so per-kernel rocprof averages cover only the headline')
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
-    ap.add_argument('--gru-kernel', choices=['coop', 'coop32', 'tag8', 'simple'], default='coop',
+    ap.add_argument('--gru-kernel', choices=['coop', 'tag16', 'tag8', 'simple'], default='coop',
                     help='GRU recurrence kernel (SEDX_TUNE_GRU_KERNEL; A/B runs)')
     ap.add_argument('--wino-block1', type=int, choices=[0, 1], default=1,
                     help='winograd precision: block 1 as Winograd too (1, default) or direct fused (0)')
@@ -613,7 +614,7 @@ def main():
     global WINO_BLOCK1
     WINO_BLOCK1 = bool(args.wino_block1)
     model = build_model(name, dev)
-    gk = {'coop': 0, 'simple': 1, 'coop32': 2, 'tag8': 3}[args.gru_kernel]
+    gk = {'coop': 0, 'simple': 1, 'tag16': 2, 'tag8': 3}[args.gru_kernel]
     if gk:
         model.set_tuning(_lib.TUNE_GRU_KERNEL, gk)
     B = args.batch
@@ -623,6 +624,11 @@ def main():
     iso_ms = None
     if rank == 0:
         progress('headline leg (%s, %s mode, B=%d, %d steps)' % (args.precision, args.mode, B, args.steps))
+    if args.mode == 'gamma':
+        res = gamma_leg(args, dev, args.precision)
+        if rank == 0:
+            print(json.dumps(res))
+        return
     if args.mode == 'clip':
         value, elapsed, stage_ms, p50_dev, p99_dev, iso_ms = clip_leg(model, wave, args, world, rank, dev,
                                                                      args.precision, isolated=side)

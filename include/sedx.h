@@ -195,16 +195,17 @@ sedx_status sedx_set_precision(sedx_handle* h, int32_t mode);
 /* Implementation choices that leave the arithmetic's meaning unchanged (A/B
  * measurement and tests; the defaults are the fastest measured):
  *  SEDX_TUNE_GRU_KERNEL   SEDX_GRU_KERNEL_COOP (default): the cooperative
- *                         recurrence: exact batches of more than 8 clips on
- *                         16 workgroups per (16-clip group, direction)
- *                         exchanging data-tagged h granules every step
- *                         (SEDX_GRU_KERNEL_TAG8: 8 workgroups per group), up
- *                         to 8 clips on the small-batch VALU kernel;
- *                         SEDX_GRU_KERNEL_COOP32: the 32-clip-group kernel
- *                         (8 workgroups, flag hand-off; x3 always uses it);
+ *                         recurrence, 8 workgroups per (32-clip group,
+ *                         direction) exchanging h slices every step (up to 8
+ *                         clips: the small-batch VALU kernel with a data-tagged
+ *                         hand-off); SEDX_GRU_KERNEL_TAG16 / _TAG8 (exact,
+ *                         more than 8 clips): 16-clip groups on 16 / 8
+ *                         workgroups exchanging data-tagged granules straight
+ *                         into the MFMA operands (lower product latency, more
+ *                         CUs held: slower beside a second batch's conv stack);
  *                         SEDX_GRU_KERNEL_SIMPLE: one workgroup per (clip,
  *                         direction), W_hh streamed from L2 (fp32 FMA).
- *  SEDX_TUNE_GRU_HANDOFF  (COOP32) SEDX_GRU_HANDOFF_AUTO (default): XCD-local hand-off
+ *  SEDX_TUNE_GRU_HANDOFF  (COOP) SEDX_GRU_HANDOFF_AUTO (default): XCD-local hand-off
  *                         when all 8 slices share an XCD, else global;
  *                         SEDX_GRU_HANDOFF_GLOBAL: always the global protocol
  *                         (same bytes, bit-identical results).
@@ -213,7 +214,7 @@ sedx_status sedx_set_precision(sedx_handle* h, int32_t mode);
  *                         conv1 launch (the 64-channel activation goes through
  *                         HBM); 0: block 1 as the direct fused fp32 kernel. */
 typedef enum { SEDX_TUNE_GRU_KERNEL = 0, SEDX_TUNE_GRU_HANDOFF = 1, SEDX_TUNE_WINO_BLOCK1 = 2 } sedx_tuning_knob;
-enum { SEDX_GRU_KERNEL_COOP = 0, SEDX_GRU_KERNEL_SIMPLE = 1, SEDX_GRU_KERNEL_COOP32 = 2, SEDX_GRU_KERNEL_TAG8 = 3 };
+enum { SEDX_GRU_KERNEL_COOP = 0, SEDX_GRU_KERNEL_SIMPLE = 1, SEDX_GRU_KERNEL_TAG16 = 2, SEDX_GRU_KERNEL_TAG8 = 3 };
 enum { SEDX_GRU_HANDOFF_AUTO = 0, SEDX_GRU_HANDOFF_GLOBAL = 1 };
 sedx_status sedx_set_tuning(sedx_handle* h, int32_t knob, int32_t value);
 

@@ -429,7 +429,7 @@ sedx_status run_body(sedx_handle* h, int64_t B, const Geometry& g, float* ws, co
     else
       launch_gru_coop(G, iB, (int)g.T3, w.whh, w.bhh, Hs, LG + align_up((size_t)M * h->nac), !x3,
                       h->gru_handoff == SEDX_GRU_HANDOFF_AUTO,
-                      h->gru_kernel == SEDX_GRU_KERNEL_COOP32 ? 2 : h->gru_kernel == SEDX_GRU_KERNEL_TAG8 ? 1 : 0,
+                      h->gru_kernel == SEDX_GRU_KERNEL_TAG16 ? 0 : h->gru_kernel == SEDX_GRU_KERNEL_TAG8 ? 1 : 2,
                       h->gru_err_dev, s);
   } else {
     linear(S, w.wqkv, w.wqkv_x3, 1536, 128, w.bqkv, G, 0);
@@ -551,7 +551,7 @@ sedx_status sedx_set_tuning(sedx_handle* h, int32_t knob, int32_t value) {
   if (!h) return SEDX_EINVAL;
   switch (knob) {
     case SEDX_TUNE_GRU_KERNEL:
-      if (value != SEDX_GRU_KERNEL_COOP && value != SEDX_GRU_KERNEL_SIMPLE && value != SEDX_GRU_KERNEL_COOP32 &&
+      if (value != SEDX_GRU_KERNEL_COOP && value != SEDX_GRU_KERNEL_SIMPLE && value != SEDX_GRU_KERNEL_TAG16 &&
           value != SEDX_GRU_KERNEL_TAG8)
         break;
       h->gru_kernel = value;

@@ -102,7 +102,12 @@ __device__ __forceinline__ void gru_fail(GruSync* sync, unsigned* host_err, unsi
   atomicOr(&sync->err, code);
   if (host_err) __hip_atomic_fetch_or(host_err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-__device__ __forceinline__ bool gru_dead(const int* s_err) { return *reinterpret_cast<const volatile int*>(s_err) != 0; }
+// the workgroup's timeout word (a __shared__ int): read as an LDS access
+// (a generic volatile pointer would become a flat load, which the compiler
+// orders with vmcnt(0) — a drain of every store in flight)
+__device__ __forceinline__ bool gru_dead(const int* s_err) {
+  return *(const volatile __attribute__((address_space(3))) int*)(s_err) != 0;
+}
 
 #ifdef SEDX_GRU_STAMPS
 #define GRU_STAMP(i)                                                                    \
@@ -493,32 +498,34 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
 // Batched exact recurrence on 16-clip groups (launches of more than
 // GRU_VALU_CLIPS clips), data-tagged hand-off straight into MFMA operands.
 // Per (16-clip group, direction) NS workgroups ("slices") own U = 256 / NS
-// hidden units = 3 U gate rows each.  8 waves, wave e = K eighth e (k = 32 e
-// .. 32 e + 31), holding W_hh[its slice's 3 U rows][its 32 k] as
-// v_mfma_f32_16x16x4_f32 A fragments.  Per step:
-//   sweep    lane (q, n) needs h_{t-1}[clip n][k = 32 e + 4 s + q], s = 0..7:
-//            exactly its B operands.  Every h value travels as one 8-byte
-//            granule {tag = step + 1, value} written by ONE sc1 store; the
-//            lane loads its 8 granules with sc1 loads and re-polls until
-//            every tag matches (cdna_hip_programming.md Guideline 16 R2: the
-//            data is the flag) — no flag, fence, LDS image or barrier in
-//            front of the product, and a wave starts as soon as the 4
-//            slices of its K eighth have published;
-//   product  3 gates x RT row tiles independent chains of 8 MFMAs (K order)
-//            -> LDS partials, double-buffered by step parity;
-//   barrier  (the step's only one)
-//   gates    thread (unit, clip): the eight partials summed in K order +
-//            b_hh, gru_cell, the new h published as a granule (double-
-//            buffered by step parity) and stored to H.
-// Per step a slice moves 32 KB of granules (16 clips x 256 x 8 B) and runs
-// 3 U x 16 x 256 MACs on the matrix pipe.
+// hidden units = 3 U gate rows each.  Two roles per workgroup:
+//   8 product waves, wave e = K eighth e (k = 32 e .. 32 e + 31), holding
+//     W_hh[the slice's 3 U rows][its 32 k] as v_mfma_f32_16x16x4_f32 A
+//     fragments.  Lane (q, n) needs h_{t-1}[clip n][k = 32 e + 4 s + q],
+//     s = 0..7: exactly its B operands.  Every h value travels as one 8-byte
+//     granule {tag = step + 1, value} written by ONE sc1 store; the lane polls
+//     one of its granules with back-off until the tag matches, reads the
+//     other seven and re-polls stragglers (cdna_hip_programming.md Guideline
+//     16 R2: the data is the flag: no flag, fence or LDS image), then 3 RT
+//     independent chains of 8 MFMAs -> LDS partials (double-buffered by step
+//     parity);
+//     The first U / 4 product waves also load the gate inputs x W_ih^T + b_ih
+//     one step ahead and stage them in LDS next to the partials;
+//   U / 4 gate waves, thread = (unit, clip): after the step's barrier the
+//     eight partials summed in K order + b_hh, gru_cell, the new h published
+//     as a granule (double-buffered by step parity) and stored to H.
+// The roles matter because vmcnt counts stores and loads in one in-order
+// queue: a wave that stored a granule (write-through) would wait for that
+// store's completion before it could consume its next loads.  The product
+// waves never store to global memory, the gate waves never load from it, and
+// the step barrier is LDS-only (a __syncthreads() would drain the stores).
 // Hazards: part[parity] of step s + 2 is written after the step s + 1
-// barrier, which every gate thread reaches after its step-s reads; a slice
-// publishes step gs only after each of its waves saw gs - 1 from every slice
-// of its K eighth, and every slice's gs - 1 granules after it saw all of
-// gs - 2 (its gate inputs), so the parity buffers are never overwritten
-// while read.  Group boundaries keep the sweep (values discarded) for the
-// same reason.
+// barrier, which every gate wave reaches after its step-s reads; a slice
+// publishes step gs only after each of its product waves saw gs - 1 from
+// every slice of its K eighth, and every slice's gs - 1 granules only after
+// all of gs - 2 was seen, so a parity buffer is never overwritten while
+// read.  Group boundaries keep the sweep (values discarded) for the same
+// reason.
 // Arithmetic contract shared by every exact kernel of this file: per (gate
 // row, clip) eight partials, each the in-order fma chain over its 32 k from
 // 0 (v_mfma_f32_16x16x4_f32 is the in-order fma chain over its four k, and
@@ -528,148 +535,167 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
 // kernels.
 constexpr int GRU_PLD = 17;        // partial rows (16 clips + pad)
 template <int NS>
-constexpr size_t gru_tag_lds() {
-  return (size_t)2 * 8 * 3 * (256 / NS) * GRU_PLD * 4;
+constexpr size_t gru_tag_lds() {   // partials [2][8][3][U][GRU_PLD], gate inputs [2][3][U][16]
+  return (size_t)2 * 8 * 3 * (256 / NS) * GRU_PLD * 4 + (size_t)2 * 3 * (256 / NS) * 16 * 4;
 }
+template <int NS>
+constexpr int gru_tag_threads() {
+  return 64 * (8 + (256 / NS) / 4);
+}
+// LDS-only workgroup barrier (no vmcnt wait: global stores stay in flight)
+__device__ __forceinline__ void gru_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 template <int NS>
-__global__ __launch_bounds__(512) void gru_tag_kernel(const float* __restrict__ G, int B, int T,
-                                                      const float* __restrict__ whh,
-                                                      const float* __restrict__ bhh, float* __restrict__ H,
-                                                      unsigned long long* X, GruSync* sync, int nslots,
-                                                      unsigned* host_err) {
+__global__ __launch_bounds__(gru_tag_threads<NS>()) void gru_tag_kernel(
+    const float* __restrict__ G, int B, int T, const float* __restrict__ whh, const float* __restrict__ bhh,
+    float* __restrict__ H, unsigned long long* X, GruSync* sync, int nslots, unsigned* host_err) {
   constexpr int U = 256 / NS;          // hidden units per slice
   constexpr int RT = U / 16;           // 16-row tiles per gate
   constexpr int PB = 8 * 3 * U * GRU_PLD;   // floats per partial buffer
-  static_assert(U % 16 == 0 && 16 * U <= 512, "slice rows");
-  extern __shared__ __attribute__((aligned(16))) float smem[];   // part[2][8 eighths][3 gates][U][GRU_PLD]
+  static_assert(U % 16 == 0, "slice rows");
+  extern __shared__ __attribute__((aligned(16))) float smem[];   // part[2][8 eighths][3 gates][U][GRU_PLD], gin[2][3][U][16]
+  float* const gin = smem + 2 * PB;
   __shared__ int s_err;                          // a bounded spin timed out: outputs become NaN
-  const int tid = threadIdx.x, lane = tid & 63, e = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int pair = blockIdx.x & 7;               // dispatch residue -> one XCD (observed; speed only)
   const int p = blockIdx.x >> 3;                 // slice 0..NS-1
   const int slot = pair >> 1, dir = pair & 1;
   if (slot >= nslots) return;                    // whole workgroup exits (uniform)
   const int ngroups = (B + 15) / 16;
-  const int q = lane >> 4, n16 = lane & 15;
   if (tid == 0) s_err = 0;
-
-  // W_hh -> A fragments: A[m][kk] = W_hh[g 256 + U p + 16 rt + m][32 e + 4 s + kk], lane = (kk, m)
-  float Wf[3][RT][8];
-#pragma unroll
-  for (int g = 0; g < 3; ++g)
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt) {
-      const float* wrow = whh + ((int64_t)dir * 768 + g * 256 + U * p + 16 * rt + n16) * 256 + 32 * e + q;
-#pragma unroll
-      for (int st = 0; st < 8; ++st) Wf[g][rt][st] = wrow[4 * st];
-    }
-  // gate phase: thread = (unit gu, clip gc)
-  const bool gate_thr = tid < 16 * U;
-  const int gu = tid >> 4, gc = tid & 15;
-  float br = 0.f, bz = 0.f, bn = 0.f;
-  if (gate_thr) {
-    br = bhh[dir * 768 + U * p + gu];
-    bz = bhh[dir * 768 + 256 + U * p + gu];
-    bn = bhh[dir * 768 + 512 + U * p + gu];
-  }
   unsigned long long* Xp = X + (int64_t)pair * 2 * 16 * 256;
   __syncthreads();
 
-  int j = 0;
-  for (int grp = slot; grp < ngroups; grp += nslots, ++j) {
-    const int c0 = grp * 16;
-    const int nc = min(16, B - c0);
-    float hreg = 0.f;                            // this thread's h_{t-1} (own slice: same (clip, unit) every step)
-    auto load_gi = [&](int s_, float& a, float& b, float& c) {
-      const int t_ = dir ? T - 1 - s_ : s_;
-      if (gate_thr && gc < nc) {
-        const float* gp = G + ((int64_t)(c0 + gc) * T + t_) * 1536 + dir * 768 + U * p + gu;
-        a = gp[0];
-        b = gp[256];
-        c = gp[512];
-      } else {
-        a = b = c = 0.f;
+  if (wave < 8) {
+    // ================= product wave: K eighth e =================
+    const int e = wave, q = lane >> 4, n16 = lane & 15;
+    // W_hh -> A fragments: A[m][kk] = W_hh[g 256 + U p + 16 rt + m][32 e + 4 s + kk], lane = (kk, m)
+    float Wf[3][RT][8];
+#pragma unroll
+    for (int g = 0; g < 3; ++g)
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        const float* wrow = whh + ((int64_t)dir * 768 + g * 256 + U * p + 16 * rt + n16) * 256 + 32 * e + q;
+#pragma unroll
+        for (int st = 0; st < 8; ++st) Wf[g][rt][st] = wrow[4 * st];
       }
-    };
-    float gi0, gi1, gi2;
-    load_gi(0, gi0, gi1, gi2);
-    for (int s = 0; s < T; ++s) {
-      const int gs = j * T + s;                  // step of this pair; tags / parities are gs-based
-      const int t = dir ? T - 1 - s : s;
-      // ---- sweep: this lane's B operands of step gs (h of gs - 1)
-      float hb[8];
-      if (gs > 0 && n16 < nc) {
-        const unsigned long long* src = Xp + ((gs - 1) & 1) * 16 * 256 + n16 * 256 + 32 * e + q;
-        unsigned long long w[8];
-        // poll ONE granule with back-off until it carries this step's tag,
-        // then read the other seven (a slice writes all its granules within a
-        // few cycles) and re-poll only stragglers: 8x fewer polling loads than
-        // sweeping all of them, which other kernels on the chip share the L2
-        // and fabric with
-        unsigned spins = 0;
-        w[0] = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        while ((unsigned)(w[0] >> 32) != (unsigned)gs && !gru_dead(&s_err)) {
-          __builtin_amdgcn_s_sleep(1);
-          if (++spins > GRU_SPIN) {
-            gru_fail(sync, host_err, 4u);
-            s_err = 1;
-            break;
-          }
+    // gate-input loader lanes: waves 0 .. U/4 - 1, lane = (unit, clip) as in the gate waves
+    const bool gl = wave < U / 4;
+    const int lu = (tid >> 4), lc = tid & 15;
+    int j = 0;
+    for (int grp = slot; grp < ngroups; grp += nslots, ++j) {
+      const int c0 = grp * 16;
+      const int nc = min(16, B - c0);
+      auto load_gi = [&](int s_, float (&v)[3]) {
+        const int t_ = dir ? T - 1 - s_ : s_;
+        if (gl && lc < nc) {
+          const float* gp = G + ((int64_t)(c0 + lc) * T + t_) * 1536 + dir * 768 + U * p + lu;
+          v[0] = gp[0];
+          v[1] = gp[256];
+          v[2] = gp[512];
+        } else {
+          v[0] = v[1] = v[2] = 0.f;
+        }
+      };
+      float gcur[3];
+      load_gi(0, gcur);
+      for (int s = 0; s < T; ++s) {
+        const int gs = j * T + s;                // step of this pair; tags / parities are gs-based
+        float gnext[3] = {0.f, 0.f, 0.f};
+        if (s + 1 < T) load_gi(s + 1, gnext);    // in flight across this step's sweep and product
+        float hb[8];
+        if (gs > 0 && n16 < nc) {
+          const unsigned long long* src = Xp + ((gs - 1) & 1) * 16 * 256 + n16 * 256 + 32 * e + q;
+          unsigned long long w[8];
+          // poll ONE granule with back-off, then read the other seven (a
+          // slice writes all its granules within a few cycles) and re-poll
+          // stragglers only: 8x fewer polling loads than sweeping them all
+          unsigned spins = 0;
           w[0] = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-#pragma unroll
-        for (int st = 1; st < 8; ++st)
-          w[st] = __hip_atomic_load(src + 4 * st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        for (;;) {
-          bool ok = true;
-#pragma unroll
-          for (int st = 0; st < 8; ++st) ok &= (unsigned)(w[st] >> 32) == (unsigned)gs;
-          if (ok || gru_dead(&s_err)) break;
-          __builtin_amdgcn_s_sleep(1);
-          if (++spins > GRU_SPIN) {
-            gru_fail(sync, host_err, 4u);
-            s_err = 1;
-            break;
+          while ((unsigned)(w[0] >> 32) != (unsigned)gs && !gru_dead(&s_err)) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > GRU_SPIN) {
+              gru_fail(sync, host_err, 4u);
+              s_err = 1;
+              break;
+            }
+            w[0] = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           }
 #pragma unroll
-          for (int st = 0; st < 8; ++st)
-            if ((unsigned)(w[st] >> 32) != (unsigned)gs)
-              w[st] = __hip_atomic_load(src + 4 * st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          for (int st = 1; st < 8; ++st)
+            w[st] = __hip_atomic_load(src + 4 * st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          for (;;) {
+            bool ok = true;
+#pragma unroll
+            for (int st = 0; st < 8; ++st) ok &= (unsigned)(w[st] >> 32) == (unsigned)gs;
+            if (ok || gru_dead(&s_err)) break;
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > GRU_SPIN) {
+              gru_fail(sync, host_err, 4u);
+              s_err = 1;
+              break;
+            }
+#pragma unroll
+            for (int st = 0; st < 8; ++st)
+              if ((unsigned)(w[st] >> 32) != (unsigned)gs)
+                w[st] = __hip_atomic_load(src + 4 * st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+#pragma unroll
+          for (int st = 0; st < 8; ++st) hb[st] = s > 0 ? __uint_as_float((unsigned)w[st]) : 0.f;
+        } else {
+#pragma unroll
+          for (int st = 0; st < 8; ++st) hb[st] = 0.f;
         }
+        f32x4_g acc[3][RT];
 #pragma unroll
-        for (int st = 0; st < 8; ++st) hb[st] = s > 0 ? __uint_as_float((unsigned)w[st]) : 0.f;
-      } else {
+        for (int g = 0; g < 3; ++g)
 #pragma unroll
-        for (int st = 0; st < 8; ++st) hb[st] = 0.f;
-      }
-      float nx0 = 0.f, nx1 = 0.f, nx2 = 0.f;
-      if (s + 1 < T) load_gi(s + 1, nx0, nx1, nx2);   // next step's inputs, in flight across this one
-      // ---- recurrent product: 3 RT independent chains over this eighth's 32 k
-      f32x4_g acc[3][RT];
+          for (int rt = 0; rt < RT; ++rt) acc[g][rt] = f32x4_g{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int g = 0; g < 3; ++g)
+        for (int st = 0; st < 8; ++st)
 #pragma unroll
-        for (int rt = 0; rt < RT; ++rt) acc[g][rt] = f32x4_g{0.f, 0.f, 0.f, 0.f};
+          for (int g = 0; g < 3; ++g)
 #pragma unroll
-      for (int st = 0; st < 8; ++st)
+            for (int rt = 0; rt < RT; ++rt)
+              acc[g][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(Wf[g][rt][st], hb[st], acc[g][rt], 0, 0, 0);
+        // D[m][n]: lane (q, n) register i holds row 4 q + i
+        float* pw = smem + (s & 1) * PB + e * 3 * U * GRU_PLD + (4 * q) * GRU_PLD + n16;
 #pragma unroll
         for (int g = 0; g < 3; ++g)
 #pragma unroll
           for (int rt = 0; rt < RT; ++rt)
-            acc[g][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(Wf[g][rt][st], hb[st], acc[g][rt], 0, 0, 0);
-      // D[m][n]: lane (q, n) register i holds row 4 q + i
-      float* pw = smem + (s & 1) * PB + e * 3 * U * GRU_PLD + (4 * q) * GRU_PLD + n16;
 #pragma unroll
-      for (int g = 0; g < 3; ++g)
+            for (int i = 0; i < 4; ++i) pw[(g * U + 16 * rt + i) * GRU_PLD] = acc[g][rt][i];
+        if (gl) {
 #pragma unroll
-        for (int rt = 0; rt < RT; ++rt)
+          for (int g = 0; g < 3; ++g) gin[(((s & 1) * 3 + g) * U + lu) * 16 + lc] = gcur[g];
+        }
 #pragma unroll
-          for (int i = 0; i < 4; ++i) pw[(g * U + 16 * rt + i) * GRU_PLD] = acc[g][rt][i];
-      __syncthreads();
-      // ---- gates, publish
-      if (gate_thr) {
+        for (int g = 0; g < 3; ++g) gcur[g] = gnext[g];
+        gru_lds_barrier();
+      }
+    }
+  } else {
+    // ================= gate wave: thread = (unit gu, clip gc) =================
+    const int gt = tid - 8 * 64;
+    const int gu = gt >> 4, gc = gt & 15;
+    const float br = bhh[dir * 768 + U * p + gu];
+    const float bz = bhh[dir * 768 + 256 + U * p + gu];
+    const float bn = bhh[dir * 768 + 512 + U * p + gu];
+    int j = 0;
+    for (int grp = slot; grp < ngroups; grp += nslots, ++j) {
+      const int c0 = grp * 16;
+      const int nc = min(16, B - c0);
+      float hreg = 0.f;                          // h_{t-1} of this (clip, unit): own slice, same thread every step
+      for (int s = 0; s < T; ++s) {
+        const int gs = j * T + s;
+        const int t = dir ? T - 1 - s : s;
+        gru_lds_barrier();                       // the product waves' partials and gate inputs of step s
         float hv = 0.f;
         if (gc < nc) {
+          const float* gq = gin + ((s & 1) * 3 * U + gu) * 16 + gc;
+          const float gi0 = gq[0], gi1 = gq[U * 16], gi2 = gq[2 * U * 16];
           const float* pp = smem + (s & 1) * PB + gu * GRU_PLD + gc;
           constexpr int GS = U * GRU_PLD;        // gate stride; eighth stride 3 GS
           float ghr = pp[0], ghz = pp[GS], ghn = pp[2 * GS];
@@ -683,7 +709,7 @@ __global__ __launch_bounds__(512) void gru_tag_kernel(const float* __restrict__ 
           ghz += bz;
           ghn += bn;
           const float hn = gru_cell(gi0, gi1, gi2, ghr, ghz, ghn, hreg);
-          hv = s_err ? __builtin_nanf("") : hn;  // NaN propagates to every slice
+          hv = gru_dead(&s_err) ? __builtin_nanf("") : hn;   // NaN propagates to every slice
           __hip_atomic_store(Xp + (gs & 1) * 16 * 256 + gc * 256 + U * p + gu,
                              ((unsigned long long)(gs + 1) << 32) | __float_as_uint(hv), __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
@@ -691,9 +717,6 @@ __global__ __launch_bounds__(512) void gru_tag_kernel(const float* __restrict__ 
         }
         hreg = hv;
       }
-      gi0 = nx0;
-      gi1 = nx1;
-      gi2 = nx2;
     }
   }
 }
@@ -712,11 +735,12 @@ static void launch_gru_tag(const float* G, int B, int T, const float* whh, const
                            unsigned long long* X, size_t sync_bytes, unsigned* host_err, hipStream_t s) {
   const int ngroups = (B + 15) / 16;
   const int nslots = ngroups < GRU_MAX_SLOTS ? ngroups : GRU_MAX_SLOTS;
-  const LaunchInfo li = launch_info(reinterpret_cast<const void*>(gru_tag_kernel<NS>), 512, gru_tag_lds<NS>());
+  const LaunchInfo li =
+      launch_info(reinterpret_cast<const void*>(gru_tag_kernel<NS>), gru_tag_threads<NS>(), gru_tag_lds<NS>());
   if (!li.ok) return;
   // sync block + the granules of the pairs in use (every tag 0)
   (void)hipMemsetAsync(sync, 0, sync_bytes + (size_t)2 * nslots * 2 * 16 * 256 * 8, s);
-  hipLaunchKernelGGL(gru_tag_kernel<NS>, dim3(8 * NS), dim3(512), li.dyn, s, G, B, T, whh, bhh, H, X, sync, nslots,
+  hipLaunchKernelGGL(gru_tag_kernel<NS>, dim3(8 * NS), dim3(gru_tag_threads<NS>()), li.dyn, s, G, B, T, whh, bhh, H, X, sync, nslots,
                      host_err);
 }
 

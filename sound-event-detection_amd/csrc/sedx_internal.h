@@ -253,8 +253,8 @@ size_t gru_coop_workspace_bytes(int B);
 // when the placement allows it (else always the global protocol).
 // host_err (nullable): host-mapped word OR-ed with the failure code when a
 // bounded hand-off spin times out (outputs of that launch are then NaN).
-// variant (exact, B > 8): 0 the 16-clip data-tagged kernel with 16 slices,
-// 1 the same with 8 slices, 2 the 32-clip flag hand-off kernel (x3 always).
+// variant (exact, B > 8): 2 the 32-clip flag hand-off kernel (default; x3
+// always), 0 the 16-clip data-tagged kernel with 16 slices, 1 with 8 slices.
 void launch_gru_coop(const float* G, int B, int T, const float* whh, const float* bhh, float* H,
                      void* ws, bool exact, bool allow_fast, int variant, unsigned* host_err, hipStream_t s);
 

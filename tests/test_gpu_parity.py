@@ -193,6 +193,25 @@ def test_gru_handoff_modes_bit_identical(prec):
     assert np.array_equal(outs[1], outs[0])
 
 
+@pytest.mark.parametrize('n_clips', [40, 80])
+def test_gru_tag_kernels_bit_identical(n_clips):
+    """The opt-in data-tagged recurrences (SEDX_GRU_KERNEL_TAG16 / TAG8: 16-clip
+    groups, granules straight into v_mfma_f32_16x16x4_f32 operands) keep the
+    exact kernels' arithmetic contract (eight in-order K partials, summed in
+    order): bit-identical to the default 32-clip kernel, ragged last group and
+    more groups than resident slots (80 clips = 5 groups of 16) included."""
+    from sedx import _lib
+    m = build(GRU).set_precision('exact')
+    wave = synth.make_waveforms(n_clips, seconds=2.0, sample_rate=16000, seed=n_clips + 3)
+    outs = {}
+    for knob in (0, 2, 3):     # COOP (default), TAG16, TAG8
+        _tune(m, _lib.TUNE_GRU_KERNEL, knob)
+        outs[knob] = run(m, wave)['framewise_output']
+    _tune(m, _lib.TUNE_GRU_KERNEL, 0)
+    assert np.isfinite(outs[0]).all()
+    assert np.array_equal(outs[2], outs[0]) and np.array_equal(outs[3], outs[0])
+
+
 def test_gru_exact_recurrence_is_fp32():
     """Exact mode runs the recurrence on fp32 MFMA operands: it agrees with
     the per-(clip, direction) fp32-FMA kernel and the oracle far inside the

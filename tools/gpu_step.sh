@@ -19,7 +19,11 @@ if [ -n "$GRU" ]; then
   done
 fi
 if [ -z "$NOTEST" ]; then
-  step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ${PYTEST_ARGS} || exit $?
+  if [ -n "$PYTEST_K" ]; then
+    step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "$PYTEST_K" || exit $?
+  else
+    step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread || exit $?
+  fi
 fi
 if [ -z "$NOBENCH" ]; then
   step bench 900 python bench.py --steps ${BENCH_STEPS:-20} --warmup 3 ${BENCH_ARGS} || exit $?
