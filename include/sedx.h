@@ -209,11 +209,20 @@ sedx_status sedx_set_precision(sedx_handle* h, int32_t mode);
  *                         when all 8 slices share an XCD, else global;
  *                         SEDX_GRU_HANDOFF_GLOBAL: always the global protocol
  *                         (same bytes, bit-identical results).
+ *  SEDX_TUNE_MEL_MFMA     (n_fft 512) 1 (default): the mel projection of the
+ *                         log-mel frontend on v_mfma_f32_16x16x4_f32 over each
+ *                         16-band tile's bin range; 0: VALU band sums.  The
+ *                         same in-order fma chain per band: bit-identical.
  *  SEDX_TUNE_WINO_BLOCK1  (SEDX_PRECISION_WINOGRAD only) 1 (default): block 1's
  *                         conv2 as Winograd F(2x2,3x3) too, fed by a separate
  *                         conv1 launch (the 64-channel activation goes through
  *                         HBM); 0: block 1 as the direct fused fp32 kernel. */
-typedef enum { SEDX_TUNE_GRU_KERNEL = 0, SEDX_TUNE_GRU_HANDOFF = 1, SEDX_TUNE_WINO_BLOCK1 = 2 } sedx_tuning_knob;
+typedef enum {
+  SEDX_TUNE_GRU_KERNEL = 0,
+  SEDX_TUNE_GRU_HANDOFF = 1,
+  SEDX_TUNE_WINO_BLOCK1 = 2,
+  SEDX_TUNE_MEL_MFMA = 3
+} sedx_tuning_knob;
 enum { SEDX_GRU_KERNEL_COOP = 0, SEDX_GRU_KERNEL_SIMPLE = 1, SEDX_GRU_KERNEL_TAG16 = 2, SEDX_GRU_KERNEL_TAG8 = 3 };
 enum { SEDX_GRU_HANDOFF_AUTO = 0, SEDX_GRU_HANDOFF_GLOBAL = 1 };
 sedx_status sedx_set_tuning(sedx_handle* h, int32_t knob, int32_t value);

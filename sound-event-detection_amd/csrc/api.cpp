@@ -31,6 +31,8 @@ struct DevWeights {
   float* window = nullptr;
   float* mel_w = nullptr;
   float* mel_tab = nullptr;   // logmel512_kernel's per-(slot, lane) band weights
+  float* mel_mt = nullptr;    // logmel512_kernel's MFMA mel table (FrontendParams::mel_mt)
+  int32_t mt_klo[4] = {}, mt_ns[4] = {}, mt_off[4] = {}, mt_floats = 0;
   int32_t mel_wmax = 0;
   int32_t* mel_off = nullptr;
   int32_t* mel_lo = nullptr;
@@ -89,6 +91,7 @@ struct sedx_handle {
   int gru_kernel = SEDX_GRU_KERNEL_COOP;   // sedx_set_tuning
   int gru_handoff = SEDX_GRU_HANDOFF_AUTO;
   int wino_block1 = 1;                     // SEDX_TUNE_WINO_BLOCK1
+  int mel_mfma = 1;                        // SEDX_TUNE_MEL_MFMA
   // sedx_set_capture: copy one stage's output of every later forward
   int cap_stage = -1;
   float* cap_buf = nullptr;
@@ -504,6 +507,17 @@ sedx_status window_geometry(const sedx_handle* h, int64_t L_clip, float sample_d
   return SEDX_OK;
 }
 
+// the MFMA mel table (nullptr when the host did not build one)
+void set_mel_mt(FrontendParams& p, const DevWeights& w, int on) {
+  p.mel_mt = on ? w.mel_mt : nullptr;
+  for (int j = 0; j < 4; ++j) {
+    p.mt_klo[j] = w.mt_klo[j];
+    p.mt_ns[j] = w.mt_ns[j];
+    p.mt_off[j] = w.mt_off[j];
+  }
+  p.mt_floats = w.mt_floats;
+}
+
 template <typename T>
 T* carve(char*& p, size_t n) {
   T* r = reinterpret_cast<T*>(p);
@@ -563,6 +577,10 @@ sedx_status sedx_set_tuning(sedx_handle* h, int32_t knob, int32_t value) {
     case SEDX_TUNE_WINO_BLOCK1:
       if (value != 0 && value != 1) break;
       h->wino_block1 = value;
+      return SEDX_OK;
+    case SEDX_TUNE_MEL_MFMA:
+      if (value != 0 && value != 1) break;
+      h->mel_mfma = value;
       return SEDX_OK;
     default:
       return fail(h, SEDX_EINVAL, "unknown tuning knob %d", (int)knob);
@@ -688,6 +706,32 @@ sedx_status sedx_finalize_weights(sedx_handle* h) {
         mel_tab[((size_t)q * 16 + b) * FE16_MEL_MW + e] = mel_w[mel_off[m] + e];
     }
   if (mel_w.empty()) mel_w.push_back(0.f);
+  // the MFMA mel path's table (n_fft 512): per 16-band tile j the bin range
+  // its bands cover, in 4-bin steps: [step][4 bins][16 bands] of melW (zero
+  // outside a band, and past the last bin)
+  std::vector<float> mel_mt;
+  int32_t mt_klo[4] = {}, mt_ns[4] = {}, mt_off[4] = {};
+  if (nfft == 512) {
+    for (int j = 0; j < 4; ++j) {
+      int klo = K, khi = -1;
+      for (int m = 16 * j; m < 16 * j + 16; ++m) {
+        const int wd = mel_off[m + 1] - mel_off[m];
+        if (wd <= 0) continue;
+        klo = std::min(klo, mel_lo[m]);
+        khi = std::max(khi, mel_lo[m] + wd - 1);
+      }
+      const int ns = khi < klo ? 0 : (khi - klo + 1 + 3) / 4;
+      mt_klo[j] = ns ? klo : 0;
+      mt_ns[j] = ns;
+      mt_off[j] = (int32_t)mel_mt.size();
+      for (int st = 0; st < ns; ++st)
+        for (int kk = 0; kk < 4; ++kk)
+          for (int n = 0; n < 16; ++n) {
+            const int k = klo + 4 * st + kk, m = 16 * j + n;
+            mel_mt.push_back(k < K ? melW[(size_t)k * 64 + m] : 0.f);
+          }
+    }
+  }
 
   auto bn_fold = [&](const std::string& p, int n, std::vector<double>& sc, std::vector<float>& mu,
                      std::vector<float>& bi) {
@@ -882,6 +926,15 @@ sedx_status sedx_finalize_weights(sedx_handle* h) {
   add((void**)&W.window, window.data(), window.size() * 4);
   add((void**)&W.mel_w, mel_w.data(), mel_w.size() * 4);
   add((void**)&W.mel_tab, mel_tab.data(), mel_tab.size() * 4);
+  if (!mel_mt.empty() && mel_mt.size() <= (size_t)FE_MT_MAX_FLOATS) {
+    add((void**)&W.mel_mt, mel_mt.data(), mel_mt.size() * 4);
+    for (int j = 0; j < 4; ++j) {
+      W.mt_klo[j] = mt_klo[j];
+      W.mt_ns[j] = mt_ns[j];
+      W.mt_off[j] = mt_off[j];
+    }
+    W.mt_floats = (int32_t)mel_mt.size();
+  }
   W.mel_wmax = mel_wmax;
   add((void**)&W.mel_off, mel_off.data(), mel_off.size() * 4);
   add((void**)&W.mel_lo, mel_lo.data(), mel_lo.size() * 4);
@@ -1078,6 +1131,7 @@ static sedx_status forward_wave(sedx_handle* h, const float* d_wave, const int16
   p.window = h->w.window;
   p.mel_w = h->w.mel_w;
   p.mel_tab = h->w.mel_tab;
+  set_mel_mt(p, h->w, h->mel_mfma);
   p.mel_wmax = h->w.mel_wmax;
   p.mel_off = h->w.mel_off;
   p.mel_lo = h->w.mel_lo;
@@ -1255,6 +1309,7 @@ static sedx_status forward_windows_impl(sedx_handle* h, const float* d_audio, in
   p.window = h->w.window;
   p.mel_w = h->w.mel_w;
   p.mel_tab = h->w.mel_tab;
+  set_mel_mt(p, h->w, h->mel_mfma);
   p.mel_wmax = h->w.mel_wmax;
   p.mel_off = h->w.mel_off;
   p.mel_lo = h->w.mel_lo;

@@ -302,23 +302,42 @@ __device__ __forceinline__ void dft16(float2 (&x)[16]) {
 
 constexpr int FE16_WAVES = 4;
 constexpr int FE16_ROW = 36;                       // floats per transpose row (16 float2 + pad)
-constexpr int FE16_FRAME = 16 * FE16_ROW + 16;     // floats per frame (transpose, then power); 592 = 16 mod 64:
-                                                   // the four frames of a wave start 16 banks apart
+// floats per frame (transpose, then power).  592 = 16 mod 64: the four frames
+// of a wave start 16 banks apart (band-sum path); 596 = 20 mod 64: the 16
+// frames of a workgroup start 20 banks apart, so the MFMA mel path's A
+// fragment reads (lane: frame l & 15, bin + (l >> 4)) hit 64 distinct banks
+template <bool MT>
+constexpr int fe16_frame() { return MT ? 16 * FE16_ROW + 20 : 16 * FE16_ROW + 16; }
 constexpr int FE16_MW = FE16_MEL_MW;               // widest mel band of the table path (bins, multiple of 4)
 __device__ __forceinline__ int fe16_band(int b, int q) { return q == 0 ? b : q == 1 ? 31 - b : q == 2 ? 32 + b : 63 - b; }
+typedef float fe_f32x4 __attribute__((ext_vector_type(4)));
 
-template <bool I16>
+// MT (mel on the matrix pipe): the workgroup's 16 frames (4 waves x 4) meet
+// in LDS after their FFTs; wave w then computes mel bands 16 w .. 16 w + 15
+// of all 16 frames as v_mfma_f32_16x16x4_f32 over the bin range those bands
+// cover (host table: per band tile the first bin and the 4-bin steps,
+// weights [step][4 bins][16 bands], zero outside each band).  A band's value
+// is the in-order fma chain over its bins from 0 (the MFMA is the in-order
+// fma chain over its four k; zero weights leave the chain unchanged for the
+// finite, non-negative powers), i.e. the band-sum path's bits, with ~1/4 of
+// its instructions per frame.
+template <bool I16, bool MT>
 __global__ __launch_bounds__(64 * FE16_WAVES) void logmel512_kernel(FrontendParams p) {
   constexpr int NFFT = 512, N2 = 256;
+  constexpr int FE16_FRAME = fe16_frame<MT>();
   __shared__ __attribute__((aligned(16))) float s_fr[FE16_WAVES][4 * FE16_FRAME];
-  extern __shared__ float s_melw[];   // [p.mel_lds_floats]
+  extern __shared__ float s_melw[];   // [p.mel_lds_floats]: per-band weights, or the MT table
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int g = lane >> 4, b = lane & 15;
   const int nnz = p.mel_off[64];
   const bool mel_in_lds = nnz <= p.mel_lds_floats;
-  if (mel_in_lds && p.mel_wmax > FE16_MW)
-    for (int i = threadIdx.x; i < nnz; i += 64 * FE16_WAVES) s_melw[i] = p.mel_w[i];
+  if constexpr (MT) {
+    for (int i = threadIdx.x; i < p.mt_floats; i += 64 * FE16_WAVES) s_melw[i] = p.mel_mt[i];
+  } else {
+    if (mel_in_lds && p.mel_wmax > FE16_MW)
+      for (int i = threadIdx.x; i < nnz; i += 64 * FE16_WAVES) s_melw[i] = p.mel_w[i];
+  }
 
   // per-lane constants: window of its 32 samples, step-2 twiddles W256^(b k1),
   // unpack twiddles W512^(b + 16 k2), its four mel bands.  The twiddle and
@@ -342,11 +361,14 @@ __global__ __launch_bounds__(64 * FE16_WAVES) void logmel512_kernel(FrontendPara
   for (int k1 = 0; k1 < 16; ++k1) tw1[k1] = reinterpret_cast<const float2*>(stage)[(2 * b * k1) & (NFFT - 1)];
 #pragma unroll
   for (int k2 = 0; k2 < 9; ++k2) tw2[k2] = reinterpret_cast<const float2*>(stage)[b + 16 * k2];
-  int mlo[4], o0[4], o1[4];
-  float bmu[4], bsc[4], bbi[4];
+  // mel constants: band-sum path, lane b of frame row g sums bands
+  // fe16_band(b, q); MT path, lane l owns band 16 wave + (l & 15)
+  constexpr int NQ = MT ? 1 : 4;
+  int mlo[NQ], o0[NQ], o1[NQ];
+  float bmu[NQ], bsc[NQ], bbi[NQ];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int m = fe16_band(b, q);
+  for (int q = 0; q < NQ; ++q) {
+    const int m = MT ? 16 * wave + b : fe16_band(b, q);
     mlo[q] = p.mel_lo[m];
     o0[q] = p.mel_off[m];
     o1[q] = p.mel_off[m + 1];
@@ -357,13 +379,15 @@ __global__ __launch_bounds__(64 * FE16_WAVES) void logmel512_kernel(FrontendPara
   // band weights per (slot q, lane b), zero-padded to the widest band rounded
   // to 4 (host table; fma(P, 0, acc) == acc exactly for finite P, so the
   // padded chain gives the band's own bits)
-  __shared__ __attribute__((aligned(16))) float s_wt[4 * 16 * FE16_MW];
+  __shared__ __attribute__((aligned(16))) float s_wt[MT ? 4 : 4 * 16 * FE16_MW];
   const int wmax = p.mel_wmax;
   const bool mel_table = wmax <= FE16_MW;
-  static_assert((4 * 16 * FE16_MW) % (64 * FE16_WAVES) == 0, "table fill");
+  if constexpr (!MT) {
+    static_assert((4 * 16 * FE16_MW) % (64 * FE16_WAVES) == 0, "table fill");
 #pragma unroll
-  for (int k = 0; k < 4 * 16 * FE16_MW / (64 * FE16_WAVES); ++k)
-    s_wt[threadIdx.x + 64 * FE16_WAVES * k] = p.mel_tab[threadIdx.x + 64 * FE16_WAVES * k];
+    for (int k = 0; k < 4 * 16 * FE16_MW / (64 * FE16_WAVES); ++k)
+      s_wt[threadIdx.x + 64 * FE16_WAVES * k] = p.mel_tab[threadIdx.x + 64 * FE16_WAVES * k];
+  }
   __syncthreads();
 
   const int total = p.n_clips * p.n_win * p.T;
@@ -411,17 +435,22 @@ __global__ __launch_bounds__(64 * FE16_WAVES) void logmel512_kernel(FrontendPara
       }
   };
 
+  // workgroup groups of 16 frames (4 per wave): every wave runs every group
+  // of its workgroup (the MT path's barriers); frames past the end compute
+  // on zeros and are not stored
   const int ngroups = (total + 3) >> 2;
-  int gi = (int)blockIdx.x * FE16_WAVES + wave;
-  const int gstride = (int)gridDim.x * FE16_WAVES;
+  const int nwg = (ngroups + FE16_WAVES - 1) / FE16_WAVES;
+  int G = (int)blockIdx.x;
   float v[32];
-  if (gi < ngroups) load(4 * gi + g, v);
-  for (; gi < ngroups; gi += gstride) {
+  if (G < nwg) load(4 * (FE16_WAVES * G + wave) + g, v);
+  for (; G < nwg; G += (int)gridDim.x) {
+    const int gi = FE16_WAVES * G + wave;
     const int fr = 4 * gi + g;
+    if (!MT && gi >= ngroups) break;             // band-sum path: waves are independent
     float2 x[16];
 #pragma unroll
     for (int a = 0; a < 16; ++a) x[a] = make_float2(v[2 * a] * win[2 * a], v[2 * a + 1] * win[2 * a + 1]);
-    if (gi + gstride < ngroups) load(4 * (gi + gstride) + g, v);   // next group, in flight
+    if (G + (int)gridDim.x < nwg) load(4 * (FE16_WAVES * (G + (int)gridDim.x) + wave) + g, v);   // next group, in flight
     // 1-2: DFT over a, twiddle W256^(b k1)
     dft16(x);
 #pragma unroll
@@ -468,6 +497,28 @@ __global__ __launch_bounds__(64 * FE16_WAVES) void logmel512_kernel(FrontendPara
         fb[N2 / 2] = (Xa.x * Xa.x + Xa.y * Xa.y) * 0.25f;
       }
     }
+    if constexpr (MT) {
+      // 5 (MT): the workgroup's 16 power spectra -> mel tile of this wave
+      __syncthreads();
+      const int fl = lane & 15, kq = lane >> 4;
+      const int kl = p.mt_klo[wave], ns = p.mt_ns[wave];
+      const float* Pf = &s_fr[0][0] + fl * FE16_FRAME + kl + kq;   // frame fl: wave fl >> 2, row fl & 3
+      const float* Wt = s_melw + p.mt_off[wave] + lane;
+      const int kmax = N2 - kl - kq;              // bins past N2 read bin N2 (finite; its weight is 0)
+      fe_f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+      for (int st = 0; st < ns; ++st)
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(Pf[min(4 * st, kmax)], Wt[64 * st], acc, 0, 0, 0);
+      // D[frame][band]: lane l register i holds frame 4 (l >> 4) + i, band 16 wave + (l & 15)
+      const int band = 16 * wave + (lane & 15);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float db = 10.0f * log10f(fmaxf(acc[i], 1e-10f));
+        db = (db - bmu[0]) * bsc[0] + bbi[0];
+        const int f = 16 * G + 4 * (lane >> 4) + i;
+        if (f < total) p.out[(int64_t)f * 64 + band] = db;
+      }
+      __syncthreads();   // mel reads done before the next group's transpose writes
+    } else {
     wave_lds_sync();
     // 5: mel bands (bin order fma chains, the four bands interleaved so
     // each step has 16 LDS reads in flight), dB, bn0
@@ -516,6 +567,7 @@ __global__ __launch_bounds__(64 * FE16_WAVES) void logmel512_kernel(FrontendPara
       if (fr < total) p.out[(int64_t)fr * 64 + fe16_band(b, q)] = db;
     }
     wave_lds_sync();   // power reads done before the next group's transpose writes
+    }
   }
 }
 
@@ -553,13 +605,14 @@ static void launch_logmel_t(const FrontendParams& p0, int64_t total, hipStream_t
 
 // one wave per four frames; every wave walks several groups so the register
 // prefetch of the next group overlaps the current one
-template <bool I16>
+template <bool I16, bool MT>
 static void launch_logmel512(const FrontendParams& p0, int64_t total, hipStream_t s) {
-  const LaunchInfo li =
-      launch_info(reinterpret_cast<const void*>(logmel512_kernel<I16>), 64 * FE16_WAVES, fe_mel_lds<512>());
+  const size_t dyn = MT ? ((size_t)p0.mt_floats * 4 + 255) / 256 * 256 : fe_mel_lds<512>();
+  const LaunchInfo li = launch_info(reinterpret_cast<const void*>(logmel512_kernel<I16, MT>), 64 * FE16_WAVES,
+                                    MT ? FE_MT_MAX_FLOATS * 4 : fe_mel_lds<512>());
   if (!li.ok) return;
   FrontendParams p = p0;
-  p.mel_lds_floats = (int32_t)(li.dyn / 4);
+  p.mel_lds_floats = (int32_t)((MT ? dyn : li.dyn) / 4);
   const int64_t groups = (total + 3) / 4;
   int64_t blocks = (groups + FE16_WAVES - 1) / FE16_WAVES;
   // register-limited to 2 waves per SIMD (~215 VGPRs): two 4-wave workgroups
@@ -567,7 +620,8 @@ static void launch_logmel512(const FrontendParams& p0, int64_t total, hipStream_
   // and would say one)
   blocks = std::min<int64_t>(blocks, (int64_t)li.ncu * 2);
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL((logmel512_kernel<I16>), dim3((unsigned)blocks), dim3(64 * FE16_WAVES), li.dyn, s, p);
+  hipLaunchKernelGGL((logmel512_kernel<I16, MT>), dim3((unsigned)blocks), dim3(64 * FE16_WAVES), MT ? dyn : li.dyn,
+                     s, p);
 }
 
 void launch_logmel(const FrontendParams& p, int n_fft, hipStream_t s) {
@@ -580,8 +634,14 @@ void launch_logmel(const FrontendParams& p, int n_fft, hipStream_t s) {
       else launch_logmel_t<256, false>(p, total, s);
       break;
     case 512:
-      if (i16) launch_logmel512<true>(p, total, s);
-      else launch_logmel512<false>(p, total, s);
+      // the MFMA mel path when the host built its table (melW bands fit)
+      if (p.mel_mt && p.mt_floats <= FE_MT_MAX_FLOATS) {
+        if (i16) launch_logmel512<true, true>(p, total, s);
+        else launch_logmel512<false, true>(p, total, s);
+      } else {
+        if (i16) launch_logmel512<true, false>(p, total, s);
+        else launch_logmel512<false, false>(p, total, s);
+      }
       break;
     case 1024:
       if (i16) launch_logmel_t<1024, true>(p, total, s);

@@ -23,6 +23,7 @@ namespace sedx {
 // logmel512_kernel: lane b of a frame's 16-lane row sums mel bands b, 31 - b,
 // 32 + b, 63 - b (slots q = 0..3, balanced widths) from a zero-padded table
 constexpr int FE16_MEL_MW = 36;
+constexpr int FE_MT_MAX_FLOATS = 8192;    // MFMA mel table limit (32 KB of LDS)
 inline int fe16_band_host(int b, int q) { return q == 0 ? b : q == 1 ? 31 - b : q == 2 ? 32 + b : 63 - b; }
 struct FrontendParams {
   const float* audio;       // base pointer (fp32 samples)
@@ -44,6 +45,11 @@ struct FrontendParams {
   int32_t mel_lds_floats;   // set by launch_logmel: LDS room for the packed mel weights
   const float* mel_tab;     // [4][16][FE16_MEL_MW] band weights of slot q, lane b (n_fft 512 kernel)
   int32_t mel_wmax;         // widest band rounded up to 4 (> FE16_MEL_MW: the per-band loop)
+  // MFMA mel (n_fft 512): per 16-band tile j the first bin, the number of
+  // 4-bin steps and the table offset; table [step][4 bins][16 bands] per tile
+  const float* mel_mt;      // nullptr: the band-sum path
+  int32_t mt_klo[4], mt_ns[4], mt_off[4];
+  int32_t mt_floats;
   const float* bn_scale;    // [64] bn0 folded
   const float* bn_mean;     // [64]
   const float* bn_bias;     // [64]

@@ -510,6 +510,26 @@ def test_stage_goldens(mt, prec, golden_dir):
         assert e <= 1e-4 * scale, (stage, e)
 
 
+@pytest.mark.parametrize('n_clips,seconds', [(3, 10.0), (37, 2.0), (1, 0.05)])
+def test_mel_mfma_bit_identical(n_clips, seconds):
+    """The n_fft 512 frontend's mel projection on v_mfma_f32_16x16x4_f32 (16
+    frames x one 16-band tile per wave, over the tile's bin range) gives the
+    VALU band sums' bits (SEDX_TUNE_MEL_MFMA 0): the X0 stage (bn0 output) is
+    bit-identical, a ragged last 16-frame group and a 6-frame clip included,
+    and matches the reference's per-stage golden."""
+    from sedx import _lib
+    m = build(GRU)
+    wave = synth.make_waveforms(n_clips, seconds=seconds, sample_rate=16000, seed=n_clips)
+    T = wave.shape[1] // 160 + 1
+    x0 = {}
+    for on in (1, 0):
+        _tune(m, _lib.TUNE_MEL_MFMA, on)
+        x0[on] = _capture(m, 0, (n_clips, T, 64), wave)
+    _tune(m, _lib.TUNE_MEL_MFMA, 1)
+    assert np.isfinite(x0[1]).all()
+    assert np.array_equal(x0[1], x0[0])
+
+
 @pytest.mark.parametrize('mt', [GRU, TRF])
 def test_winograd_vs_exact(mt):
     """fp32 Winograd F(2x2,3x3) conv (blocks 2-4) against the direct fp32 conv

@@ -148,7 +148,7 @@ def test_dataparallel_replicas_reuse_the_source_handle(monkeypatch):
 
     class FakeNative(object):          # stands in for the libsedx handle (no GPU here)
         def __init__(self, cfg, idx):
-            self.device_index, self.signature, self.precision, self.h = idx, None, 'exact', None
+            self.device_index, self.signature, self.precision, self.h = idx, None, 'winograd', None
 
         def load(self, sd):
             loads.append(len(sd))

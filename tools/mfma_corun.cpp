@@ -73,6 +73,46 @@ __global__ __launch_bounds__(256) void probe_pk(float* out, int iters) {
   out[gid] = x.x + x.y * 3.0f + y.x * 5.0f + y.y * 7.0f;
 }
 
+// probe 4: packed fp32 results written to LDS and read back by other lanes
+// (the FFT frontend's pattern: v_pk_* arithmetic feeding ds_write, then
+// cross-lane ds_read), wave-local hand-offs only
+__global__ __launch_bounds__(256) void probe_pk_lds(float* out, int iters) {
+  __shared__ f32x2 ring[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int gid = blockIdx.x * 256 + threadIdx.x;
+  f32x2 x = {1.0f + gid * 1e-6f, 0.5f - gid * 1e-7f}, y = {0.25f, -0.125f};
+  const f32x2 c = {0.999f, 1.0001f}, d = {1e-3f, -2e-3f};
+  for (int it = 0; it < iters; ++it) {
+    x = __builtin_elementwise_fma(x, c, y * d);
+    ring[w][lane] = x;                       // ds_write_b64 of a v_pk result
+    __builtin_amdgcn_s_waitcnt(0xc07f);      // lgkmcnt(0)
+    __builtin_amdgcn_wave_barrier();
+    const f32x2 o = ring[w][(lane * 37 + it) & 63];
+    y = y * c + o * d;
+    __builtin_amdgcn_wave_barrier();
+  }
+  out[gid] = x.x + x.y * 3.0f + y.x * 5.0f + y.y * 7.0f;
+}
+
+// probe 5: packed fp32 under a PARTIAL exec mask — a lane-dependent trip
+// count (lane l runs 8 + (l & 31) iterations, like the mel band sums whose
+// widths grow with the band), so the last iterations of each wave run with
+// only the upper lanes of each 32-lane half active
+__global__ __launch_bounds__(256) void probe_pk_div(float* out, int iters) {
+  const int lane = threadIdx.x & 63;
+  const int gid = blockIdx.x * 256 + threadIdx.x;
+  f32x2 x = {1.0f + gid * 1e-6f, 0.5f - gid * 1e-7f}, y = {0.25f, -0.125f};
+  const f32x2 c = {0.999f, 1.0001f}, d = {1e-3f, -2e-3f};
+  for (int it = 0; it < iters; ++it) {
+    const int n = 8 + (lane & 31);
+    for (int k = 0; k < n; ++k) {
+      x = __builtin_elementwise_fma(x, c, y * d);
+      y = y * c + x * d;
+    }
+  }
+  out[gid] = x.x + x.y * 3.0f + y.x * 5.0f + y.y * 7.0f;
+}
+
 // logmel-like gather: reflect-padded 64-bit sample indices, global loads
 __global__ __launch_bounds__(256) void probe_gather(const float* __restrict__ audio, int64_t L, int64_t T,
                                                     int64_t total, float* out) {
@@ -137,9 +177,11 @@ int main(int argc, char** argv) {
            bad_runs, R * 8, bad_vals);
     fflush(stdout);
   }
-  for (int probe = 3; probe >= 0; --probe) {
+  for (int probe = 5; probe >= 0; --probe) {
     auto launch = [&](float* o, hipStream_t s) {
-      if (probe == 3) hipLaunchKernelGGL(probe_pk, dim3(blocks), dim3(256), 0, s, o, 400);
+      if (probe == 5) hipLaunchKernelGGL(probe_pk_div, dim3(blocks), dim3(256), 0, s, o, 20);
+      else if (probe == 4) hipLaunchKernelGGL(probe_pk_lds, dim3(blocks), dim3(256), 0, s, o, 400);
+      else if (probe == 3) hipLaunchKernelGGL(probe_pk, dim3(blocks), dim3(256), 0, s, o, 400);
       else if (probe == 0) hipLaunchKernelGGL(probe_trans, dim3(blocks), dim3(256), 0, s, o, 200);
       else if (probe == 1) hipLaunchKernelGGL(probe_lds, dim3(blocks), dim3(256), 0, s, o, 200);
       else hipLaunchKernelGGL(probe_valu, dim3(blocks), dim3(256), 0, s, o, 400);
@@ -163,7 +205,7 @@ int main(int argc, char** argv) {
       hipDeviceSynchronize();
     }
     printf("probe %d (%s): %d of %d runs beside mfma_spin differ, %zu values (%s)\n", probe,
-           probe == 3 ? "packed fp32" : probe == 0 ? "VALU+trans" : probe == 1 ? "LDS" : "VALU fma", bad_runs, 8 * R, bad_vals,
+           probe == 5 ? "packed fp32, partial exec (divergent trip counts)" : probe == 4 ? "packed fp32 -> LDS -> other lanes" : probe == 3 ? "packed fp32" : probe == 0 ? "VALU+trans" : probe == 1 ? "LDS" : "VALU fma", bad_runs, 8 * R, bad_vals,
            hipGetErrorString(hipGetLastError()));
     fflush(stdout);
   }
