@@ -209,10 +209,14 @@ sedx_status sedx_set_precision(sedx_handle* h, int32_t mode);
  *                         when all 8 slices share an XCD, else global;
  *                         SEDX_GRU_HANDOFF_GLOBAL: always the global protocol
  *                         (same bytes, bit-identical results).
- *  SEDX_TUNE_MEL_MFMA     (n_fft 512) 1 (default): the mel projection of the
- *                         log-mel frontend on v_mfma_f32_16x16x4_f32 over each
- *                         16-band tile's bin range; 0: VALU band sums.  The
- *                         same in-order fma chain per band: bit-identical.
+ *  SEDX_TUNE_MEL_MFMA     (n_fft 512) 0 (default): the log-mel frontend's mel
+ *                         projection as VALU band sums; 1: on
+ *                         v_mfma_f32_16x16x4_f32, the workgroup's 16 frames x
+ *                         one 16-band tile per wave over the tile's bin range
+ *                         (the same in-order fma chain per band:
+ *                         bit-identical; measured 1.4x slower at B = 32: the
+ *                         tile's single MFMA chain and two workgroup barriers
+ *                         per 16 frames cost more than the band sums' VALU).
  *  SEDX_TUNE_WINO_BLOCK1  (SEDX_PRECISION_WINOGRAD only) 1 (default): block 1's
  *                         conv2 as Winograd F(2x2,3x3) too, fed by a separate
  *                         conv1 launch (the 64-channel activation goes through

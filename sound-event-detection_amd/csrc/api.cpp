@@ -91,7 +91,7 @@ struct sedx_handle {
   int gru_kernel = SEDX_GRU_KERNEL_COOP;   // sedx_set_tuning
   int gru_handoff = SEDX_GRU_HANDOFF_AUTO;
   int wino_block1 = 1;                     // SEDX_TUNE_WINO_BLOCK1
-  int mel_mfma = 1;                        // SEDX_TUNE_MEL_MFMA
+  int mel_mfma = 0;                        // SEDX_TUNE_MEL_MFMA (measured slower: opt-in)
   // sedx_set_capture: copy one stage's output of every later forward
   int cap_stage = -1;
   float* cap_buf = nullptr;

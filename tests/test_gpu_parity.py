@@ -512,9 +512,10 @@ def test_stage_goldens(mt, prec, golden_dir):
 
 @pytest.mark.parametrize('n_clips,seconds', [(3, 10.0), (37, 2.0), (1, 0.08)])
 def test_mel_mfma_bit_identical(n_clips, seconds):
-    """The n_fft 512 frontend's mel projection on v_mfma_f32_16x16x4_f32 (16
-    frames x one 16-band tile per wave, over the tile's bin range) gives the
-    VALU band sums' bits (SEDX_TUNE_MEL_MFMA 0): the X0 stage (bn0 output) is
+    """The n_fft 512 frontend's opt-in mel projection on
+    v_mfma_f32_16x16x4_f32 (SEDX_TUNE_MEL_MFMA 1: 16 frames x one 16-band tile
+    per wave, over the tile's bin range) gives the default VALU band sums'
+    bits: the X0 stage (bn0 output) is
     bit-identical, a ragged last 16-frame group and a 9-frame clip included,
     and matches the reference's per-stage golden."""
     from sedx import _lib
@@ -525,7 +526,7 @@ def test_mel_mfma_bit_identical(n_clips, seconds):
     for on in (1, 0):
         _tune(m, _lib.TUNE_MEL_MFMA, on)
         x0[on] = _capture(m, 0, (n_clips, T, 64), wave)
-    _tune(m, _lib.TUNE_MEL_MFMA, 1)
+    _tune(m, _lib.TUNE_MEL_MFMA, 0)
     assert np.isfinite(x0[1]).all()
     assert np.array_equal(x0[1], x0[0])
 
