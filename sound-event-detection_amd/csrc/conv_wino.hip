@@ -64,7 +64,11 @@ struct WinoGeom {
 #ifndef SEDX_WINO_NBUF
 #define SEDX_WINO_NBUF 3
 #endif
-  static constexpr int NBUF = TG == 4 ? SEDX_WINO_NBUF : 3;   // ring depth
+#ifndef SEDX_WINO_NBUF64
+#define SEDX_WINO_NBUF64 SEDX_WINO_NBUF
+#endif
+  // ring depth (F = 64: block 1's conv2 streams its 525 MB input from HBM)
+  static constexpr int NBUF = TG == 4 ? (F == 64 ? SEDX_WINO_NBUF64 : SEDX_WINO_NBUF) : 3;
   static constexpr int UW = W_SZ / 256;              // 1-KiB DMA units per chunk
   static constexpr int UA = PLP / 64;
   static constexpr int U = UW + UA;

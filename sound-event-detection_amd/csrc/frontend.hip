@@ -12,6 +12,8 @@
 //  dense ERB weight reduction / nfft, power_to_db(top_db=80), per-clip
 //  max-abs normalisation and int16 quantisation (utils/gammatone/fftweight.py:
 //  15-60,126-168; utils/features.py:361-370; utils/utilities.py:73-79).
+#include <type_traits>
+
 #include "sedx_internal.h"
 
 namespace sedx {
@@ -697,25 +699,64 @@ __device__ __forceinline__ double2 zmul(double2 a, double2 b) {
 __device__ __forceinline__ double2 zadd(double2 a, double2 b) { return make_double2(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ double2 zsub(double2 a, double2 b) { return make_double2(a.x - b.x, a.y - b.y); }
 
-// Stockham FFT of N2 complex points by P threads of the block (block barriers).
+// Stockham FFT of N2 complex points by P threads of the block (block
+// barriers).  The twiddles a thread multiplies by depend only on its thread
+// index and the stage, so they live in registers (ZTw slots, loaded once per
+// launch from the host table): the LDS holds just the two FFT buffers.
+template <int N2, int Ns>
+constexpr int zradix() { return ((N2 / Ns) % 4 == 0) ? 4 : 2; }
+// register slots of the stages from Ns on (butterflies per thread x (R - 1))
 template <int N2, int Ns, int P>
-__device__ __forceinline__ double2* zstockham(double2* X, double2* Y, const double2* tw, int tid) {
+constexpr int zslots() {
+  if constexpr (Ns >= N2) {
+    return 0;
+  } else {
+    constexpr int R = zradix<N2, Ns>();
+    constexpr int nb = N2 / R;
+    constexpr int bpt = (nb + P - 1) / P;
+    return (Ns > 1 ? bpt * (R - 1) : 0) + zslots<N2, Ns * R, P>();
+  }
+}
+template <int N2, int Ns, int P, int OFF, int NT>
+__device__ __forceinline__ void zload_tw(const double2* __restrict__ g_tw, double2 (&tw)[NT], int tid) {
+  if constexpr (Ns < N2) {
+    constexpr int NFFT = 2 * N2;
+    constexpr int R = zradix<N2, Ns>();
+    constexpr int nb = N2 / R;
+    constexpr int bpt = (nb + P - 1) / P;
+    constexpr int step = NFFT / (Ns * R);
+    if constexpr (Ns > 1) {
+#pragma unroll
+      for (int bb = 0; bb < bpt; ++bb) {
+        const int j = bb * P + tid;
+        const int k = j & (Ns - 1);
+#pragma unroll
+        for (int r = 1; r < R; ++r) tw[OFF + bb * (R - 1) + r - 1] = j < nb ? g_tw[r * k * step] : make_double2(0.0, 0.0);
+      }
+    }
+    zload_tw<N2, Ns * R, P, OFF + (Ns > 1 ? bpt * (R - 1) : 0)>(g_tw, tw, tid);
+  }
+}
+template <int N2, int Ns, int P, int OFF, int NT>
+__device__ __forceinline__ double2* zstockham(double2* X, double2* Y, const double2 (&tw)[NT], int tid) {
   if constexpr (Ns >= N2) {
     return X;
   } else {
-    constexpr int NFFT = 2 * N2;
-    constexpr int R = ((N2 / Ns) % 4 == 0) ? 4 : 2;
+    constexpr int R = zradix<N2, Ns>();
     constexpr int nb = N2 / R;
-    constexpr int step = NFFT / (Ns * R);
-    for (int j = tid; j < nb; j += P) {
+    constexpr int bpt = (nb + P - 1) / P;
+#pragma unroll
+    for (int bb = 0; bb < bpt; ++bb) {
+      const int j = bb * P + tid;
+      if (j >= nb) break;
       const int k = j & (Ns - 1);
       const int base = (j - k) * R + k;
       if constexpr (R == 4) {
         double2 v0 = X[j], v1 = X[j + nb], v2 = X[j + 2 * nb], v3 = X[j + 3 * nb];
         if constexpr (Ns > 1) {
-          v1 = zmul(v1, tw[k * step]);
-          v2 = zmul(v2, tw[2 * k * step]);
-          v3 = zmul(v3, tw[3 * k * step]);
+          v1 = zmul(v1, tw[OFF + bb * 3]);
+          v2 = zmul(v2, tw[OFF + bb * 3 + 1]);
+          v3 = zmul(v3, tw[OFF + bb * 3 + 2]);
         }
         const double2 a0 = zadd(v0, v2), a1 = zsub(v0, v2);
         const double2 b0 = zadd(v1, v3), b1 = zsub(v1, v3);
@@ -726,71 +767,113 @@ __device__ __forceinline__ double2* zstockham(double2* X, double2* Y, const doub
         Y[base + 3 * Ns] = zsub(a1, mib1);
       } else {
         double2 v0 = X[j], v1 = X[j + nb];
-        if constexpr (Ns > 1) v1 = zmul(v1, tw[k * step]);
+        if constexpr (Ns > 1) v1 = zmul(v1, tw[OFF + bb]);
         Y[base] = zadd(v0, v1);
         Y[base + Ns] = zsub(v0, v1);
       }
     }
     __syncthreads();
-    return zstockham<N2, Ns * R, P>(Y, X, tw, tid);
+    return zstockham<N2, Ns * R, P, OFF + (Ns > 1 ? bpt * (R - 1) : 0)>(Y, X, tw, tid);
   }
 }
 
 // Real-input spectrum bin k (0..N2) from the N2-point complex FFT Z of the
 // packed sequence z[m] = x[2m] + i x[2m+1].
 template <int N2>
-__device__ __forceinline__ double2 zreal_bin(const double2* Z, const double2* tw, int k) {
+__device__ __forceinline__ double2 zreal_bin(const double2* Z, double2 twk, int k) {
   const double2 A = Z[k & (N2 - 1)];
   const double2 Bz = Z[(N2 - k) & (N2 - 1)];
   const double2 E = make_double2(0.5 * (A.x + Bz.x), 0.5 * (A.y - Bz.y));
   const double2 O = make_double2(0.5 * (A.y + Bz.y), -0.5 * (A.x - Bz.x));
-  return zadd(E, zmul(tw[k], O));
+  return zadd(E, zmul(twk, O));
 }
 
 constexpr int GAMMA_SPEC_THREADS = 256;
 
 template <int NFFT>
-constexpr size_t gamma_spec_lds() {   // twiddles + window + two FFT buffers
-  return (size_t)NFFT * sizeof(double2) + (size_t)NFFT * sizeof(double) + (size_t)NFFT * sizeof(double2);
+constexpr size_t gamma_spec_lds() {   // the two FFT buffers
+  return (size_t)NFFT * sizeof(double2);
 }
 
+// One workgroup per frame at a time, walking frames.  Thread tid owns the
+// packed complex samples m = tid + 256 i: their window values, every
+// twiddle of its butterflies and of its unpack bins stay in registers for
+// the whole launch (LDS holds only the FFT buffers: several workgroups per
+// CU), and the next frame's samples are loaded while the current frame is
+// transformed.
 template <int NFFT>
 __global__ __launch_bounds__(GAMMA_SPEC_THREADS) void gamma_spec_kernel(GammaParams p) {
   constexpr int N2 = NFFT / 2;
   constexpr int NB = N2 + 1;
+  constexpr int P = GAMMA_SPEC_THREADS;
+  constexpr int PER = N2 / P;                                  // packed samples per thread
+  constexpr int NT = zslots<N2, 1, P>();
+  constexpr int UB = (NB + P - 1) / P;                         // unpack bins per thread
+  static_assert(N2 % P == 0, "whole packed samples per thread");
   extern __shared__ double2 s_gdyn[];
-  double2* s_tw = s_gdyn;                                      // [NFFT]
-  double2* X = s_gdyn + NFFT;                                  // [N2]
+  double2* X = s_gdyn;                                         // [N2]
   double2* Y = X + N2;                                         // [N2]
-  double* s_win = reinterpret_cast<double*>(Y + N2);           // [NFFT]
   const int tid = threadIdx.x;
-  for (int i = tid; i < NFFT; i += GAMMA_SPEC_THREADS) {
-    s_tw[i] = p.twiddle[i];
-    s_win[i] = p.window[i];
+  double2 tw[NT > 0 ? NT : 1];
+  if constexpr (NT > 0) zload_tw<N2, 1, P, 0>(p.twiddle, tw, tid);
+  double2 twu[UB];
+#pragma unroll
+  for (int i = 0; i < UB; ++i) {
+    const int k = tid + P * i;
+    twu[i] = k < NB ? p.twiddle[k] : make_double2(0.0, 0.0);
   }
-  __syncthreads();
+  double2 wv[PER];                                             // window of this thread's samples
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int m = tid + P * i;
+    wv[i] = make_double2(p.window[2 * m], p.window[2 * m + 1]);
+  }
   const int64_t total = (int64_t)p.B * p.T;
-  for (int64_t fr = blockIdx.x; fr < total; fr += gridDim.x) {
+  // samples of frame fr (zeros past the filled frames: the row is zeroed)
+  auto load = [&](int64_t fr, float2 (&v)[PER]) {
+    const int64_t b = fr / p.T;
+    const int t = (int)(fr - b * p.T);
+    if (fr >= total || t >= p.T_fill) {
+#pragma unroll
+      for (int i = 0; i < PER; ++i) v[i] = make_float2(0.f, 0.f);
+      return;
+    }
+    const float* src = p.audio + b * p.L + (int64_t)t * p.hop;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int m = tid + P * i;
+      v[i] = make_float2(src[2 * m], src[2 * m + 1]);
+    }
+  };
+  float2 v[PER];
+  int64_t fr = blockIdx.x;
+  load(fr, v);
+  for (; fr < total; fr += gridDim.x) {
     const int64_t b = fr / p.T;
     const int t = (int)(fr - b * p.T);
     double* row = p.mag + fr * p.kp;
     if (t >= p.T_fill) {        // column never written by specgram's loop: zeros
-      for (int k = tid; k < p.kp; k += GAMMA_SPEC_THREADS) row[k] = 0.0;
+      for (int k = tid; k < p.kp; k += P) row[k] = 0.0;
+      load(fr + gridDim.x, v);
       continue;
     }
-    const float* src = p.audio + b * p.L + (int64_t)t * p.hop;
-    for (int m = tid; m < N2; m += GAMMA_SPEC_THREADS)
-      X[m] = make_double2(s_win[2 * m] * (double)src[2 * m], s_win[2 * m + 1] * (double)src[2 * m + 1]);
-    __syncthreads();
-    const double2* Z = zstockham<N2, 1, GAMMA_SPEC_THREADS>(X, Y, s_tw, tid);
-    for (int k = tid; k < p.kp; k += GAMMA_SPEC_THREADS) {
-      double v = 0.0;
-      if (k < NB) {
-        const double2 Xk = zreal_bin<N2>(Z, s_tw, k);
-        v = hypot(Xk.x, Xk.y);    // numpy abs(complex)
-      }
-      row[k] = v;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int m = tid + P * i;
+      X[m] = make_double2(wv[i].x * (double)v[i].x, wv[i].y * (double)v[i].y);
     }
+    load(fr + gridDim.x, v);    // next frame's samples, in flight during this FFT
+    __syncthreads();
+    const double2* Z = zstockham<N2, 1, P, 0>(X, Y, tw, tid);
+#pragma unroll
+    for (int i = 0; i < UB; ++i) {
+      const int k = tid + P * i;
+      if (k < NB) {
+        const double2 Xk = zreal_bin<N2>(Z, twu[i], k);
+        row[k] = hypot(Xk.x, Xk.y);   // numpy abs(complex)
+      }
+    }
+    for (int k = NB + tid; k < p.kp; k += P) row[k] = 0.0;   // row padding
     __syncthreads();            // Z read before the next frame's writes
   }
 }
@@ -804,70 +887,107 @@ __device__ __forceinline__ double ord2d(unsigned long long u) {
 }
 
 // db[b][ch][t] = 10 log10(max(1e-10, sum_k W[ch][k] |X_t[k]| / nfft)) over a
-// tile of 64 frames of one clip x 64 channels; 256 threads, 4 x 4 outputs
-// each, K staged through LDS 32 bins at a time.
+// tile of 64 frames of one clip x 64 channels on the f64 matrix pipe:
+// v_mfma_f64_16x16x4f64, wave w = frames 16 w .. 16 w + 15 x the 4
+// 16-channel tiles, K in 4-bin steps (one A and four B ds_read_b64 per 4
+// MFMAs; the VALU form of this product was LDS-bandwidth bound at 4 B per
+// FMA).  K staged in blocks of 32 bins: LDS double buffer, loads issued two
+// blocks ahead into registers (the magnitudes stream from HBM: one block's
+// MFMAs are shorter than a load's latency), one barrier per block.  Two
+// workgroups per CU.  The int16 codes are
+// checked against the reference's (test_gamma*): f64 sums in a different
+// order move a value by ~1e-16 relative, a code step is ~3e-5 relative.
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+constexpr int ERB_TF = 64, ERB_KB = 32;
 __global__ __launch_bounds__(256) void gamma_erb_kernel(GammaParams p) {
-  __shared__ double As[32][64];   // [k][frame]
-  __shared__ double Ws[32][64];   // [k][channel]
+  __shared__ __attribute__((aligned(16))) double As[2][ERB_KB][ERB_TF];   // [k][frame]
+  __shared__ __attribute__((aligned(16))) double Ws[2][ERB_KB][64];       // [k][channel]
   __shared__ double s_red[2][4];
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int64_t b = blockIdx.y;
-  const int t0 = blockIdx.x * 64;
-  const int tf = tid >> 4, tc = tid & 15;
-  double acc[4][4] = {};
+  const int t0 = blockIdx.x * ERB_TF;
   const double* M = p.mag + b * (int64_t)p.T * p.kp;
+  // staging roles: A: frame lf, bins lk .. lk + 7 of the block; W: 8
+  // contiguous doubles of the [k][64] block
   const int lf = tid >> 2, lk = (tid & 3) * 8;
   const bool frame_ok = t0 + lf < p.T;
   const double* arow = M + (int64_t)(frame_ok ? t0 + lf : 0) * p.kp + lk;
-  for (int k0 = 0; k0 < p.kp; k0 += 32) {
+  // register stages: blocks kb + 1, kb + 2 (native vectors: HIP's double2
+  // struct copies kept these in scratch)
+  typedef double d2v __attribute__((ext_vector_type(2)));
+  d2v ra[2][4], rw[2][4];
+  auto gload = [&](int k0, int r) __attribute__((always_inline)) {
 #pragma unroll
-    for (int j = 0; j < 8; j += 2) {
-      double2 v = frame_ok ? *reinterpret_cast<const double2*>(arow + k0 + j) : make_double2(0.0, 0.0);
-      As[lk + j][lf] = v.x;
-      As[lk + j + 1][lf] = v.y;
+    for (int j = 0; j < 4; ++j)
+      ra[r][j] = frame_ok ? *reinterpret_cast<const d2v*>(arow + k0 + 2 * j) : d2v{0.0, 0.0};
+    const d2v* wsrc = reinterpret_cast<const d2v*>(p.weightsT + (int64_t)k0 * 64) + 4 * tid;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) rw[r][j] = wsrc[j];
+  };
+  auto swrite = [&](int buf, int r) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      As[buf][lk + 2 * j][lf] = ra[r][j][0];
+      As[buf][lk + 2 * j + 1][lf] = ra[r][j][1];
     }
-    const double* wsrc = p.weightsT + (int64_t)k0 * 64;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) (&Ws[0][0])[tid + 256 * j] = wsrc[tid + 256 * j];
-    __syncthreads();
-#pragma unroll 4
-    for (int kk = 0; kk < 32; ++kk) {
-      const double2 a01 = *reinterpret_cast<const double2*>(&As[kk][tf * 4]);
-      const double2 a23 = *reinterpret_cast<const double2*>(&As[kk][tf * 4 + 2]);
-      const double2 w01 = *reinterpret_cast<const double2*>(&Ws[kk][tc * 4]);
-      const double2 w23 = *reinterpret_cast<const double2*>(&Ws[kk][tc * 4 + 2]);
-      const double a[4] = {a01.x, a01.y, a23.x, a23.y};
-      const double w[4] = {w01.x, w01.y, w23.x, w23.y};
+    for (int j = 0; j < 4; ++j) reinterpret_cast<d2v*>(&Ws[buf][0][0])[4 * tid + j] = rw[r][j];
+  };
+  f64x4 acc[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+  for (int n = 0; n < 4; ++n) acc[n] = f64x4{0.0, 0.0, 0.0, 0.0};
+  const int kq = lane >> 4, c16 = lane & 15;
+  const int nkb = p.kp / ERB_KB;                 // kp is a multiple of 32
+  gload(0, 0);
+  if (nkb > 1) gload(ERB_KB, 1);
+  swrite(0, 0);
+  __syncthreads();
+  // block kb: LDS buffer kb & 1; register stage (kb + 1) & 1 holds block kb + 1.
+  // Blocks in pairs so every register-stage index is a compile-time constant
+  // (a runtime index would put the stages in scratch memory)
+  auto block = [&](int kb, auto par) __attribute__((always_inline)) {   // inlined: ra / rw stay in VGPRs
+    constexpr int PAR = decltype(par)::value;    // kb & 1
+    if (kb >= nkb) return;
+    if (kb + 2 < nkb) gload((kb + 2) * ERB_KB, PAR);   // two blocks ahead (stage PAR was written out)
 #pragma unroll
-        for (int c = 0; c < 4; ++c) acc[i][c] = fma(a[i], w[c], acc[i][c]);
+    for (int st = 0; st < ERB_KB / 4; ++st) {
+      // A[m = frame][k]: lane (kq, m = c16); B[k][n = channel]: lane (kq, n = c16)
+      const double a = As[PAR][4 * st + kq][16 * w + c16];
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+        acc[n] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, Ws[PAR][4 * st + kq][16 * n + c16], acc[n], 0, 0, 0);
     }
+    if (kb + 1 < nkb) swrite(PAR ^ 1, PAR ^ 1);  // the other buffer: last read in block kb - 1
     __syncthreads();
+  };
+  for (int kb = 0; kb < nkb; kb += 2) {
+    block(kb, std::integral_constant<int, 0>{});
+    block(kb + 1, std::integral_constant<int, 1>{});
   }
+  // D[frame][channel] (f64 16x16 layout, cdna_hip_programming.md): lane
+  // (q = lane >> 4, c16) register i holds frame 16 w + q + 4 i, channel 16 n + c16
   double mx = -INFINITY, mn = INFINITY;
   const double nfft = (double)p.nfft;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int t = t0 + tf * 4 + i;
-    if (t >= p.T) continue;
+  for (int n = 0; n < 4; ++n)
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const double g = acc[i][c] / nfft;
+    for (int i = 0; i < 4; ++i) {
+      const int t = t0 + 16 * w + kq + 4 * i;
+      if (t >= p.T) continue;
+      const double g = acc[n][i] / nfft;
       const double db = 10.0 * log10(fmax(1e-10, g));   // - 10 log10(max(amin, ref=1)) == 0
-      p.db[(b * 64 + tc * 4 + c) * p.T + t] = db;
+      p.db[(b * 64 + 16 * n + c16) * p.T + t] = db;
       mx = fmax(mx, db);
       mn = fmin(mn, db);
     }
-  }
   // block max / min -> one atomic each per tile (every tile lies in one clip)
   for (int o = 32; o > 0; o >>= 1) {
     mx = fmax(mx, __shfl_xor(mx, o));
     mn = fmin(mn, __shfl_xor(mn, o));
   }
-  if ((tid & 63) == 0) {
-    s_red[0][tid >> 6] = mx;
-    s_red[1][tid >> 6] = mn;
+  if (lane == 0) {
+    s_red[0][w] = mx;
+    s_red[1][w] = mn;
   }
   __syncthreads();
   if (tid == 0) {
@@ -934,7 +1054,7 @@ void launch_gamma(const GammaParams& p, hipStream_t s) {
     launch_gamma_spec<512>(p, s);
   else
     return note_launch_error(hipErrorInvalidValue);
-  hipLaunchKernelGGL(gamma_erb_kernel, dim3((p.T + 63) / 64, p.B), dim3(256), 0, s, p);
+  hipLaunchKernelGGL(gamma_erb_kernel, dim3((p.T + ERB_TF - 1) / ERB_TF, p.B), dim3(256), 0, s, p);
   hipLaunchKernelGGL(gamma_quant_kernel, dim3(2048), dim3(256), 0, s, p);
 }
 

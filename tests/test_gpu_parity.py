@@ -266,6 +266,13 @@ def test_graphed_forward_bit_identical(model):
         out = g(w)
         for k in ('framewise_output', 'clipwise_output'):
             assert torch.equal(out[k], ref[k]), (mt, k)
+    # a pipelined handle waits on an event recorded outside any capture: refused
+    m.set_pipelined(True)
+    try:
+        with pytest.raises(RuntimeError):
+            inference.GraphedForward(m, w0)
+    finally:
+        m.set_pipelined(False)
 
 
 def test_windowed_and_events(model, golden_dir):
