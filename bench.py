@@ -65,8 +65,9 @@ DTYPE = {'exact': 'f32',
          'x3': 'bf16x3-split (3 bf16 MFMAs per f32 MAC: hi*hi + hi*lo + lo*hi, f32 accumulate)'}
 # Winograd F(2x2,3x3): 16 matrix-pipe multiplies per 2x2 output tile where the
 # direct conv does 36 ('winograd' mode: blocks 2-4, and block 1's conv2 unless
-# --wino-block1 0 keeps block 1 as the direct fused launch)
-WINO_BLOCK1 = True
+# --wino-block1 0 keeps block 1 as the direct fused launch; 1 feeds it from a
+# separate conv1 launch, 2 computes conv1 inside the Winograd launch)
+WINO_BLOCK1 = 2
 WINO_MUL = 16.0 / 36.0
 
 
@@ -380,6 +381,8 @@ PROFILE_SUMMARY = os.path.join(REPO, 'profiles', 'r03_kernel_summary.json')
 # block 1's conv1 (Cin 1 -> 64) computed inside the b1c2 launch (winograd
 # mode with the Winograd block 1: its own launch, stage b1c1)
 def fused_block1(precision):
+    # matrix-pipe conv1 inside the b1c2 launch (exact / x3 / --wino-block1 0);
+    # --wino-block1 2 computes it inside too, but on the VALU (not priced here)
     return precision != 'winograd' or not WINO_BLOCK1
 
 
@@ -390,6 +393,8 @@ def conv_kernel_name(stage, precision):
     bn = 64 if cout == 64 else 128
     if precision == 'x3':
         return 'sedx::conv3x3_x3_kernel<%d, %d, %d, %s>' % (F, bn, epi, 'true' if stage == 'b1c2' else 'false')
+    if precision == 'winograd' and stage == 'b1c2' and WINO_BLOCK1 == 2:
+        return 'sedx::wino_block1_kernel<2>'
     if precision == 'winograd' and stage in wino_stages():
         # 4 tile groups (8 waves) at the bench shapes
         return 'sedx::conv3x3_wino_kernel<%d, %d, 4>' % (F, epi)
@@ -601,8 +606,9 @@ def main():
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
     ap.add_argument('--gru-kernel', choices=['coop', 'tag16', 'tag8', 'simple'], default='coop',
                     help='GRU recurrence kernel (SEDX_TUNE_GRU_KERNEL; A/B runs)')
-    ap.add_argument('--wino-block1', type=int, choices=[0, 1], default=1,
-                    help='winograd precision: block 1 as Winograd too (1, default) or direct fused (0)')
+    ap.add_argument('--wino-block1', type=int, choices=[0, 1, 2], default=None,
+                    help='winograd precision: block 1 as Winograd with conv1 inside the launch (2), fed by a '
+                         'separate conv1 launch (1), or as the direct fused kernel (0); default: WINO_BLOCK1')
     args = ap.parse_args()
 
     world, rank, local = distributed.init()
@@ -612,7 +618,8 @@ def main():
     torch.cuda.set_device(dev)
     name = MODEL_NAMES[args.model]
     global WINO_BLOCK1
-    WINO_BLOCK1 = bool(args.wino_block1)
+    if args.wino_block1 is not None:
+        WINO_BLOCK1 = args.wino_block1
     model = build_model(name, dev)
     gk = {'coop': 0, 'simple': 1, 'tag16': 2, 'tag8': 3}[args.gru_kernel]
     if gk:

@@ -217,10 +217,13 @@ sedx_status sedx_set_precision(sedx_handle* h, int32_t mode);
  *                         bit-identical; measured 1.4x slower at B = 32: the
  *                         tile's single MFMA chain and two workgroup barriers
  *                         per 16 frames cost more than the band sums' VALU).
- *  SEDX_TUNE_WINO_BLOCK1  (SEDX_PRECISION_WINOGRAD only) 1 (default): block 1's
- *                         conv2 as Winograd F(2x2,3x3) too, fed by a separate
- *                         conv1 launch (the 64-channel activation goes through
- *                         HBM); 0: block 1 as the direct fused fp32 kernel. */
+ *  SEDX_TUNE_WINO_BLOCK1  (SEDX_PRECISION_WINOGRAD only) 2 (default): block 1
+ *                         as ONE launch — conv1 computed into conv2's halo
+ *                         images in LDS (the 64-channel activation never
+ *                         exists), conv2 as Winograd F(2x2,3x3), pool;
+ *                         1: the same conv2 fed by a separate conv1 launch
+ *                         (the activation through HBM; bit-identical to 2);
+ *                         0: block 1 as the direct fused fp32 kernel. */
 typedef enum {
   SEDX_TUNE_GRU_KERNEL = 0,
   SEDX_TUNE_GRU_HANDOFF = 1,

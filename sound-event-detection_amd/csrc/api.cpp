@@ -90,7 +90,7 @@ struct sedx_handle {
   int precision = SEDX_PRECISION_WINOGRAD;   // GEMM arithmetic (sedx_set_precision; the default is fp32 Winograd)
   int gru_kernel = SEDX_GRU_KERNEL_COOP;   // sedx_set_tuning
   int gru_handoff = SEDX_GRU_HANDOFF_AUTO;
-  int wino_block1 = 1;                     // SEDX_TUNE_WINO_BLOCK1
+  int wino_block1 = 2;                     // SEDX_TUNE_WINO_BLOCK1 (2: conv1 inside the Winograd launch)
   int mel_mfma = 0;                        // SEDX_TUNE_MEL_MFMA (measured slower: opt-in)
   // sedx_set_capture: copy one stage's output of every later forward
   int cap_stage = -1;
@@ -310,7 +310,7 @@ WsLayout ws_layout(const sedx_handle* h, int64_t B, const Geometry& g) {
   // modes: conv1's 64-channel activation never exists), then the conv1
   // outputs of blocks 2-4, then the head scratch
   size_t a = block1_pad_floats((int)B, (int)g.T);
-  if (wino_block1_on(h)) a = std::max(a, (size_t)B * g.T * 64 * 64);   // conv1's activation
+  if (wino_block1_on(h) && h->wino_block1 == 1) a = std::max(a, (size_t)B * g.T * 64 * 64);   // conv1's activation
   a = std::max(a, (size_t)B * g.T1 * 32 * 128);
   a = std::max(a, (size_t)B * g.T2 * 16 * 256);
   a = std::max(a, (size_t)B * g.T3 * 8 * 512);
@@ -368,9 +368,11 @@ sedx_status run_body(sedx_handle* h, int64_t B, const Geometry& g, float* ws, co
   // staging (the b1c1 stage is just the zero-bordered copy of the bn0 output)
   if (x3) HIP_TRY(h, hipMemsetAsync(sched, 0, 7 * CONV_SCHED_INTS * sizeof(int), s));
   const bool wb1 = wino_block1_on(h);
-  if (wb1)   // Winograd block 1: conv1's activation [B][T][64][64] into A
+  // Winograd block 1: 1 = conv1's activation [B][T][64][64] into A by its
+  // own launch; 2 = conv1 inside the Winograd launch (reads X0 itself)
+  if (wb1 && h->wino_block1 == 1)
     launch_conv1_nhwc(X0, iB, (int)g.T, w.c1_w, w.c1_b, A, s);
-  else
+  else if (!wb1)
     launch_pad_x0(X0, iB, (int)g.T, A, s);
   struct L {
     const float* in;
@@ -390,6 +392,8 @@ sedx_status run_body(sedx_handle* h, int64_t B, const Geometry& g, float* ws, co
     if (x3 && i == 0)
       launch_block1_fused_x3(nullptr, iB, c.T, A, w.c1_wt, w.c1_b, w.wx3[c.idx], w.cb[c.idx], c.out,
                              sched, s);
+    else if (i == 0 && wb1 && h->wino_block1 == 2)
+      launch_block1_wino(X0, iB, c.T, w.c1_w, w.c1_b, w.wu[c.idx], w.cb[c.idx], c.out, w.zero, w.trash, s);
     else if (i == 0 && wb1)
       launch_conv3x3_wino(A, iB, c.T, 64, 64, 64, w.wu[c.idx], w.cb[c.idx], c.out, EPI_POOL2, w.zero, w.trash, s);
     else if (i == 0)
@@ -575,7 +579,7 @@ sedx_status sedx_set_tuning(sedx_handle* h, int32_t knob, int32_t value) {
       h->gru_handoff = value;
       return SEDX_OK;
     case SEDX_TUNE_WINO_BLOCK1:
-      if (value != 0 && value != 1) break;
+      if (value != 0 && value != 1 && value != 2) break;
       h->wino_block1 = value;
       return SEDX_OK;
     case SEDX_TUNE_MEL_MFMA:

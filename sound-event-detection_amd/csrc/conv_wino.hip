@@ -48,9 +48,14 @@ namespace sedx {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-template <int F, int TG>
+// TG tile groups x NG channel groups of 32 per workgroup (2 TG NG waves).
+// C1 (block 1, F = 64): the input is the bn0 output X0 [B][T][64] and conv1
+// (Cin 1 -> 64, BN folded, ReLU) is computed into each chunk's halo image in
+// LDS (below): conv1's 64-channel activation never exists in HBM.
+template <int F, int TG, int NG = 1, bool C1 = false>
 struct WinoGeom {
-  static constexpr int WAVES = 2 * TG;
+  static constexpr int NGW = TG * NG;                // waves per position half
+  static constexpr int WAVES = 2 * NGW;
   static constexpr int THREADS = 64 * WAVES;
   static constexpr int P = 32 * TG;                  // tiles per workgroup
   static constexpr int FT = F / 2;                   // tiles per tile row
@@ -58,8 +63,10 @@ struct WinoGeom {
   static constexpr int RT = 2 * TRW + 2, CS = F + 2, KC = 4;
   static constexpr int PL = RT * CS;                 // halo pixels
   static constexpr int PLP = (PL + 63) / 64 * 64;    // whole 64-pixel DMA units
-  static constexpr int A_SZ = KC * PLP;              // floats: [pixel][4 ch]
-  static constexpr int W_SZ = 16 * KC * 32;          // floats: [p][h][n 32][ks]
+  // floats: [pixel][4 ch] (C1: a 64-pixel conv1 group for every wave; the
+  // groups past the halo write zeros into the padding)
+  static constexpr int A_SZ = KC * (C1 && PLP < 128 * TG * NG ? 128 * TG * NG : PLP);
+  static constexpr int W_SZ = 16 * KC * 32 * NG;     // floats: [p][h][n 32 NG][ks]
   static constexpr int BUF = A_SZ + W_SZ;
 #ifndef SEDX_WINO_NBUF
 #define SEDX_WINO_NBUF 3
@@ -70,15 +77,25 @@ struct WinoGeom {
   // ring depth (F = 64: block 1's conv2 streams its 525 MB input from HBM)
   static constexpr int NBUF = TG == 4 ? (F == 64 ? SEDX_WINO_NBUF64 : SEDX_WINO_NBUF) : 3;
   static constexpr int UW = W_SZ / 256;              // 1-KiB DMA units per chunk
-  static constexpr int UA = PLP / 64;
+  static constexpr int UA = C1 ? 0 : PLP / 64;       // halo units (C1 computes the halo instead)
   static constexpr int U = UW + UA;
   static constexpr int UPW = (U + WAVES - 1) / WAVES;
   static constexpr int VM_MIN = U / WAVES;           // units of the wave with the fewest
   static constexpr int XCH = WAVES * 8 * 4 * 64;     // floats: epilogue exchange, [wave][r 8][4][lane]
-  static constexpr int LDS_BYTES = 4 * (NBUF * BUF + XCH);   // ring, then the epilogue exchange
+  // C1: an item's X0 rows t0 - 2 .. t0 + RT - 1 ([row][F], zero rows outside
+  // the clip), two buffers by item parity, in 1-KiB DMA units; the conv1
+  // halo pixels in 64-pixel groups, one group per wave
+  static constexpr int XROWS = RT + 2;
+  static constexpr int UX = C1 ? (XROWS * F + 255) / 256 : 0;
+  static constexpr int X0_SZ = 256 * UX;
+  static constexpr int XA_OFF = NBUF * BUF + XCH;
+  static constexpr int NGRP = C1 ? WAVES : 0;
+  static constexpr int LDS_BYTES = 4 * (NBUF * BUF + XCH + 2 * X0_SZ);   // ring, epilogue exchange, X0 tiles
+  static constexpr int WG_PER_CU = WAVES == 8 || LDS_BYTES > 80 * 1024 ? 1 : 2;
   static_assert(P % FT == 0, "whole tile rows per workgroup");
   static_assert(VM_MIN * (NBUF - 1) <= 63, "vmcnt field");
-  static_assert(LDS_BYTES <= (TG == 4 ? 160 : 80) * 1024, "LDS per workgroup (1 per CU at TG 4, else 2)");
+  static_assert(LDS_BYTES <= 160 * 1024, "LDS per workgroup");
+  static_assert(!C1 || (F == 64 && PLP <= 64 * WAVES && UX <= WAVES && NBUF == 3), "C1: block 1 (64 bins), a conv1 group per wave");
 };
 
 // raw workgroup barrier behind "this wave's DMAs older than its N youngest
@@ -112,13 +129,14 @@ __device__ __forceinline__ void wino_bt4(float* x) {
 
 // the kernel body for position half PH (wave-uniform; a template parameter so
 // the transform, the U rows and the patch offsets are static per wave)
-template <int F, int EPI, int TG, int PH>
+template <int F, int EPI, int TG, int PH, int NG, bool C1>
 __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, int T, int Cin, int Cout,
                                           const float* __restrict__ U, const float* __restrict__ bias,
                                           float* __restrict__ out, const float* __restrict__ zero16,
-                                          float* __restrict__ trash, int tb_per_clip, int ngroups) {
+                                          float* __restrict__ trash, int tb_per_clip, int ngroups,
+                                          const float* __restrict__ w1, const float* __restrict__ b1) {
   constexpr int ph = PH;
-  using G = WinoGeom<F, TG>;
+  using G = WinoGeom<F, TG, NG, C1>;
   constexpr int WAVES = G::WAVES;
   // unit u = wv + WAVES k of this wave: a weight unit, a halo unit, or none.
   // Folded at compile time where k alone decides (UW a multiple of WAVES:
@@ -133,7 +151,10 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int tg = wv % TG;   // tile group (waves tg, tg + TG: position halves 0, 1 — one SIMD)
+  // (tile group, channel group) of the wave: waves q, q + NGW are its
+  // position halves 0, 1 (one SIMD)
+  const int tg = wv % TG;
+  const int cg = NG == 1 ? 0 : (wv % G::NGW) / TG;
   // Persistent: workgroup g takes items g, g + gridDim.x, ... (gridDim.x a
   // multiple of 8, so every item of a workgroup is on its XCD).  XCD-aware
   // item decode: item -> XCD id & 7; on one XCD, tile blocks in order, each
@@ -146,7 +167,7 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
     if (tb >= B * tb_per_clip) return false;
     b_ = tb / tb_per_clip;
     t0_ = 2 * (tb - b_ * tb_per_clip) * G::TRW;   // first row (2 x first tile row)
-    n0_ = (j - jb * ngroups) * 32;
+    n0_ = (j - jb * ngroups) * 32 * NG;
     return true;
   };
   // this workgroup's 128 trash floats (spread: the dummy and out-of-range
@@ -167,9 +188,9 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
   const int pt = 32 * tg + (lane & 31);
   const int a_base = ((pt / FT) * HC + (pt % FT)) * KC + 2 * khalf;
   auto a_off = [&](int i, int jj) { return ((((i & 1) << 1) | (jj & 1)) * Q + (i >> 1) * HC + (jj >> 1)) * KC; };
-  // B side: U slab [p][h][n][ks], lane (h = khalf, n = lane & 31), this
-  // wave's positions 8 ph .. 8 ph + 7
-  const int b_base = G::A_SZ + 8 * ph * 128 + khalf * 64 + 2 * (lane & 31);
+  // B side: U slab [p][h][n][ks], lane (h = khalf, n = 32 cg + (lane & 31)),
+  // this wave's positions 8 ph .. 8 ph + 7 (rows of 64 NG floats)
+  const int b_base = G::A_SZ + 8 * ph * 128 * NG + khalf * 64 * NG + 64 * cg + 2 * (lane & 31);
 
   // ---- LDS-DMA units of this wave (unit u -> wave u % WAVES): LDS offsets
   // fixed, sources per item ----
@@ -188,8 +209,9 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
       const int u = wv + WAVES * k;
       off[k] = -1;
       if (is_w(k)) {
-        const int row = 4 * u + (lane >> 4);   // (p, h) row of 2 x 32 floats
-        off[k] = row * 2 * Cout + 4 * (lane & 15);
+        constexpr int LPR = 16 * NG;   // lanes per (p, h) row of 2 x 32 NG floats
+        const int row = (64 / LPR) * u + lane / LPR;
+        off[k] = row * 2 * Cout + 4 * (lane % LPR);
       } else if (present(k, wv)) {
         const int slot = 64 * (u - G::UW) + lane;
         const int q = slot / Q, rem = slot - q * Q;
@@ -240,6 +262,82 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
     ptrs(doff, n0);
   }
 
+  // ---- C1: conv1 into the halo images.  Wave wv < NGRP owns halo slots
+  // 64 wv + lane (one pixel per lane, the parity-plane slot order of the
+  // halo DMA).  Per item its 3x3 X0 window sits in 9 registers, read from the
+  // item's X0 tile in LDS (LDS-DMA'd with the previous item's last chunk, or
+  // in the prologue); per chunk it computes its pixel's 4 channels of the
+  // chunk c + 2 (two ahead: chunk c + 1 is read during chunk c) into that
+  // chunk's ring buffer, one 16-byte LDS write.  Per channel the 9 taps are
+  // one fma chain in tap order from 0, then + bias and ReLU — the operation
+  // order of conv1_nhwc_kernel (and of the direct kernel's fused conv1), so
+  // the outputs are bit-identical to the unfused Winograd block 1.  conv2's
+  // zero padding: halo pixels outside the clip store 0. ----
+  [[maybe_unused]] float xw[C1 ? 9 : 1];
+  [[maybe_unused]] bool c1_ov = false;
+  [[maybe_unused]] const int pslot = 64 * wv + lane;
+  [[maybe_unused]] int pr = 0, pc = 0;
+  if constexpr (C1) {
+    const int sl = pslot < G::PL ? pslot : 0;
+    const int q = sl / Q, rem = sl - q * Q;
+    pr = 2 * (rem / HC) + (q >> 1);
+    pc = 2 * (rem % HC) + (q & 1);
+  }
+  // X0 rows t0_ - 2 + xr of clip b_ -> X0 tile xb (unit x: wave x; 16 lanes a row)
+  [[maybe_unused]] auto x0_dma = [&](int b_, int t0_, int xb) {
+    if (wv < G::UX) {   // wave-uniform
+      const int xr = 4 * wv + (lane >> 4);
+      const int t = t0_ - 2 + xr;
+      const float* src = (xr < G::XROWS && t >= 0 && t < T) ? in + ((b_ * T + t) * F + 4 * (lane & 15)) : zero16;
+      const uint32_t m0_ =
+          (uint32_t)(size_t)(__attribute__((address_space(3))) float*)(smem + G::XA_OFF + xb * G::X0_SZ + 256 * wv);
+      sedx_glds16(src, __builtin_amdgcn_readfirstlane(m0_));
+    }
+    asm volatile("" ::: "memory");
+  };
+  // the lane's window from X0 tile xb (columns outside the bins read as 0;
+  // rows outside the clip are zero rows of the tile) and its pixel's validity
+  [[maybe_unused]] auto load_window = [&](int t0_, int xb) {
+    {
+      const float* xa = smem + G::XA_OFF + xb * G::X0_SZ;
+#pragma unroll
+      for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx) {
+          const int col = pc - 2 + dx;
+          const float v = xa[(pr + dy) * F + min(max(col, 0), F - 1)];
+          xw[dy * 3 + dx] = (col >= 0 && col < F) ? v : 0.0f;
+        }
+      const int t = t0_ - 1 + pr;
+      c1_ov = pslot < G::PL && t >= 0 && t < T && pc >= 1 && pc <= F;
+    }
+  };
+  // channels 4 cc .. 4 cc + 3 of the lane's pixel -> ring buffer cb
+  // (the chunk's 36 weights + 4 biases are wave-uniform: scalar loads)
+  [[maybe_unused]] auto c1_weights = [&](int cc, float (&wq)[40]) {
+#pragma unroll
+    for (int i = 0; i < 36; ++i) wq[i] = w1[36 * cc + i];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) wq[36 + i] = b1[4 * cc + i];
+  };
+  [[maybe_unused]] auto conv1w = [&](const float (&wq)[40], int cb) {
+    float y[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float a = 0.0f;
+#pragma unroll
+      for (int k = 0; k < 9; ++k) a = fmaf(xw[k], wq[9 * i + k], a);
+      const float v = fmaxf(a + wq[36 + i], 0.0f);
+      y[i] = c1_ov ? v : 0.0f;
+    }
+    *reinterpret_cast<float4*>(smem + cb * G::BUF + 4 * pslot) = make_float4(y[0], y[1], y[2], y[3]);
+  };
+  [[maybe_unused]] auto conv1 = [&](int cc, int cb) {
+    float wq[40];
+    c1_weights(cc, wq);
+    conv1w(wq, cb);
+  };
+
   f32x16 acc[8];
 #pragma unroll
   for (int p = 0; p < 8; ++p)
@@ -259,7 +357,7 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
       for (int jj = 0; jj < 4; ++jj)
         pd[i][jj] = *reinterpret_cast<const float2*>(sm + a_base + a_off(ph + i, jj));
 #pragma unroll
-    for (int p = 0; p < 8; ++p) un[p] = *reinterpret_cast<const float2*>(sm + b_base + p * 128);
+    for (int p = 0; p < 8; ++p) un[p] = *reinterpret_cast<const float2*>(sm + b_base + p * 128 * NG);
   };
   // V rows 2 ph, 2 ph + 1 of B^T d B from patch rows ph .. ph + 2
   //   ph 0: d0 - d2, d1 + d2      ph 1: d2 - d1, d1 - d3
@@ -296,7 +394,15 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
   // k-step 1 (2 khalf + 1) — with the next chunk's LDS reads spread over the
   // first 8 and its transform over the last 8.  (Keeping the two k-steps of
   // an accumulator apart with a scheduling barrier measured 6 % slower.)
-  auto step = [&](const float (&vc)[2][8], const float2 (&uc)[8], int nbuf, float (&vn)[2][8], float2 (&un)[8]) {
+  // C1: then conv1 of channel chunk cc into ring buffer cb (cc < 0: none)
+  auto step = [&](const float (&vc)[2][8], const float2 (&uc)[8], int nbuf, float (&vn)[2][8], float2 (&un)[8],
+                  int cc = -1, int cb = 0) {
+#ifdef SEDX_C1_PRELOAD
+    // the weights' scalar loads issued at the top of the step (their wait
+    // then falls on the transform's)
+    [[maybe_unused]] float wq[C1 ? 40 : 1];
+    if constexpr (C1) c1_weights(cc, wq);
+#endif
 #pragma unroll
     for (int p = 0; p < 8; ++p) acc[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(vc[0][p], uc[p].x, acc[p], 0, 0, 0);
 #pragma unroll
@@ -304,15 +410,28 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
     float2 pd[3][4];
     issue_reads(nbuf, pd, un);
     transform(pd, vn);
+#ifdef SEDX_C1_PRELOAD
+    if constexpr (C1) conv1w(wq, cb);
+#else
+    if constexpr (C1) conv1(cc, cb);
+#endif
+#ifdef SEDX_WINO_READS_FIRST
+    // every LDS read of the next chunk ahead of the MFMAs (~1000 cycles of
+    // the SIMD's matrix work before the transform consumes them)
+    __builtin_amdgcn_sched_group_barrier(0x100, 20, 0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+#else
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
       __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // 2 LDS reads
     }
+#endif
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
-      __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);   // 5 VALU
+      __builtin_amdgcn_sched_group_barrier(0x002, C1 ? 11 : 5, 0);   // 5 VALU (C1: + conv1's)
     }
   };
 
@@ -321,6 +440,9 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
   // epilogue stores per wave (all issued: out-of-range ones go to trash)
   constexpr int S = EPI == EPI_FMEAN ? 4 : EPI == EPI_POOL2 ? 8 : 32;
   static_assert(G::VM_MIN * (NB - 2) + S <= 63, "vmcnt field");
+  static_assert(!C1 || G::VM_MIN * NB + S <= 63, "vmcnt field");
+  int xpar = 0;   // C1: the current item's X0 tile
+  if constexpr (C1) x0_dma(b, t0, 0);
 #pragma unroll
   for (int c = 0; c < NB; ++c) dma_cur(c, c);   // nchunks >= 8 (launcher)
   // S stores to trash: every item, the first included, then has S stores
@@ -331,6 +453,14 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
     const float zf = 0.0f;
 #pragma unroll
     for (int i = 0; i < S; ++i) asm volatile("global_store_dword %0, %1, off" ::"v"(vt), "v"(zf) : "memory");
+  }
+  if constexpr (C1) {
+    // the first item's X0 tile landed (the NB chunks' DMAs and the S stores
+    // may be in flight): its window, then conv1 of chunks 0 and 1
+    wino_bar_n<G::VM_MIN * NB + S>();
+    load_window(t0, 0);
+    conv1(0, 0);
+    conv1(1, 1);
   }
   // chunk 0 landed: younger chunks 1 .. NB - 1 and the S stores may be in flight
   wino_bar<G::VM_MIN, NB - 1, S>(NB - 1);
@@ -364,7 +494,7 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
     }
   };
   float* const xo = smem + NB * G::BUF + wv * (8 * 4 * 64);                    // this wave's slots [r 8][4][lane]
-  const float* const xi = smem + NB * G::BUF + (tg + TG * (1 - ph)) * (8 * 4 * 64);   // the partner's
+  const float* const xi = smem + NB * G::BUF + (wv % G::NGW + G::NGW * (1 - ph)) * (8 * 4 * 64);   // the partner's
 
   // top of chunk c: chunk c + 1 landed (c + 2 .. c + NB - 1 of the item
   // sequence may be in flight) and every wave has consumed chunk c's buffer
@@ -376,7 +506,7 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
     const int nitem = item + (int)gridDim.x;
     int nb_ = 0, nt0 = 0, nn0 = 0;
     const bool has_next = decode(nitem, nb_, nt0, nn0);
-    const float bv = bias[n0 + (lane & 31)];   // loaded early: its wait must not drain the DMAs
+    const float bv = bias[n0 + 32 * cg + (lane & 31)];   // loaded early: its wait must not drain the DMAs
     {   // the item's chunk 0 (landed: the previous barrier waited for it)
       float2 pd[3][4];
       issue_reads(buf, pd, ua);
@@ -405,14 +535,21 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
       const int b1 = buf == NB - 1 ? 0 : buf + 1, b2 = b1 == NB - 1 ? 0 : b1 + 1;
       // chunks 1 and 2 of an item: the S stores (previous epilogue, or the
       // prologue's) were issued after their DMAs
+      // C1: conv1 runs two chunks ahead — chunk + 2 into b2, chunk + 3 into
+      // buf; over the last pair those are the next item's chunks 0 and 1,
+      // from its window (its X0 tile was DMA'd with chunk nchunks - 1)
       if constexpr (MID) {
         wino_bar_n<G::VM_MIN * (NB - 2) + (FIRST ? S : 0)>();
         dma_cur(chunk + NB, buf);
       } else {
         wino_bar<G::VM_MIN, NB - 2, FIRST ? S : 0>(has_next ? NB - 2 : max(0, min(NB - 2, nchunks - chunk - 2)));
         issue(chunk + NB, buf);
+        // (without a next item: the current item's tile again, unused — the
+        // pipeline stays branch-free; so are the window and conv1 below)
+        if constexpr (C1 && !LAST) x0_dma(has_next ? nb_ : b, has_next ? nt0 : t0, xpar ^ 1);
       }
-      step(va, ua, b1, vb, ubv);
+      if constexpr (C1 && LAST) load_window(has_next ? nt0 : t0, xpar ^ 1);
+      step(va, ua, b1, vb, ubv, C1 ? (LAST ? 0 : chunk + 2) : -1, b2);
       if constexpr (MID) {
         wino_bar_n<G::VM_MIN * (NB - 2) + (FIRST ? S : 0)>();
         dma_cur(chunk + 1 + NB, b1);
@@ -421,12 +558,13 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
         issue(chunk + 1 + NB, b1);
       }
       if constexpr (!LAST) {
-        step(vb, ubv, b2, va, ua);
+        step(vb, ubv, b2, va, ua, C1 ? chunk + 3 : -1, buf);
       } else {
 #pragma unroll
         for (int p = 0; p < 8; ++p) acc[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(vb[0][p], ubv[p].x, acc[p], 0, 0, 0);
 #pragma unroll
         for (int p = 0; p < 8; ++p) acc[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(vb[1][p], ubv[p].y, acc[p], 0, 0, 0);
+        if constexpr (C1) conv1(1, buf);
       }
       buf = b2;
     };
@@ -449,7 +587,7 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
     }
     // LDS-only barrier (__syncthreads() would drain the next item's DMAs)
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    const int n = n0 + (lane & 31);
+    const int n = n0 + 32 * cg + (lane & 31);
     // full Y of register 8 ph + k (+ bias, ReLU), as y[a][b]
     auto outtile = [&](int k, float y[2][2]) {
       float mine[4];
@@ -513,6 +651,7 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
     // the partner's reads of this item's exchange slots finish before the
     // next item's epilogue overwrites them: many barriers lie between
     item = nitem;
+    xpar ^= 1;
     b = nb_;
     t0 = nt0;
     n0 = nn0;
@@ -530,9 +669,25 @@ __global__ __launch_bounds__(128 * TG, TG == 4 ? 1 : 2) void conv3x3_wino_kernel
     const float* __restrict__ bias, float* __restrict__ out, const float* __restrict__ zero16,
     float* __restrict__ trash, int tb_per_clip, int ngroups) {
   if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) < TG)
-    wino_body<F, EPI, TG, 0>(in, B, T, Cin, Cout, U, bias, out, zero16, trash, tb_per_clip, ngroups);
+    wino_body<F, EPI, TG, 0, 1, false>(in, B, T, Cin, Cout, U, bias, out, zero16, trash, tb_per_clip, ngroups,
+                                       nullptr, nullptr);
   else
-    wino_body<F, EPI, TG, 1>(in, B, T, Cin, Cout, U, bias, out, zero16, trash, tb_per_clip, ngroups);
+    wino_body<F, EPI, TG, 1, 1, false>(in, B, T, Cin, Cout, U, bias, out, zero16, trash, tb_per_clip, ngroups,
+                                       nullptr, nullptr);
+}
+
+// Block 1 in one launch: conv1 (computed into the halo images) + Winograd
+// conv2 + 2x2 pool, TG tile groups x both 32-channel groups per workgroup
+// (the conv1 halo serves all 64 output channels)
+template <int TG>
+__global__ __launch_bounds__(256 * TG, (WinoGeom<64, TG, 2, true>::WG_PER_CU)) void wino_block1_kernel(
+    const float* __restrict__ x0, int B, int T, const float* __restrict__ U, const float* __restrict__ bias,
+    float* __restrict__ out, const float* __restrict__ zero16, float* __restrict__ trash, int tb_per_clip,
+    const float* __restrict__ w1, const float* __restrict__ b1) {
+  if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) < 2 * TG)
+    wino_body<64, EPI_POOL2, TG, 0, 2, true>(x0, B, T, 64, 64, U, bias, out, zero16, trash, tb_per_clip, 1, w1, b1);
+  else
+    wino_body<64, EPI_POOL2, TG, 1, 2, true>(x0, B, T, 64, 64, U, bias, out, zero16, trash, tb_per_clip, 1, w1, b1);
 }
 
 static int wino_device_cus() {
@@ -629,6 +784,39 @@ void launch_conv3x3_wino(const float* in, int B, int T, int F, int Cin, int Cout
       case 8: launch_wino_f<8>(in_s, bs, T, Cin, Cout, U, bias, out_s, epi, zero16, trash, s); break;
       default: return note_launch_error(hipErrorInvalidValue);
     }
+  }
+}
+
+template <int TG>
+static void launch_block1_w(const float* x0, int B, int T, const float* U, const float* bias, float* out,
+                            const float* w1, const float* b1, const float* zero16, float* trash, hipStream_t s) {
+  using G = WinoGeom<64, TG, 2, true>;
+  const int tb_per_clip = (T / 2 + G::TRW - 1) / G::TRW;   // pooled: an odd last t-row is dropped
+  const int64_t tblocks = (int64_t)B * tb_per_clip;
+  const int64_t nitems = (tblocks + 7) / 8 * 8;           // one channel group (64 channels) per item
+  if (nitems > INT32_MAX || tblocks <= 0 || (int64_t)B * T * 64 >= INT32_MAX) return note_launch_error(hipErrorInvalidValue);
+  const int64_t resident = (int64_t)wino_device_cus() * G::WG_PER_CU / 8 * 8;
+  const int64_t per = (nitems + WINO_ITEMS - 1) / WINO_ITEMS;
+  const int64_t nwg = std::min<int64_t>(nitems, std::max<int64_t>(std::max<int64_t>(8, resident), (per + 7) / 8 * 8));
+  auto* k_ = wino_block1_kernel<TG>;
+  if (!launch_info(reinterpret_cast<const void*>(k_), G::THREADS, G::LDS_BYTES).ok) return;
+  hipLaunchKernelGGL(k_, dim3((unsigned)nwg), dim3(G::THREADS), G::LDS_BYTES, s, x0, B, T, U, bias, out, zero16, trash,
+                     tb_per_clip, w1, b1);
+}
+
+void launch_block1_wino(const float* x0, int B, int T, const float* w1, const float* b1, const float* U,
+                        const float* bias, float* out, const float* zero16, float* trash, hipStream_t s) {
+  if (B <= 0 || T < 2) return note_launch_error(hipErrorInvalidValue);
+  // 32-bit X0 offsets: batches past 2^31 floats run as several launches over
+  // whole clips (same per-clip work)
+  const int64_t in_clip = (int64_t)T * 64, out_clip = (int64_t)(T / 2) * 32 * 64;
+  const int64_t bmax = (INT32_MAX - 1) / in_clip;
+  for (int64_t b0 = 0; b0 < B; b0 += bmax) {
+    const int bs = (int)std::min<int64_t>(bmax, B - b0);
+    // 2 tile groups x 2 channel groups (64 tiles x 64 channels, 8 waves)
+    // at every batch size (with 1 tile group the 4 waves would not cover
+    // the halo's conv1 pixel groups)
+    launch_block1_w<2>(x0 + b0 * in_clip, bs, T, U, bias, out + b0 * out_clip, w1, b1, zero16, trash, s);
   }
 }
 

@@ -120,6 +120,12 @@ void launch_conv3x3_wino(const float* in, int B, int T, int F, int Cin, int Cout
                          const float* U, const float* bias, float* out, int epi,
                          const float* zero16, float* trash, hipStream_t s);
 void pack_conv_wino(const double* wf, int Cin, int Cout, float* U);   // U: Cin * Cout * 16 floats
+// block 1 as one Winograd launch: conv1 (w1 [64][9] folded, b1 [64], ReLU)
+// computed into conv2's halo images in LDS, conv2 (U of block 1's conv2) +
+// bias + ReLU + 2x2 pool: X0 [B][T][64] -> [B][T/2][32][64]; bit-identical to
+// launch_conv1_nhwc followed by launch_conv3x3_wino
+void launch_block1_wino(const float* x0, int B, int T, const float* w1, const float* b1, const float* U,
+                        const float* bias, float* out, const float* zero16, float* trash, hipStream_t s);
 // block 1's conv1 + BN + ReLU: X0 [B][T][64] -> [B][T][64][64] (w1 [64][9] folded, b1 [64])
 void launch_conv1_nhwc(const float* x0, int B, int T, const float* w1, const float* b1, float* out,
                        hipStream_t s);

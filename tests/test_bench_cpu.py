@@ -62,22 +62,27 @@ def test_cpu_info(bench):
 
 def test_roofline_winograd_block1(bench):
     """Winograd mode: b1c2 is a Winograd launch (executed FLOPs 16/36 of the
-    direct conv2, conv1 in its own b1c1 launch); with --wino-block1 0 it is
-    the direct fused launch again."""
+    direct conv2) — by default with conv1 computed inside it on the VALU
+    (--wino-block1 2: not priced on the matrix pipe), or fed by its own b1c1
+    launch (1); with --wino-block1 0 it is the direct fused launch again."""
     stage = {s: 0.2 for s in bench.CONV_STAGES}
     stage['b1c2'] = 1.0
     stage['b1c1'] = 0.1
-    assert bench.WINO_BLOCK1
+    assert bench.WINO_BLOCK1 == 2
     w = bench.roofline(stage, 32, 'winograd')
-    assert w['kernel'] == 'sedx::conv3x3_wino_kernel<64, 1, 4> (b1c2)'
+    assert w['kernel'] == 'sedx::wino_block1_kernel<2> (b1c2)'
     assert w['flops_per_launch'] == bench.conv_flops('b1c2', 32, 1001) * 16.0 / 36.0
     try:
-        bench.WINO_BLOCK1 = False
+        bench.WINO_BLOCK1 = 1
+        w = bench.roofline(stage, 32, 'winograd')
+        assert w['kernel'] == 'sedx::conv3x3_wino_kernel<64, 1, 4> (b1c2)'
+        assert w['flops_per_launch'] == bench.conv_flops('b1c2', 32, 1001) * 16.0 / 36.0
+        bench.WINO_BLOCK1 = 0
         d = bench.roofline(stage, 32, 'winograd')
         assert d['kernel'].startswith('sedx::conv3x3_kernel<64, 64, 1, true')
         assert d['flops_per_launch'] == bench.conv_flops('b1c2', 32, 1001) + 2.0 * 32 * 1001 * 64 * 64 * 9
     finally:
-        bench.WINO_BLOCK1 = True
+        bench.WINO_BLOCK1 = 2
 
 
 def test_roofline_fracs_are_fractions(bench):

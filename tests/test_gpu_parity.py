@@ -579,10 +579,11 @@ def test_config5_transformer_b256():
         assert e <= TOL
 
 
-@pytest.mark.parametrize('wino_block1', [0, 1])
+@pytest.mark.parametrize('wino_block1', [0, 1, 2])
 def test_winograd_block1_knob(wino_block1):
-    """SEDX_TUNE_WINO_BLOCK1: block 1 as the Winograd F = 64 launch fed by the
-    separate conv1 launch (1, the default) or as the direct fused kernel (0);
+    """SEDX_TUNE_WINO_BLOCK1: block 1 as the Winograd F = 64 launch with conv1
+    computed inside it (2), fed by a separate conv1 launch (1), or as the
+    direct fused kernel (0);
     both within the Winograd bar of the oracle at the headline batch, with
     identical thresholded events, and an odd-length clip (partial last tile
     row, pooled rows dropped by floor) as close."""
@@ -609,8 +610,29 @@ def test_wino_block1_knob_errors():
     m = build(GRU)
     nat = m.native(torch.device('cuda', 0))
     L = _lib.lib()
-    assert L.sedx_set_tuning(nat.h, _lib.TUNE_WINO_BLOCK1, 2) != 0
+    assert L.sedx_set_tuning(nat.h, _lib.TUNE_WINO_BLOCK1, 3) != 0
+    assert L.sedx_set_tuning(nat.h, _lib.TUNE_WINO_BLOCK1, -1) != 0
     assert L.sedx_set_tuning(nat.h, _lib.TUNE_WINO_BLOCK1, 1) == 0
+
+
+@pytest.mark.parametrize('B,seconds', [(32, 10.0), (3, 7.33), (1, 2.0), (5, 0.33)])
+def test_wino_block1_conv1_fused_bit_identical(B, seconds):
+    """Block 1 with conv1 computed inside the Winograd launch (2) against the
+    separate conv1 launch (1): the same fma chain per channel, the same
+    conv2 — every block-1 output and the framewise output bit for bit equal,
+    at the headline batch, an odd length (partial last tile block, odd last
+    row dropped by the pool), one short clip and clips of a few frames."""
+    from sedx import _lib
+    wave = synth.make_waveforms(B, seconds=seconds, sample_rate=16000, seed=31 + B)
+    T = wave.shape[1] // 160 + 1                  # frames (hop 160, centred STFT)
+    outs = []
+    for v in (1, 2):
+        m = build(GRU).set_precision('winograd').set_tuning(_lib.TUNE_WINO_BLOCK1, v)
+        b1 = _capture(m, 2, (B, T // 2, 32, 64), wave)
+        assert not np.isnan(b1).any()
+        outs.append((b1, run(m, wave)['framewise_output']))
+    assert np.array_equal(outs[0][0], outs[1][0]), 'block 1 outputs differ'
+    assert np.array_equal(outs[0][1], outs[1][1]), 'framewise outputs differ'
 
 
 def test_winograd_batch_past_32bit_offsets():
