@@ -313,7 +313,8 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
     }
   };
   // channels 4 cc .. 4 cc + 3 of the lane's pixel -> ring buffer cb
-  // (the chunk's 36 weights + 4 biases are wave-uniform: scalar loads)
+  // (the chunk's 36 weights + 4 biases are wave-uniform: scalar loads; issued
+  // at the top of the chunk instead, the launch measured 2 % slower)
   [[maybe_unused]] auto c1_weights = [&](int cc, float (&wq)[40]) {
 #pragma unroll
     for (int i = 0; i < 36; ++i) wq[i] = w1[36 * cc + i];
@@ -397,12 +398,6 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
   // C1: then conv1 of channel chunk cc into ring buffer cb (cc < 0: none)
   auto step = [&](const float (&vc)[2][8], const float2 (&uc)[8], int nbuf, float (&vn)[2][8], float2 (&un)[8],
                   int cc = -1, int cb = 0) {
-#ifdef SEDX_C1_PRELOAD
-    // the weights' scalar loads issued at the top of the step (their wait
-    // then falls on the transform's)
-    [[maybe_unused]] float wq[C1 ? 40 : 1];
-    if constexpr (C1) c1_weights(cc, wq);
-#endif
 #pragma unroll
     for (int p = 0; p < 8; ++p) acc[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(vc[0][p], uc[p].x, acc[p], 0, 0, 0);
 #pragma unroll
@@ -410,11 +405,7 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
     float2 pd[3][4];
     issue_reads(nbuf, pd, un);
     transform(pd, vn);
-#ifdef SEDX_C1_PRELOAD
-    if constexpr (C1) conv1w(wq, cb);
-#else
     if constexpr (C1) conv1(cc, cb);
-#endif
 #ifdef SEDX_WINO_READS_FIRST
     // every LDS read of the next chunk ahead of the MFMAs (~1000 cycles of
     // the SIMD's matrix work before the transform consumes them)

@@ -1,6 +1,6 @@
-"""Host-side cost of one B=1 forward: time to return from model(w) (launches
+"""Host-side cost of one forward: time to return from model(w) (launches
 issued) vs to completion, and the C ABI call alone (sedx_forward via ctypes).
-    python tools/host_overhead.py"""
+    python tools/host_overhead.py [batch]   (default 1 clip of 10 s)"""
 import os
 import sys
 import time
@@ -12,7 +12,8 @@ import torch  # noqa: E402
 from sedx import synth  # noqa: E402
 
 dev = torch.device('cuda:0')
-w = torch.from_numpy(synth.make_waveforms(1, seconds=10.0, sample_rate=16000, seed=11)).to(dev)
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 1
+w = torch.from_numpy(synth.make_waveforms(B, seconds=10.0, sample_rate=16000, seed=11)).to(dev)
 m = bench.build_model('Cnn_9layers_Gru_FrameAtt', dev)
 with torch.no_grad():
     for _ in range(10):
