@@ -90,7 +90,11 @@ struct WinoGeom {
   static constexpr int X0_SZ = 256 * UX;
   static constexpr int XA_OFF = NBUF * BUF + XCH;
   static constexpr int NGRP = C1 ? WAVES : 0;
-  static constexpr int LDS_BYTES = 4 * (NBUF * BUF + XCH + 2 * X0_SZ);   // ring, epilogue exchange, X0 tiles
+  // the layer's biases (Cout <= 512), LDS-DMA'd once in the prologue: read
+  // from LDS, the epilogue's bias needs no vmcnt wait (which would also wait
+  // for the next item's DMAs in flight)
+  static constexpr int BIAS_OFF = XA_OFF + 2 * X0_SZ, BIAS_MAX = 512;
+  static constexpr int LDS_BYTES = 4 * (BIAS_OFF + BIAS_MAX);   // ring, epilogue exchange, X0 tiles, biases
   static constexpr int WG_PER_CU = WAVES == 8 || LDS_BYTES > 80 * 1024 ? 1 : 2;
   static_assert(P % FT == 0, "whole tile rows per workgroup");
   static_assert(VM_MIN * (NBUF - 1) <= 63, "vmcnt field");
@@ -433,6 +437,15 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
   static_assert(G::VM_MIN * (NB - 2) + S <= 63, "vmcnt field");
   static_assert(!C1 || G::VM_MIN * NB + S <= 63, "vmcnt field");
   int xpar = 0;   // C1: the current item's X0 tile
+  // the biases (oldest DMA of the prologue: covered by its first wait); unit
+  // u = wave u, lanes past Cout read the zero block
+  if (wv < G::BIAS_MAX / 256) {   // wave-uniform
+    const int i = 256 * wv + 4 * lane;
+    const uint32_t m0_ =
+        (uint32_t)(size_t)(__attribute__((address_space(3))) float*)(smem + G::BIAS_OFF + 256 * wv);
+    sedx_glds16(i < Cout ? bias + i : zero16, __builtin_amdgcn_readfirstlane(m0_));
+    asm volatile("" ::: "memory");
+  }
   if constexpr (C1) x0_dma(b, t0, 0);
 #pragma unroll
   for (int c = 0; c < NB; ++c) dma_cur(c, c);   // nchunks >= 8 (launcher)
@@ -497,7 +510,6 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
     const int nitem = item + (int)gridDim.x;
     int nb_ = 0, nt0 = 0, nn0 = 0;
     const bool has_next = decode(nitem, nb_, nt0, nn0);
-    const float bv = bias[n0 + 32 * cg + (lane & 31)];   // loaded early: its wait must not drain the DMAs
     {   // the item's chunk 0 (landed: the previous barrier waited for it)
       float2 pd[3][4];
       issue_reads(buf, pd, ua);
@@ -569,6 +581,11 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
 
     // ---- epilogue ----
     const int tr0 = t0 / 2;
+    // the item's first output row as a 64-bit base; every store adds a
+    // 32-bit offset within the item (no per-store 64-bit index math)
+    float* const ob = EPI == EPI_FMEAN ? out + ((int64_t)b * T + t0) * Cout
+                      : EPI == EPI_POOL2 ? out + ((int64_t)b * (T / 2) + tr0) * (F / 2) * Cout
+                                         : out + ((int64_t)b * T + t0) * F * Cout;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       float y[4];
@@ -578,7 +595,13 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
     }
     // LDS-only barrier (__syncthreads() would drain the next item's DMAs)
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    const int n = n0 + 32 * cg + (lane & 31);
+    // an opaque copy of the lane index: the store offsets below are computed
+    // here instead of being hoisted out of the item loop as live registers
+    int le = lane;
+    asm volatile("" : "+v"(le));
+    const int khe = le >> 5;
+    const int n = n0 + 32 * cg + (le & 31);
+    const float bv = smem[G::BIAS_OFF + n];
     // full Y of register 8 ph + k (+ bias, ReLU), as y[a][b]
     auto outtile = [&](int k, float y[2][2]) {
       float mine[4];
@@ -600,14 +623,14 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
         float y[4][2][2];
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) outtile(4 * qq + jj, y[jj]);
-        const int trl = 8 * tg + 2 * q + khalf;
+        const int trl = 8 * tg + 2 * q + khe;
 #pragma unroll
         for (int a = 0; a < 2; ++a) {
           float sum = 0.0f;
 #pragma unroll
           for (int jj = 0; jj < 4; ++jj) sum = (sum + y[jj][a][0]) + y[jj][a][1];
           const int t = t0 + 2 * trl + a;
-          float* dst = t < T ? out + ((int64_t)b * T + t) * Cout + n : tr_lane;
+          float* dst = t < T ? ob + (2 * trl + a) * Cout + n : tr_lane;
           *dst = sum * (1.0f / F);
         }
       }
@@ -615,7 +638,7 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const int r = 8 * ph + k;
-        const int m = (r & 3) + 8 * (r >> 2) + 4 * khalf;
+        const int m = (r & 3) + 8 * (r >> 2) + 4 * khe;
         const int ptile = 32 * tg + m;
         const int trl = ptile / FT, tf = ptile % FT;
         float y[2][2];
@@ -624,13 +647,13 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
           const int To = T / 2;
           const int to = tr0 + trl;
           const float pv = (((y[0][0] + y[0][1]) + y[1][0]) + y[1][1]) * 0.25f;
-          float* dst = to < To ? out + (((int64_t)b * To + to) * (F / 2) + tf) * Cout + n : tr_lane;
+          float* dst = to < To ? ob + (trl * (F / 2) + tf) * Cout + n : tr_lane;
           *dst = pv;
         } else {
 #pragma unroll
           for (int a = 0; a < 2; ++a) {
             const int t = t0 + 2 * trl + a;
-            float* o = t < T ? out + (((int64_t)b * T + t) * F + 2 * tf) * Cout + n : tr_lane;
+            float* o = t < T ? ob + ((2 * trl + a) * F + 2 * tf) * Cout + n : tr_lane;
             const int64_t o1 = t < T ? Cout : 64;
             o[0] = y[a][0];
             o[o1] = y[a][1];
