@@ -604,7 +604,7 @@ def main():
                     help='headline only (no x3 / config 3 / config 4 / window legs, no latency_b1): '
                          'profiling passes use it so per-kernel rocprof averages cover only the headline')
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
-    ap.add_argument('--gru-kernel', choices=['coop', 'tag16', 'tag8', 'simple'], default='coop',
+    ap.add_argument('--gru-kernel', choices=['coop', 'tag16', 'tag8', 'simple', 'coop16'], default='coop',
                     help='GRU recurrence kernel (SEDX_TUNE_GRU_KERNEL; A/B runs)')
     ap.add_argument('--wino-block1', type=int, choices=[0, 1, 2], default=None,
                     help='winograd precision: block 1 as Winograd with conv1 inside the launch (2), fed by a '
@@ -621,7 +621,7 @@ def main():
     if args.wino_block1 is not None:
         WINO_BLOCK1 = args.wino_block1
     model = build_model(name, dev)
-    gk = {'coop': 0, 'simple': 1, 'tag16': 2, 'tag8': 3}[args.gru_kernel]
+    gk = {'coop': 0, 'simple': 1, 'tag16': 2, 'tag8': 3, 'coop16': 4}[args.gru_kernel]
     if gk:
         model.set_tuning(_lib.TUNE_GRU_KERNEL, gk)
     B = args.batch

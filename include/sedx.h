@@ -194,7 +194,12 @@ sedx_status sedx_set_precision(sedx_handle* h, int32_t mode);
 
 /* Implementation choices that leave the arithmetic's meaning unchanged (A/B
  * measurement and tests; the defaults are the fastest measured):
- *  SEDX_TUNE_GRU_KERNEL   SEDX_GRU_KERNEL_COOP (default): the cooperative
+ *  SEDX_TUNE_GRU_KERNEL   SEDX_GRU_KERNEL_AUTO (default): COOP on a pipelined
+ *                         handle (sedx_set_pipelined: the recurrence runs
+ *                         beside the next batch's conv stack, fewer CUs held
+ *                         measured faster), COOP16 otherwise (one batch at a
+ *                         time: the shorter recurrence);
+ *                         SEDX_GRU_KERNEL_COOP: the cooperative
  *                         recurrence, 8 workgroups per (32-clip group,
  *                         direction) exchanging h slices every step (up to 8
  *                         clips: the small-batch VALU kernel with a data-tagged
@@ -204,7 +209,12 @@ sedx_status sedx_set_precision(sedx_handle* h, int32_t mode);
  *                         into the MFMA operands (lower product latency, more
  *                         CUs held: slower beside a second batch's conv stack);
  *                         SEDX_GRU_KERNEL_SIMPLE: one workgroup per (clip,
- *                         direction), W_hh streamed from L2 (fp32 FMA).
+ *                         direction), W_hh streamed from L2 (fp32 FMA);
+ *                         SEDX_GRU_KERNEL_COOP16 (exact, more than 8 clips):
+ *                         the cooperative kernel on 16 workgroups per
+ *                         (32-clip group, direction) — half the serial
+ *                         product per step, twice the CUs held;
+ *                         bit-identical to COOP.
  *  SEDX_TUNE_GRU_HANDOFF  (COOP) SEDX_GRU_HANDOFF_AUTO (default): XCD-local hand-off
  *                         when all 8 slices share an XCD, else global;
  *                         SEDX_GRU_HANDOFF_GLOBAL: always the global protocol
@@ -230,7 +240,14 @@ typedef enum {
   SEDX_TUNE_WINO_BLOCK1 = 2,
   SEDX_TUNE_MEL_MFMA = 3
 } sedx_tuning_knob;
-enum { SEDX_GRU_KERNEL_COOP = 0, SEDX_GRU_KERNEL_SIMPLE = 1, SEDX_GRU_KERNEL_TAG16 = 2, SEDX_GRU_KERNEL_TAG8 = 3 };
+enum {
+  SEDX_GRU_KERNEL_COOP = 0,
+  SEDX_GRU_KERNEL_SIMPLE = 1,
+  SEDX_GRU_KERNEL_TAG16 = 2,
+  SEDX_GRU_KERNEL_TAG8 = 3,
+  SEDX_GRU_KERNEL_COOP16 = 4,
+  SEDX_GRU_KERNEL_AUTO = 5
+};
 enum { SEDX_GRU_HANDOFF_AUTO = 0, SEDX_GRU_HANDOFF_GLOBAL = 1 };
 sedx_status sedx_set_tuning(sedx_handle* h, int32_t knob, int32_t value);
 

@@ -88,7 +88,7 @@ struct sedx_handle {
   size_t ws_bytes = 0;
   // optional per-stage timing (sedx_set_profiling): events at stage boundaries
   int precision = SEDX_PRECISION_WINOGRAD;   // GEMM arithmetic (sedx_set_precision; the default is fp32 Winograd)
-  int gru_kernel = SEDX_GRU_KERNEL_COOP;   // sedx_set_tuning
+  int gru_kernel = SEDX_GRU_KERNEL_AUTO;   // sedx_set_tuning
   int gru_handoff = SEDX_GRU_HANDOFF_AUTO;
   int wino_block1 = 2;                     // SEDX_TUNE_WINO_BLOCK1 (2: conv1 inside the Winograd launch)
   int mel_mfma = 0;                        // SEDX_TUNE_MEL_MFMA (measured slower: opt-in)
@@ -436,7 +436,12 @@ sedx_status run_body(sedx_handle* h, int64_t B, const Geometry& g, float* ws, co
     else
       launch_gru_coop(G, iB, (int)g.T3, w.whh, w.bhh, Hs, LG + align_up((size_t)M * h->nac), !x3,
                       h->gru_handoff == SEDX_GRU_HANDOFF_AUTO,
-                      h->gru_kernel == SEDX_GRU_KERNEL_TAG16 ? 0 : h->gru_kernel == SEDX_GRU_KERNEL_TAG8 ? 1 : 2,
+                      h->gru_kernel == SEDX_GRU_KERNEL_TAG16 ? 0 : h->gru_kernel == SEDX_GRU_KERNEL_TAG8 ? 1
+                      : h->gru_kernel == SEDX_GRU_KERNEL_COOP16 ? 3
+                      // AUTO: beside the next batch's conv stack (pipelined) the 8-slice
+                      // kernel holds half the CUs; one batch at a time 16 slices halve
+                      // the recurrence's serial product
+                      : h->gru_kernel == SEDX_GRU_KERNEL_AUTO ? (h->pipelined ? 2 : 3) : 2,
                       h->gru_err_dev, s);
   } else {
     linear(S, w.wqkv, w.wqkv_x3, 1536, 128, w.bqkv, G, 0);
@@ -570,7 +575,7 @@ sedx_status sedx_set_tuning(sedx_handle* h, int32_t knob, int32_t value) {
   switch (knob) {
     case SEDX_TUNE_GRU_KERNEL:
       if (value != SEDX_GRU_KERNEL_COOP && value != SEDX_GRU_KERNEL_SIMPLE && value != SEDX_GRU_KERNEL_TAG16 &&
-          value != SEDX_GRU_KERNEL_TAG8)
+          value != SEDX_GRU_KERNEL_TAG8 && value != SEDX_GRU_KERNEL_COOP16 && value != SEDX_GRU_KERNEL_AUTO)
         break;
       h->gru_kernel = value;
       return SEDX_OK;

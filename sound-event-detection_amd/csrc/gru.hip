@@ -92,7 +92,7 @@ struct GruSync {                      // zeroed every launch
   unsigned ready[8][16];              // per pair: id-exchange arrivals
   unsigned xcc[8][16];                // per pair: slice XCC ids (+1)
   unsigned cnt[8][16];                // per pair: global-protocol step counter
-  unsigned flag[8][8][16];            // per pair, per slice: fast-protocol step flag
+  unsigned flag[8][16][16];           // per pair, per slice: fast-protocol step flag
   unsigned long long stamps[8];       // SEDX_GRU_STAMPS diagnostic builds only
   unsigned mode;                      // 1 = XCD-local protocol was used by pair 0
 };
@@ -120,7 +120,10 @@ __device__ __forceinline__ bool gru_dead(const int* s_err) {
 #define GRU_STAMP(i)
 #endif
 
-template <bool EXACT, bool VALU>
+// NS slices per (group, direction): 8 (32 hidden units each), or 16 (exact
+// MFMA product only: 16 units each, 16x16x4 MFMAs, half the serial product
+// per step; the same fma chains, so bit-identical to NS 8)
+template <bool EXACT, bool VALU, int NS = 8>
 __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__ G, int B, int T,
                                                        const float* __restrict__ whh,
                                                        const float* __restrict__ bhh,
@@ -136,8 +139,11 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
   __shared__ int s_fast;
   __shared__ int s_err;                        // a bounded spin timed out: outputs become NaN
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  static_assert(NS == 8 || (NS == 16 && EXACT && !VALU), "16 slices: the exact MFMA product");
+  constexpr int US = 256 / NS;                 // hidden units per slice
+  constexpr int NPAIR = 32 * US;               // (clip, unit) pairs of a slice's gate phase
   const int pair = blockIdx.x & 7;             // dispatch residue -> one XCD (observed)
-  const int p = blockIdx.x >> 3;               // slice 0..7
+  const int p = blockIdx.x >> 3;               // slice 0 .. NS - 1
   const int slot = pair >> 1, dir = pair & 1;
   if (slot >= nslots) return;                  // whole workgroup exits (uniform)
   const int nt = wave % 3, kq = wave / 3, h = lane >> 5;
@@ -152,7 +158,7 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __hip_atomic_fetch_add(&sync->ready[pair][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     unsigned spins = 0;
-    while (g_ld(&sync->ready[pair][0]) < 8u) {
+    while (g_ld(&sync->ready[pair][0]) < (unsigned)NS) {
       __builtin_amdgcn_s_sleep(1);
       if (++spins > GRU_SPIN) {
         gru_fail(sync, host_err, 1u);
@@ -162,7 +168,7 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
     }
     int fast = allow_fast;
     const unsigned x0 = g_ld(&sync->xcc[pair][0]);
-    for (int i = 1; i < 8; ++i) fast &= (g_ld(&sync->xcc[pair][i]) == x0);
+    for (int i = 1; i < NS; ++i) fast &= (g_ld(&sync->xcc[pair][i]) == x0);
     s_fast = fast;
   }
   __syncthreads();
@@ -176,9 +182,17 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
   // W_hh slice -> B fragments: B[k][n] = W_hh[gate row n][k]
   bf16x8_g Bhi[4], Blo[4];
   static_assert(EXACT || !VALU, "the VALU product is the exact arithmetic");
-  float Bf[EXACT && !VALU ? 32 : 1];
+  float Bf[EXACT && !VALU ? (NS == 16 ? 16 : 32) : 1];
   float4 Wv[VALU ? 16 : 1];   // VALU: the lane's gate row over its whole K quarter
-  {
+  if constexpr (NS == 16) {
+    // 16x16x4: lane (k = lane >> 4, unit lane & 15) of steps s of eighths
+    // 2 kq + e: Bf[8 e + s] = W_hh[row][64 kq + 32 e + 4 s + (lane >> 4)]
+    const float* wrow = whh + ((int64_t)dir * 768 + nt * 256 + US * p + (lane & 15)) * 256;
+#pragma unroll
+    for (int e = 0; e < 2; ++e)
+#pragma unroll
+      for (int st = 0; st < 8; ++st) Bf[8 * e + st] = wrow[64 * kq + 32 * e + 4 * st + (lane >> 4)];
+  } else {
     const float* wrow = whh + ((int64_t)dir * 768 + nt * 256 + 32 * p + (lane & 31)) * 256;
     if constexpr (VALU) {
 #pragma unroll
@@ -200,10 +214,10 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
     }
   }
   float* Af = reinterpret_cast<float*>(Aimg);  // EXACT: h_{s-1} [256 k][32 clips], swizzled
-  const int u = tid & 31;                      // gate-phase unit (768 % 32 == 0)
-  const float br = bhh[dir * 768 + 32 * p + u];
-  const float bz = bhh[dir * 768 + 256 + 32 * p + u];
-  const float bn = bhh[dir * 768 + 512 + 32 * p + u];
+  const int u = tid % US;                      // gate-phase unit (768 % US == 0)
+  const float br = bhh[dir * 768 + US * p + u];
+  const float bz = bhh[dir * 768 + 256 + US * p + u];
+  const float bn = bhh[dir * 768 + 512 + US * p + u];
   float* Xs = X + (int64_t)pair * 2 * 32 * 256;
   unsigned* C = &sync->cnt[pair][0];
   unsigned* Fl = &sync->flag[pair][0][0];
@@ -234,9 +248,9 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int pr = tid + 768 * i;
-        const int c = pr >> 5;
-        if (pr < 1024 && c < nc) {
-          const float* gp = G + ((int64_t)(c0 + c) * T + t) * 1536 + dir * 768 + 32 * p + u;
+        const int c = pr / US;
+        if (pr < NPAIR && c < nc) {
+          const float* gp = G + ((int64_t)(c0 + c) * T + t) * 1536 + dir * 768 + US * p + u;
           gi[i][0] = gp[0];
           gi[i][1] = gp[256];
           gi[i][2] = gp[512];
@@ -249,7 +263,7 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
       // at every step
       if (!VALU && gs > 0) {
         if (fast) {
-          if (tid < 8) {
+          if (tid < NS) {
             unsigned spins = 0;
             while (!gru_dead(&s_err) && g_ld(Fl + tid * 16) < (unsigned)gs) {
               if (++spins > GRU_SPIN) {
@@ -260,7 +274,7 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
             }
           }
         } else if (tid == 0) {
-          const unsigned target = 8u * (unsigned)gs;
+          const unsigned target = (unsigned)NS * (unsigned)gs;
           unsigned spins = 0;
           while (!gru_dead(&s_err) && g_ld(C) < target) {
             __builtin_amdgcn_s_sleep(1);
@@ -355,9 +369,9 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
             Aimg[(ks * 32 + c) * 4 + (hh ^ sw)] = hi;
             Aimg[(ks * 32 + c) * 4 + ((2 + hh) ^ sw)] = lo;
           }
-          if ((oct >> 2) == p) {
+          if (oct / (US / 8) == p) {   // the slice's own units: h_{s-1} for the gate phase
 #pragma unroll
-            for (int e = 0; e < 8; ++e) hprev[c][8 * (oct & 3) + e] = v[e];
+            for (int e = 0; e < 8; ++e) hprev[c][8 * (oct % (US / 8)) + e] = v[e];
           }
         }
       }
@@ -386,6 +400,36 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
           part[2 * kq][nt][c][lane & 31] = a0;
           part[2 * kq + 1][nt][c][lane & 31] = a1;
         }
+      } else if constexpr (EXACT && NS == 16) {
+        // four chains per wave — (eighth 2 kq + e, clip tile mt) — each over
+        // its 32 k in ascending order, 4 k per v_mfma_f32_16x16x4_f32: the
+        // fma chains of the 32x32x2 form, so the same bits
+        const int cl = lane & 15, kk = lane >> 4;
+        f32x4_g a4[2][2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+#pragma unroll
+          for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) a4[e][mt][r] = 0.f;
+#pragma unroll
+        for (int st = 0; st < 8; ++st)
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const int k = 64 * kq + 32 * e + 4 * st + kk;
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt) {
+              const float a = Af[k * 32 + ((16 * mt + cl) ^ ((k >> 3) & 31))];
+              a4[e][mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, Bf[8 * e + st], a4[e][mt], 0, 0, 0);
+            }
+          }
+        // D row 4 (lane >> 4) + r = clip 16 mt + 4 kk + r, column = unit cl
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+#pragma unroll
+          for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) part[2 * kq + e][nt][16 * mt + 4 * kk + r][cl] = a4[e][mt][r];
       } else if constexpr (EXACT) {
         const int c = lane & 31;
 #pragma unroll
@@ -410,7 +454,7 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
           acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(alo, Bhi[ks], acc, 0, 0, 0);
         }
       }
-      if constexpr (EXACT && !VALU) {
+      if constexpr (EXACT && !VALU && NS == 8) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           part[2 * kq][nt][(r & 3) + 8 * (r >> 2) + 4 * h][lane & 31] = acc[r];
@@ -429,8 +473,8 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
       for (int i = 0; i < 2; ++i) {
         const int pr = tid + 768 * i;
         hvs[i] = 0.f;
-        if (pr < 1024) {
-          const int c = pr >> 5;
+        if (pr < NPAIR) {
+          const int c = pr / US;
           if (c < nc) {
             float ghr = part[0][0][c][u], ghz = part[0][1][c][u], ghn = part[0][2][c][u];
 #pragma unroll
@@ -446,11 +490,11 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
             const float hn = gru_cell(gi[i][0], gi[i][1], gi[i][2], ghr, ghz, ghn, hp);
             hvs[i] = s_err ? __builtin_nanf("") : hn;   // NaN propagates to every slice
           }
-          float* xp = dst + c * 256 + 32 * p + u;
+          float* xp = dst + c * 256 + US * p + u;
           if (c >= nc) {
             // absent clip: nothing to publish
           } else if (VALU) {
-            __hip_atomic_store(Gx + (gs & 1) * GRU_VALU_CLIPS * 256 + c * 256 + 32 * p + u,
+            __hip_atomic_store(Gx + (gs & 1) * GRU_VALU_CLIPS * 256 + c * 256 + US * p + u,
                                ((unsigned long long)(gs + 1) << 32) | __float_as_uint(hvs[i]), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
           } else if (fast) {
@@ -482,9 +526,9 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int pr = tid + 768 * i;
-        const int c = pr >> 5;
-        if (pr < 1024 && c < nc)
-          H[((int64_t)(c0 + c) * T + t) * 512 + dir * 256 + 32 * p + u] = hvs[i];
+        const int c = pr / US;
+        if (pr < NPAIR && c < nc)
+          H[((int64_t)(c0 + c) * T + t) * 512 + dir * 256 + US * p + u] = hvs[i];
       }
     }
   }
@@ -750,7 +794,7 @@ void launch_gru_coop(const float* G, int B, int T, const float* whh, const float
   const size_t sync_bytes = (sizeof(GruSync) + 255) & ~size_t(255);
   float* X = reinterpret_cast<float*>(static_cast<char*>(ws) + sync_bytes);
   const bool valu = exact && B <= GRU_VALU_CLIPS;
-  if (exact && !valu && variant != 2) {
+  if (exact && !valu && variant != 2 && variant != 3) {
     auto* Xg = reinterpret_cast<unsigned long long*>(X);
     if (variant == 1)
       launch_gru_tag<8>(G, B, T, whh, bhh, H, sync, Xg, sync_bytes, host_err, s);
@@ -765,6 +809,9 @@ void launch_gru_coop(const float* G, int B, int T, const float* whh, const float
   (void)hipMemsetAsync(sync, 0, sync_bytes + (valu ? (size_t)2 * 2 * GRU_VALU_CLIPS * 256 * 8 : 0), s);
   if (valu)
     launch_kernel(gru_coop_kernel<true, true>, dim3(64), 768, s, G, B, T, whh, bhh, H, X, sync, nslots,
+                  allow_fast ? 1 : 0, host_err);
+  else if (exact && variant == 3)   // 16 slices per (group, direction)
+    launch_kernel(gru_coop_kernel<true, false, 16>, dim3(128), 768, s, G, B, T, whh, bhh, H, X, sync, nslots,
                   allow_fast ? 1 : 0, host_err);
   else if (exact)
     launch_kernel(gru_coop_kernel<true, false>, dim3(64), 768, s, G, B, T, whh, bhh, H, X, sync, nslots,

@@ -195,21 +195,24 @@ def test_gru_handoff_modes_bit_identical(prec):
 
 @pytest.mark.parametrize('n_clips', [40, 80])
 def test_gru_tag_kernels_bit_identical(n_clips):
-    """The opt-in data-tagged recurrences (SEDX_GRU_KERNEL_TAG16 / TAG8: 16-clip
-    groups, granules straight into v_mfma_f32_16x16x4_f32 operands) keep the
-    exact kernels' arithmetic contract (eight in-order K partials, summed in
-    order): bit-identical to the default 32-clip kernel, ragged last group and
-    more groups than resident slots (80 clips = 5 groups of 16) included."""
+    """The data-tagged recurrences (SEDX_GRU_KERNEL_TAG16 / TAG8: 16-clip
+    groups, granules straight into v_mfma_f32_16x16x4_f32 operands) and the
+    16-slice cooperative kernel (COOP16: 16 units per workgroup on 16x16x4
+    MFMAs) keep the exact kernels' arithmetic contract (eight in-order K
+    partials, summed in order): bit-identical to the 8-slice 32-clip kernel,
+    ragged last group and more groups than resident slots (80 clips) included;
+    AUTO (the default: COOP16 on an unpipelined handle) too."""
     from sedx import _lib
     m = build(GRU).set_precision('exact')
     wave = synth.make_waveforms(n_clips, seconds=2.0, sample_rate=16000, seed=n_clips + 3)
     outs = {}
-    for knob in (0, 2, 3):     # COOP (default), TAG16, TAG8
+    for knob in (0, 2, 3, 4, 5):     # COOP, TAG16, TAG8, COOP16, AUTO
         _tune(m, _lib.TUNE_GRU_KERNEL, knob)
         outs[knob] = run(m, wave)['framewise_output']
-    _tune(m, _lib.TUNE_GRU_KERNEL, 0)
+    _tune(m, _lib.TUNE_GRU_KERNEL, 5)
     assert np.isfinite(outs[0]).all()
-    assert np.array_equal(outs[2], outs[0]) and np.array_equal(outs[3], outs[0])
+    for knob in (2, 3, 4, 5):
+        assert np.array_equal(outs[knob], outs[0]), knob
 
 
 def test_gru_exact_recurrence_is_fp32():
@@ -222,7 +225,7 @@ def test_gru_exact_recurrence_is_fp32():
     coop = run(m, wave)
     _tune(m, _lib.TUNE_GRU_KERNEL, 1)
     simple = run(m, wave)
-    _tune(m, _lib.TUNE_GRU_KERNEL, 0)
+    _tune(m, _lib.TUNE_GRU_KERNEL, 5)
     ref = O.forward(O.full_state(synth.make_state_dict(GRU, seed=0)), GRU, wave=wave)
     for k in ('framewise_output', 'embedding'):
         e_cs = err(coop[k], simple[k])

@@ -3,9 +3,9 @@
 # (two-stream timed region and one batch at a time) per SEDX_TUNE_GRU_KERNEL.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-for r in 1 2; do
-  for k in ${KERNELS:-coop tag16 tag8}; do
-    timeout -k 10 200 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --gru-kernel $k > gpurun_out/gru_$k$r.log 2>&1 || exit $?
+for r in ${ROUNDS:-1 2}; do
+  for k in ${KERNELS:-coop tag16 tag8 coop16}; do
+    timeout -k 10 200 python bench.py --steps 20 --warmup 3 --no-cpu-baseline ${BENCH_ARGS} --gru-kernel $k > gpurun_out/gru_$k$r.log 2>&1 || exit $?
     python3 -c "
 import json
 s=open('gpurun_out/gru_$k$r.log').read(); d=json.loads(s[s.rfind('{\"metric\"'):].split('\n')[0])

@@ -13,7 +13,7 @@ struct Sync {                         // must mirror GruSync in gru.hip
   unsigned ready[8][16];
   unsigned xcc[8][16];
   unsigned cnt[8][16];
-  unsigned flag[8][8][16];
+  unsigned flag[8][16][16];
   unsigned long long stamps[8];
   unsigned mode;
 };
@@ -37,14 +37,14 @@ int main(int argc, char** argv) {
   hipMemcpy(Bb, hb.data(), hb.size() * 4, hipMemcpyHostToDevice);
   hipEvent_t e0, e1;
   hipEventCreate(&e0); hipEventCreate(&e1);
-  // variants: 0 = tagged 16-clip groups x 16 slices, 1 = tagged x 8 slices,
+  // variants: 0 = tagged 16-clip groups x 16 slices, 1 = tagged x 8 slices, 3 = coop on 16 slices,
   // 2 = the 32-clip flag kernel (fast = XCD-local hand-off allowed)
   std::vector<float> ref;
   for (int exact = 1; exact >= 0; --exact)
-    for (int variant = 0; variant < 3; ++variant)
+    for (int variant = 0; variant < 4; ++variant)
     for (int fast = 0; fast < 2; ++fast) {
       if ((!exact || variant < 2) && !fast) continue;
-      if (!exact && variant < 2) continue;
+      if (!exact && (variant < 2 || variant == 3)) continue;
       sedx::launch_gru_coop(G, B, T, W, Bb, H, ws, exact, fast, variant, nullptr, 0);
       hipDeviceSynchronize();
       if (exact) {   // every exact variant must give the same bits
