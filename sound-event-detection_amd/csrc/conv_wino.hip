@@ -410,19 +410,15 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
     issue_reads(nbuf, pd, un);
     transform(pd, vn);
     if constexpr (C1) conv1(cc, cb);
-#ifdef SEDX_WINO_READS_FIRST
-    // every LDS read of the next chunk ahead of the MFMAs (~1000 cycles of
-    // the SIMD's matrix work before the transform consumes them)
-    __builtin_amdgcn_sched_group_barrier(0x100, 20, 0);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-#else
+    // (measured slower: every LDS read ahead of the MFMAs, -10 %: the
+    // transform then waits at the end of the chunk with nothing to overlap;
+    // C1's conv1 beside the first MFMAs with its weights loaded a chunk
+    // ahead, b1c2 +5 %: the reads then issue late)
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
       __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // 2 LDS reads
     }
-#endif
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
