@@ -710,6 +710,13 @@ static int wino_device_cus() {
 #define SEDX_WINO_ITEMS 4
 #endif
 constexpr int WINO_ITEMS = SEDX_WINO_ITEMS;
+// block 1's one-launch kernel: ~8 items per workgroup (isolated 0.731-0.733
+// ms against 0.735-0.744 at 4 and 0.748-0.752 at 2; the two-stream headline
+// the same within noise over four alternating rounds, tools/gpu_ab_iso.sh)
+#ifndef SEDX_WINO_ITEMS_B1
+#define SEDX_WINO_ITEMS_B1 8
+#endif
+constexpr int WINO_ITEMS_B1 = SEDX_WINO_ITEMS_B1;
 
 template <int F, int TG>
 static void launch_wino_w(const float* in, int B, int T, int Cin, int Cout, const float* U, const float* bias,
@@ -806,7 +813,7 @@ static void launch_block1_w(const float* x0, int B, int T, const float* U, const
   const int64_t nitems = (tblocks + 7) / 8 * 8;           // one channel group (64 channels) per item
   if (nitems > INT32_MAX || tblocks <= 0 || (int64_t)B * T * 64 >= INT32_MAX) return note_launch_error(hipErrorInvalidValue);
   const int64_t resident = (int64_t)wino_device_cus() * G::WG_PER_CU / 8 * 8;
-  const int64_t per = (nitems + WINO_ITEMS - 1) / WINO_ITEMS;
+  const int64_t per = (nitems + WINO_ITEMS_B1 - 1) / WINO_ITEMS_B1;
   const int64_t nwg = std::min<int64_t>(nitems, std::max<int64_t>(std::max<int64_t>(8, resident), (per + 7) / 8 * 8));
   auto* k_ = wino_block1_kernel<TG>;
   if (!launch_info(reinterpret_cast<const void*>(k_), G::THREADS, G::LDS_BYTES).ok) return;
