@@ -375,7 +375,7 @@ def stage_times_isolated(model, wave, dev, reps):
 # from the rocprofv3 passes of this bench command (tools/profile_round.sh ->
 # tools/pmc_summary.py; FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE),
 # committed under profiles/.
-PROFILE_SUMMARY = os.path.join(REPO, 'profiles', 'r03c_kernel_summary.json')
+PROFILE_SUMMARY = os.path.join(REPO, 'profiles', 'r03d_kernel_summary.json')
 
 
 # block 1's conv1 (Cin 1 -> 64) computed inside the b1c2 launch (winograd
