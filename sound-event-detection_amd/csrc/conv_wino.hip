@@ -266,9 +266,9 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
     ptrs(doff, n0);
   }
 
-  // ---- C1: conv1 into the halo images.  Wave wv < NGRP owns halo slots
-  // 64 wv + lane (one pixel per lane, the parity-plane slot order of the
-  // halo DMA).  Per item its 3x3 X0 window sits in 9 registers, read from the
+  // ---- C1: conv1 into the halo images.  Wave wv owns halo slots 64 wv +
+  // lane (one pixel per lane, the parity-plane slot order of the halo DMA;
+  // slots past the halo compute into the padding, so no wave branches).  Per item its 3x3 X0 window sits in 9 registers, read from the
   // item's X0 tile in LDS (LDS-DMA'd with the previous item's last chunk, or
   // in the prologue); per chunk it computes its pixel's 4 channels of the
   // chunk c + 2 (two ahead: chunk c + 1 is read during chunk c) into that
@@ -399,7 +399,7 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
   // k-step 1 (2 khalf + 1) — with the next chunk's LDS reads spread over the
   // first 8 and its transform over the last 8.  (Keeping the two k-steps of
   // an accumulator apart with a scheduling barrier measured 6 % slower.)
-  // C1: then conv1 of channel chunk cc into ring buffer cb (cc < 0: none)
+  // C1: then conv1 of channel chunk cc into ring buffer cb
   auto step = [&](const float (&vc)[2][8], const float2 (&uc)[8], int nbuf, float (&vn)[2][8], float2 (&un)[8],
                   int cc = -1, int cb = 0) {
 #pragma unroll
