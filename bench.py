@@ -652,6 +652,16 @@ def main():
     for _ in range(3):
         h2h()
     p50, p99 = latency(h2h, B, max(5, min(args.steps, 20))) if args.mode == 'clip' else (None, None)
+    # the same from int16 host input: the reference's batched clip driver
+    # reads HDF5 int16 waveforms (utils/data_generator.py:20-49); the model
+    # takes them as they are and dequantises on the device (half the PCIe bytes)
+    p50_i16 = None
+    if args.mode == 'clip' and side:
+        host_i16 = (torch.clamp(wave, -1.0, 1.0) * 32767.0).to(torch.int16).cpu().pin_memory()
+        h2h16 = host_to_host_step(model, host_i16, host_out, dev, world, rank)
+        for _ in range(3):
+            h2h16()
+        p50_i16, _ = latency(h2h16, B, max(5, min(args.steps, 20)))
 
     extra = {}
     if side:
@@ -736,6 +746,7 @@ def main():
             'ms_per_clip_p50_note': 'per batch, one at a time, from pinned host input (H2D on a copy '
                                     'stream) to framewise in pinned host memory on rank 0',
             'ms_per_clip_p50_device': round(p50_dev, 4) if p50_dev is not None else None,
+            'ms_per_clip_p50_i16_input': round(p50_i16, 4) if p50_i16 is not None else None,
             'ms_per_clip_p99_device': round(p99_dev, 4) if p99_dev is not None else None,
             'roofline': roof, 'cpu_baseline': cpu, 'stage_ms': stage_ms,
             # the libsedx.so this run loaded (SEDX_PKG selects another build for A/B runs)
