@@ -136,36 +136,83 @@ sedx_status sedx_gamma_features(sedx_handle* h, const float* d_audio, int64_t B,
                                 size_t workspace_bytes, void* stream);
 sedx_status sedx_gamma_workspace_size(const sedx_handle* h, int64_t B, int64_t L, size_t* bytes);
 
-/* Windowed driver (pytorch/predict.py:297-349; main_strong.py:790-833).
- * Slices every clip into windows of `sample_duration` s at stride
- * `overlap_value` s (loop `while end <= audio_duration`), runs ALL windows of
- * ALL clips as one batch, overlap-adds (utilities.py:405-423) and applies the
- * reference's avg_merge divisor schedule (utilities.py:425-446).
- *   d_audio       [n_clips, L_clip] (every clip has duration L_clip/sr)
- *   pad_clip      0 = predict.py (each window pad_truncate'd),
- *                 1 = main_strong (clip pad_truncate'd to 10 s first)
+/* Windowed drivers: pytorch/predict.py:297-349 (`predict`) and
+ * pytorch/main_strong.py:786-835 (`inference_prob_overlap`) / :1052-1100
+ * (`inference_prob_vote`).  The reference's loops take three independent
+ * numbers, kept apart here exactly as they are there:
+ *   stride      how far `start` advances per window:
+ *                 predict.py  `start += 1` with --overlap, else
+ *                             `start += sample_duration` (predict.py:334-337);
+ *                 main_strong `start += overlap_value` (main_strong.py:829, :1094)
+ *               (start is an int in predict.py, a float64 running sum in
+ *               main_strong; window w reads samples int(start_w * sr) ...)
+ *   merge step  int(100 * overlap_value) frames, computed in float64
+ *               (utilities.py:406, :426; vad.py:63): window w lands at frame
+ *               w * step of the merged output WHATEVER the stride
+ *   loop bound  `while end <= audio_duration`, end = start + sample_duration,
+ *               audio_duration = librosa.get_duration of the file (predict.py:277,
+ *               main_strong.py:778).
+ * predict.py pad_truncate's every window to sample_duration s (:305);
+ * main_strong pad_truncate's the whole clip to 10 s (:790) and feeds each
+ * window as sliced, so a window that runs past 10 s is SHORTER (its own
+ * forward, fewer frames; the merge then follows numpy's slicing and
+ * broadcasting exactly, raising SEDX_EINVAL where numpy raises). */
+typedef enum { SEDX_DRIVER_PREDICT = 0, SEDX_DRIVER_MAIN_STRONG = 1 } sedx_window_driver;
+typedef struct {
+  int32_t driver;           /* sedx_window_driver */
+  int32_t overlap;          /* PREDICT: predict.py --overlap (stride 1 s, else sample_duration s); MAIN_STRONG: ignored */
+  int32_t sample_duration;  /* seconds (an int in both drivers: predict.py:701, main_strong.py:746) */
+  int32_t reserved;         /* must be 0 */
+  double overlap_value;     /* merge step int(100 * overlap_value); MAIN_STRONG: also the stride */
+  double audio_duration;    /* the loop bound in seconds; <= 0: L_clip / sample_rate */
+} sedx_window_spec;
+
+/* Handle-free loop control: the sample offset of every window and the
+ * samples the model receives for it (h_len: sample_duration * sr, except
+ * main_strong windows that run past the 10 s padded clip).  Fills at most
+ * `capacity` entries (h_start / h_len may be NULL) and sets *n_windows.
+ * SEDX_EINVAL for sample_duration <= 0 or a stride <= 0 (the reference's loop
+ * never ends).  The model-dependent limits (a window of <= n_fft/2 samples
+ * fails the STFT's reflect padding, pytorch/stft.py:237; fewer than 8 frames
+ * fail the third 2x2 pooling, models.py:139) are checked by
+ * sedx_window_geometry, which needs the handle. */
+sedx_status sedx_window_starts(int32_t sample_rate, int64_t L_clip, const sedx_window_spec* spec,
+                               int64_t* h_start, int64_t* h_len, int64_t capacity, int64_t* n_windows);
+/* Handle-free host merge: utilities.merge applied window by window exactly
+ * as the drivers call it (predict.py:323-329), then utilities.avg_merge when
+ * `avg` (predict.py:349), on float32 host arrays.  h_win = the windows'
+ * framewise outputs [frames[w]][C] concatenated in window order; h_out
+ * [merged_frames][C] (NULL: size query).  Slicing with numpy's clamping and
+ * broadcasting semantics; SEDX_EINVAL where numpy raises (broadcast of
+ * mismatched lengths, avg_merge with a zero step). */
+sedx_status sedx_merge_host(const float* h_win, const int64_t* frames, int64_t n_win, int64_t C,
+                            int32_t sample_duration, double overlap_value, int32_t avg, float* h_out,
+                            int64_t capacity_frames, int64_t* merged_frames);
+
+/* Runs ALL windows of ALL clips as one batch (a main_strong window shorter
+ * than sample_duration as its own small batch), overlap-adds on the GPU
+ * (utilities.py:405-423) and applies the avg_merge divisor schedule
+ * (utilities.py:425-446).
+ *   d_audio       [n_clips, L_clip] (every clip the same length)
  *   d_merged      [n_clips, merged_frames, classes_num]
- * sedx_window_geometry returns n_windows per clip and merged_frames. */
-sedx_status sedx_window_geometry(const sedx_handle* h, int64_t L_clip, float sample_duration,
-                                 float overlap_value, int32_t pad_clip, int64_t* n_windows,
-                                 int64_t* window_samples, int64_t* merged_frames);
-sedx_status sedx_forward_windows(sedx_handle* h, const float* d_audio, int64_t n_clips,
-                                 int64_t L_clip, float sample_duration, float overlap_value,
-                                 int32_t pad_clip, float* d_merged, void* d_workspace,
+ * sedx_window_geometry returns n_windows per clip, samples per full window
+ * and merged_frames. */
+sedx_status sedx_window_geometry(const sedx_handle* h, int64_t L_clip, const sedx_window_spec* spec,
+                                 int64_t* n_windows, int64_t* window_samples, int64_t* merged_frames);
+sedx_status sedx_forward_windows(sedx_handle* h, const float* d_audio, int64_t n_clips, int64_t L_clip,
+                                 const sedx_window_spec* spec, float* d_merged, void* d_workspace,
                                  size_t workspace_bytes, void* stream);
 sedx_status sedx_window_workspace_size(const sedx_handle* h, int64_t n_clips, int64_t L_clip,
-                                       float sample_duration, float overlap_value,
-                                       int32_t pad_clip, size_t* bytes);
-/* Voting variant (inference_prob_vote, pytorch/main_strong.py:1058-1097):
+                                       const sedx_window_spec* spec, size_t* bytes);
+/* Voting variant (inference_prob_vote, pytorch/main_strong.py:1052-1100):
  * every window's framewise output is binarised, x > bin_thres[k] (host f64
  * [classes_num]; the reference passes sed_low_threshold, main_strong.py:1082,
  * binarize_pred :870-883), and the 0/1 windows are overlap-added with
  * utilities.merge — no avg_merge.  d_votes [n_clips, merged_frames,
  * classes_num] holds the vote counts (exact small integers) for
  * sedx_events_device(mode = 1).  Workspace: sedx_window_workspace_size. */
-sedx_status sedx_forward_windows_vote(sedx_handle* h, const float* d_audio, int64_t n_clips,
-                                      int64_t L_clip, float sample_duration, float overlap_value,
-                                      int32_t pad_clip, const double* bin_thres, float* d_votes,
+sedx_status sedx_forward_windows_vote(sedx_handle* h, const float* d_audio, int64_t n_clips, int64_t L_clip,
+                                      const sedx_window_spec* spec, const double* bin_thres, float* d_votes,
                                       void* d_workspace, size_t workspace_bytes, void* stream);
 
 /* Arithmetic of the GEMM-shaped work: the 9-layer conv stack (96.8 % of the
@@ -306,7 +353,8 @@ sedx_status sedx_events(const float* h_framewise, int64_t n_clips, int64_t T, in
  *           counts from sedx_forward_windows_vote, as
  *           frame_binary_prediction_to_event_prediction
  *           (utils/utilities.py:216-276) calls it; high_thres is unused there
- *           (may be NULL), overlap_value / sample_duration give its blocks.
+ *           (may be NULL), overlap_value (float64, int(100 * overlap_value)
+ *           frames per block, vad.py:63) / sample_duration give its blocks.
  *   d_x       [n_clips, T, C] device
  *   d_events  int32 [capacity][4] (clip, class, bgn, fin) in (clip, class,
  *             time) order; events past capacity are dropped
@@ -318,7 +366,7 @@ sedx_status sedx_events_workspace_size(int64_t n_clips, int64_t T, int64_t C, si
 sedx_status sedx_events_device(const float* d_x, int64_t n_clips, int64_t T, int64_t C,
                                const double* high_thres, const double* low_thres,
                                int32_t use_low_thres, const int64_t* n_smooth, const int64_t* n_salt,
-                               int32_t mode, float overlap_value, int32_t sample_duration,
+                               int32_t mode, double overlap_value, int32_t sample_duration,
                                int32_t* d_events, int64_t capacity, int64_t* d_info,
                                void* d_workspace, size_t workspace_bytes, void* stream);
 

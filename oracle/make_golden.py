@@ -103,18 +103,32 @@ DEFAULT_PREDICT = {'audio_tagging_threshold': 0.099, 'sed_high_threshold': 0.5,
                    'sed_low_threshold': 0.3, 'n_smooth': 10, 'n_salt': 10}   # predict.py:252-257
 
 
-def windowed(m, audio, sr, sample_duration, overlap_value, pad_clip_to):
-    """predict.py:297-349 / main_strong.py:790-833 loop with reference parts."""
-    audio_duration = len(audio) / float(sr)
-    if pad_clip_to is not None:
-        audio = ref_util.pad_truncate_sequence(audio, pad_clip_to)
+def windowed(m, audio, sr, sample_duration, overlap_value, driver='predict', overlap=True, audio_duration=None):
+    """The reference drivers' window loops line for line, around the
+    reference's own model, merge and avg_merge:
+      driver='predict'      pytorch/predict.py:277-349 — every window
+                            pad_truncate'd to sample_duration s (:263, :305);
+                            ``start += 1`` with --overlap, else ``start +=
+                            sample_duration`` (:334-337)
+      driver='main_strong'  pytorch/main_strong.py:778-832 — the clip
+                            pad_truncate'd to 10 s (:761, :790), windows
+                            sliced without padding (:795-797), ``start +=
+                            overlap_value`` (:829)
+    audio_duration stands for librosa.get_duration(filename) (predict.py:277,
+    main_strong.py:778): the file's own length."""
+    if audio_duration is None:
+        audio_duration = len(audio) / float(sr)
+    audio_full = ref_util.pad_truncate_sequence(audio, sr * 10) if driver == 'main_strong' else audio
+    audio_samples = sr * sample_duration
     num_segment, start, end, merged, prev = 1, 0, 0, None, None
     while end <= audio_duration:
-        s = int(start * sr)
-        seg = audio[s:int(sample_duration * sr) + s]
-        if pad_clip_to is None:
-            seg = ref_util.pad_truncate_sequence(seg, sr * sample_duration)
-        seg = torch.reshape(torch.Tensor(seg), (1, -1))
+        start_index = int(start * sr)
+        end_index = int((sample_duration * sr) + start_index)
+        seg = audio_full[start_index:end_index]
+        if driver == 'predict':
+            seg = ref_util.pad_truncate_sequence(seg, audio_samples)
+        seg = torch.Tensor(seg)
+        seg = torch.reshape(seg, (1, seg.size()[0]))
         with torch.no_grad():
             curr = m(seg)['framewise_output'].data.cpu().numpy()
         if num_segment == 2:
@@ -124,7 +138,10 @@ def windowed(m, audio, sr, sample_duration, overlap_value, pad_clip_to):
         else:
             merged = curr
         prev = curr
-        start += overlap_value
+        if driver == 'predict':
+            start += 1 if overlap else sample_duration
+        else:
+            start += overlap_value
         end = start + sample_duration
         num_segment += 1
     return ref_util.avg_merge(merged, sample_duration, overlap_value)
@@ -187,8 +204,8 @@ def main():
     for mt in (GRU, TRF):
         m = build(mt)
         audio = full[0].astype(np.float32)
-        merged = windowed(m, audio, 16000, 5, 1, None)
-        merged_ms = windowed(m, audio, 16000, 6, 0.5, 16000 * 10)   # main_strong sweep setting
+        merged = windowed(m, audio, 16000, 5, 1, 'predict', overlap=True)       # run.sh's predict.py call
+        merged_ms = windowed(m, audio, 16000, 6, 0.5, 'main_strong')           # main_strong sweep setting
         np.savez_compressed(os.path.join(OUT, 'windowed_%s.npz' % mt),
                             merged_5_1=merged, merged_6_05=merged_ms)
         ev_out[mt] = {'default': events(merged.copy(), DEFAULT_PREDICT),

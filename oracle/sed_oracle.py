@@ -287,33 +287,47 @@ def avg_merge(merged, sample_duration, overlap_value=1):
     return merged
 
 
-def window_starts(audio_duration, sample_duration, overlap_value):
+def window_starts(audio_duration, sample_duration, stride):
     """Loop control of pytorch/predict.py:297-338 and
-    pytorch/main_strong.py:791-832 (``while end <= audio_duration``)."""
+    pytorch/main_strong.py:791-832 (``while end <= audio_duration``;
+    ``start += stride``)."""
     starts = []
     start, end = 0, 0
     while end <= audio_duration:
         starts.append(start)
-        start += overlap_value
+        start += stride
         end = start + sample_duration
     return starts
 
 
-def predict_windows(sd, model_type, audio, sample_rate, sample_duration=5,
-                    overlap_value=1, pad_clip_to=None):
-    """Per-clip windowed inference: predict.py:297-349 (pad_clip_to=None) or
-    main_strong.py:790-833 (pad_clip_to = 10 s of samples).  Runs the model
-    batch-1 per window exactly like the reference; returns merged [1,N,C]."""
-    audio_duration = len(audio) / float(sample_rate)
-    if pad_clip_to is not None:
-        audio = pad_truncate_sequence(audio, pad_clip_to)
+def driver_stride(driver, sample_duration, overlap_value, overlap=True):
+    """predict.py:334-337 (``start += 1`` with --overlap, else ``start +=
+    sample_duration``) / main_strong.py:829 (``start += overlap_value``)."""
+    if driver == 'predict':
+        return 1 if overlap else sample_duration
+    if driver == 'main_strong':
+        return overlap_value
+    raise ValueError(driver)
+
+
+def predict_windows(sd, model_type, audio, sample_rate, sample_duration=5, overlap_value=1.0,
+                    driver='predict', overlap=True, audio_duration=None):
+    """Per-clip windowed inference: predict.py:297-349 (driver='predict':
+    every window pad_truncate'd, :305) or main_strong.py:786-835
+    (driver='main_strong': the clip pad_truncate'd to 10 s, :790, windows
+    sliced without padding, :795-797).  Runs the model batch-1 per window
+    exactly like the reference; returns merged [1,N,C]."""
+    if audio_duration is None:
+        audio_duration = len(audio) / float(sample_rate)
+    if driver == 'main_strong':
+        audio = pad_truncate_sequence(audio, sample_rate * 10)
     n_win = int(sample_rate * sample_duration)
     merged, prev = None, None
-    for num_segment, start in enumerate(window_starts(audio_duration, sample_duration,
-                                                      overlap_value), start=1):
+    stride = driver_stride(driver, sample_duration, overlap_value, overlap)
+    for num_segment, start in enumerate(window_starts(audio_duration, sample_duration, stride), start=1):
         s = int(start * sample_rate)
         seg = audio[s:int(sample_duration * sample_rate) + s]
-        if pad_clip_to is None:
+        if driver == 'predict':
             seg = pad_truncate_sequence(seg, n_win)
         seg = torch.Tensor(np.asarray(seg))[None, :]
         curr = forward(sd, model_type, wave=seg)['framewise_output'].numpy()
@@ -425,19 +439,17 @@ def activity_detection_binary(x, overlap_value, sample_duration, thres, low_thre
 
 
 def predict_windows_vote(sd, model_type, audio, sample_rate, sample_duration, overlap_value,
-                         bin_thres, pad_clip_to=None):
-    """inference_prob_vote window loop (pytorch/main_strong.py:1058-1097):
-    binarised windows merged with utilities.merge, no avg_merge."""
-    audio_duration = len(audio) / float(sample_rate)
-    if pad_clip_to is not None:
-        audio = pad_truncate_sequence(audio, pad_clip_to)
+                         bin_thres, audio_duration=None):
+    """inference_prob_vote window loop (pytorch/main_strong.py:1052-1100): the
+    clip pad_truncate'd to 10 s, stride overlap_value, binarised windows
+    merged with utilities.merge, no avg_merge."""
+    if audio_duration is None:
+        audio_duration = len(audio) / float(sample_rate)
+    audio = pad_truncate_sequence(audio, sample_rate * 10)
     merged, prev = None, None
-    for num_segment, start in enumerate(window_starts(audio_duration, sample_duration,
-                                                      overlap_value), start=1):
+    for num_segment, start in enumerate(window_starts(audio_duration, sample_duration, overlap_value), start=1):
         s = int(start * sample_rate)
         seg = audio[s:int(sample_duration * sample_rate) + s]
-        if pad_clip_to is None:
-            seg = pad_truncate_sequence(seg, int(sample_rate * sample_duration))
         seg = torch.Tensor(np.asarray(seg))[None, :]
         curr = binarize_pred(forward(sd, model_type, wave=seg)['framewise_output'].numpy(), bin_thres)
         if num_segment == 1:

@@ -458,62 +458,103 @@ sedx_status run_body(sedx_handle* h, int64_t B, const Geometry& g, float* ws, co
   return launch_status(h);
 }
 
-// -------- window geometry (predict.py:297-338 / main_strong.py:791-832) --------
+// -------- windowed drivers (predict.py:297-349 / main_strong.py:786-835) --------
+// windows fed to the model as one batch: consecutive windows of one length
+// (every predict.py window; main_strong's full windows, then each window
+// that runs past the 10 s padded clip on its own)
+struct WinGroup {
+  int w0 = 0, nw = 0;
+  int64_t len = 0;
+  Geometry g{};
+};
 struct WinGeom {
+  WindowLoop loop;
   int n_win = 0;
-  int64_t win_samples = 0;
-  std::vector<int64_t> start;   // sample offset of every window (the device table repeats this sequence)
-  int64_t clip_len = 0;     // valid samples backing each clip
-  int step = 0, interval = 0, sd = 0;
-  int64_t Tw = 0, N = 0;
-  Geometry g;
+  int64_t full_len = 0;     // samples of a full window (sample_duration * sr)
+  int64_t clip_len = 0;     // samples backing each clip (beyond: pad_truncate zeros)
+  int64_t step = 0;         // int(100 * overlap_value)
+  int sd = 0;
+  std::vector<WinGroup> groups;
+  MergePlan plan;
 };
 
-sedx_status window_geometry(const sedx_handle* h, int64_t L_clip, float sample_duration,
-                            float overlap_value, int32_t pad_clip, WinGeom* wg) {
+sedx_status window_geometry(const sedx_handle* h, int64_t L_clip, const sedx_window_spec* spec, bool avg,
+                            WinGeom* wg) {
   sedx_handle* hm = const_cast<sedx_handle*>(h);
+  if (!spec) return fail(hm, SEDX_EINVAL, "null window spec");
   const int sr = h->cfg.sample_rate;
-  const double sd = sample_duration, ov = overlap_value;
-  if (!(sd > 0) || !(ov > 0) || sd != std::floor(sd))
-    return fail(hm, SEDX_EINVAL, "sample_duration must be a positive integer number of seconds"
-                                 " and overlap_value > 0");
-  if (L_clip <= 0) return fail(hm, SEDX_EINVAL, "empty clip");
-  const double duration = (double)L_clip / sr;
-  double start = 0.0, end = 0.0;
-  int n = 0;
-  wg->start.clear();
-  // unbounded like the reference's loop; the window count is limited only by
-  // the 32-bit item indexing of the launches (checked by the callers per batch)
-  while (end <= duration) {
-    if (n >= (1 << 24)) return fail(hm, SEDX_EINVAL, "too many windows per clip");
-    wg->start.push_back((int64_t)(start * sr));
-    ++n;
-    start += ov;
-    end = start + sd;
+  if (const char* why = window_loop(sr, L_clip, *spec, &wg->loop)) return fail(hm, SEDX_EINVAL, "%s", why);
+  // int(100 * overlap_value) in float64 (utilities.py:406, :426)
+  const double stepd = 100.0 * spec->overlap_value;
+  if (!(std::fabs(stepd) < 1e9)) return fail(hm, SEDX_EINVAL, "overlap_value out of range");
+  wg->step = (int64_t)stepd;
+  wg->sd = spec->sample_duration;
+  wg->n_win = (int)wg->loop.start.size();
+  wg->full_len = (int64_t)spec->sample_duration * sr;
+  wg->clip_len = spec->driver == SEDX_DRIVER_MAIN_STRONG ? std::min<int64_t>(L_clip, (int64_t)sr * 10) : L_clip;
+  wg->groups.clear();
+  std::vector<int64_t> frames(wg->n_win);
+  for (int w = 0; w < wg->n_win; ++w) {
+    const int64_t len = wg->loop.len[w];
+    // the model raises on these windows: STFT reflect padding needs more
+    // than n_fft/2 samples (stft.py:237), the third 2x2 pool one frame
+    // (models.py:139)
+    if (len <= h->cfg.window_size / 2)
+      return fail(hm, SEDX_EINVAL, "window %d has %lld samples: too short for the STFT's reflect padding", w,
+                  (long long)len);
+    if (wg->groups.empty() || wg->groups.back().len != len) {
+      WinGroup g;
+      g.w0 = w;
+      g.len = len;
+      g.g = geometry_from_T(h, conv_T(h, len));
+      if (g.g.T3 < 1) return fail(hm, SEDX_EINVAL, "window %d too short for the CNN", w);
+      wg->groups.push_back(g);
+    }
+    ++wg->groups.back().nw;
+    frames[w] = wg->groups.back().g.out_frames;
   }
-  wg->n_win = n;
-  wg->win_samples = (int64_t)(sd * sr);
-  if (pad_clip) {
-    const int64_t padded = (int64_t)sr * 10;
-    wg->clip_len = std::min<int64_t>(L_clip, padded);
-    for (int i = 0; i < n; ++i)
-      if (wg->start[i] + wg->win_samples > padded)
-        return fail(hm, SEDX_EINVAL, "window %d runs past the 10 s padded clip (reference feeds a "
-                                     "shorter window there)", i);
-  } else {
-    wg->clip_len = L_clip;
-  }
-  wg->g = geometry_from_T(h, conv_T(h, wg->win_samples));
-  wg->Tw = wg->g.out_frames;
-  wg->step = (int)(100 * ov);
-  wg->sd = (int)sd;
-  wg->interval = (int)(sd * 100) - wg->step;
-  if (wg->step <= 0 || wg->Tw < wg->step)
-    return fail(hm, SEDX_EINVAL, "overlap step %d frames incompatible with %lld-frame windows",
-                wg->step, (long long)wg->Tw);
-  wg->N = wg->Tw + (int64_t)(n - 1) * wg->step;
-  if (wg->g.T3 < 1) return fail(hm, SEDX_EINVAL, "window too short for the CNN");
+  if (const char* why = build_merge_plan(frames, wg->step, wg->sd, avg, &wg->plan))
+    return fail(hm, SEDX_EINVAL, "%s", why);
   return SEDX_OK;
+}
+
+// per-call device area after the model workspace: per-window framewise and
+// clipwise outputs, vote thresholds, then the tables (window starts, output
+// bases, merge plan), all at 256-B aligned float offsets
+struct WinLayout {
+  size_t model_bytes = 0;             // max over the groups' ws_layout
+  std::vector<size_t> fw_off, clip_off;   // per group, floats from the area start
+  size_t vthr = 0, tables = 0, table_bytes = 0, total_bytes = 0;
+  size_t t_start = 0, t_wb = 0, t_wcs = 0, t_off = 0, t_src = 0, t_div = 0;   // byte offsets in the tables
+};
+
+WinLayout win_layout(const sedx_handle* h, int64_t n_clips, const WinGeom& wg) {
+  WinLayout l;
+  const int64_t C = h->cfg.classes_num;
+  for (const auto& g : wg.groups) l.model_bytes = std::max(l.model_bytes, ws_layout(h, n_clips * g.nw, g.g).total_bytes);
+  size_t off = l.model_bytes / sizeof(float);
+  for (const auto& g : wg.groups) {
+    l.fw_off.push_back(off);
+    off += align_up((size_t)n_clips * g.nw * g.g.out_frames * C);
+  }
+  for (const auto& g : wg.groups) {
+    l.clip_off.push_back(off);
+    off += align_up((size_t)n_clips * g.nw * C);
+  }
+  l.vthr = off;
+  off += align_up(2 * (size_t)C);
+  l.tables = off;
+  auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+  size_t b = 0;
+  l.t_start = b; b += al(8 * (size_t)wg.n_win);
+  l.t_wb = b;    b += al(8 * (size_t)wg.n_win);
+  l.t_wcs = b;   b += al(8 * (size_t)wg.n_win);
+  l.t_off = b;   b += al(4 * ((size_t)wg.plan.N + 1));
+  l.t_src = b;   b += al(8 * wg.plan.src.size());
+  l.t_div = b;   b += al(4 * (size_t)wg.plan.N);
+  l.table_bytes = b;
+  l.total_bytes = off * sizeof(float) + b;
+  return l;
 }
 
 // the MFMA mel table (nullptr when the host did not build one)
@@ -1248,33 +1289,22 @@ sedx_status sedx_gamma_workspace_size(const sedx_handle* h, int64_t B, int64_t L
   return SEDX_OK;
 }
 
-sedx_status sedx_window_geometry(const sedx_handle* h, int64_t L_clip, float sample_duration,
-                                 float overlap_value, int32_t pad_clip, int64_t* n_windows,
-                                 int64_t* window_samples, int64_t* merged_frames) {
+sedx_status sedx_window_geometry(const sedx_handle* h, int64_t L_clip, const sedx_window_spec* spec,
+                                 int64_t* n_windows, int64_t* window_samples, int64_t* merged_frames) {
   if (!h) return SEDX_EINVAL;
   WinGeom wg;
-  sedx_status st = window_geometry(h, L_clip, sample_duration, overlap_value, pad_clip, &wg);
+  sedx_status st = window_geometry(h, L_clip, spec, false, &wg);
   if (st != SEDX_OK) return st;
   if (n_windows) *n_windows = wg.n_win;
-  if (window_samples) *window_samples = wg.win_samples;
-  if (merged_frames) *merged_frames = wg.N;
+  if (window_samples) *window_samples = wg.full_len;
+  if (merged_frames) *merged_frames = wg.plan.N;
   return SEDX_OK;
 }
 
-static size_t window_ws_bytes(const sedx_handle* h, int64_t n_clips, const WinGeom& wg) {
-  const int64_t items = n_clips * wg.n_win;
-  const WsLayout l = ws_layout(h, items, wg.g);
-  // + per-window framewise, clipwise, (vote mode) the f64 binarisation
-  // thresholds and the window table (int64 per window)
-  const size_t extra = (size_t)items * (wg.Tw * h->cfg.classes_num + h->cfg.classes_num) + 2 * h->cfg.classes_num +
-                       2 * (size_t)wg.n_win + 4 * 64;
-  return l.total_bytes + extra * sizeof(float);
-}
-
-// one batch of all windows of all clips, then the merge (avg or vote)
-static sedx_status forward_windows_impl(sedx_handle* h, const float* d_audio, int64_t n_clips,
-                                        int64_t L_clip, float sample_duration, float overlap_value,
-                                        int32_t pad_clip, const double* h_vote_thres, float* d_merged,
+// every window of every clip through the model (one batch per window group),
+// then the merge by the host's plan (avg or vote)
+static sedx_status forward_windows_impl(sedx_handle* h, const float* d_audio, int64_t n_clips, int64_t L_clip,
+                                        const sedx_window_spec* spec, const double* h_vote_thres, float* d_merged,
                                         void* d_workspace, size_t workspace_bytes, void* stream) {
   if (!h) return SEDX_EINVAL;
   if (!h->finalized) return fail(h, SEDX_ESTATE, "weights not finalised");
@@ -1283,84 +1313,120 @@ static sedx_status forward_windows_impl(sedx_handle* h, const float* d_audio, in
     return fail(h, SEDX_EINVAL, "windowed inference needs a logmel model");
   if (!d_audio || !d_merged || n_clips <= 0) return fail(h, SEDX_EINVAL, "null pointer or empty batch");
   WinGeom wg;
-  sedx_status st = window_geometry(h, L_clip, sample_duration, overlap_value, pad_clip, &wg);
+  sedx_status st = window_geometry(h, L_clip, spec, h_vote_thres == nullptr, &wg);
   if (st != SEDX_OK) return st;
-  if (wg.win_samples <= h->cfg.window_size / 2)
-    return fail(h, SEDX_EINVAL, "window too short for reflect padding");
   // the frontend and conv launches index items with 32-bit sizes (as forward_wave)
-  if (n_clips > INT32_MAX / wg.n_win || n_clips * wg.n_win * wg.g.T > INT32_MAX / 64)
-    return fail(h, SEDX_EINVAL, "batch too large: %lld clips x %d windows", (long long)n_clips, wg.n_win);
+  for (const auto& g : wg.groups)
+    if (n_clips > INT32_MAX / g.nw || n_clips * g.nw * g.g.T > INT32_MAX / 64)
+      return fail(h, SEDX_EINVAL, "batch too large: %lld clips x %d windows", (long long)n_clips, g.nw);
+  if (n_clips * wg.plan.N > INT32_MAX / h->cfg.classes_num)
+    return fail(h, SEDX_EINVAL, "merged output too large");
   DeviceGuard dg(h->device);
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const int64_t items = n_clips * wg.n_win;
-  const WsLayout l = ws_layout(h, items, wg.g);
+  const WinLayout wl = win_layout(h, n_clips, wg);
   float* ws = nullptr;
-  st = get_ws(h, window_ws_bytes(h, n_clips, wg), d_workspace, workspace_bytes, &ws);
+  st = get_ws(h, wl.total_bytes, d_workspace, workspace_bytes, &ws);
   if (st != SEDX_OK) return st;
   const int C = h->cfg.classes_num;
-  float* fw = ws + l.total_bytes / sizeof(float);
-  float* clip = fw + align_up((size_t)items * wg.Tw * C);
-  double* vthr = reinterpret_cast<double*>(clip + align_up((size_t)items * C));
-  int64_t* wstart = reinterpret_cast<int64_t*>(reinterpret_cast<float*>(vthr) + align_up(2 * (size_t)C));
-  launch_window_starts(wg.n_win, (double)overlap_value, h->cfg.sample_rate, wstart, s);
+  // tables: built on the host, one copy (the host vector is consumed by the
+  // call: pageable-source hipMemcpyAsync stages it before returning)
+  std::vector<char> blob(wl.table_bytes, 0);
+  int64_t* t_start = reinterpret_cast<int64_t*>(blob.data() + wl.t_start);
+  int64_t* t_wb = reinterpret_cast<int64_t*>(blob.data() + wl.t_wb);
+  int64_t* t_wcs = reinterpret_cast<int64_t*>(blob.data() + wl.t_wcs);
+  int32_t* t_off = reinterpret_cast<int32_t*>(blob.data() + wl.t_off);
+  int2* t_src = reinterpret_cast<int2*>(blob.data() + wl.t_src);
+  int32_t* t_div = reinterpret_cast<int32_t*>(blob.data() + wl.t_div);
+  std::copy(wg.loop.start.begin(), wg.loop.start.end(), t_start);
+  for (size_t gi = 0; gi < wg.groups.size(); ++gi) {
+    const WinGroup& g = wg.groups[gi];
+    for (int i = 0; i < g.nw; ++i) {
+      t_wb[g.w0 + i] = (int64_t)(wl.fw_off[gi] - wl.model_bytes / sizeof(float)) + (int64_t)i * g.g.out_frames * C;
+      t_wcs[g.w0 + i] = (int64_t)g.nw * g.g.out_frames * C;
+    }
+  }
+  std::copy(wg.plan.off.begin(), wg.plan.off.end(), t_off);
+  for (size_t j = 0; j < wg.plan.src.size(); ++j) {
+    const int32_t id = wg.plan.src[j];
+    const int w = (int)(std::upper_bound(wg.plan.win_base.begin(), wg.plan.win_base.end(), id) -
+                        wg.plan.win_base.begin()) - 1;
+    t_src[j] = make_int2(w, id - wg.plan.win_base[w]);
+  }
+  std::copy(wg.plan.div.begin(), wg.plan.div.end(), t_div);
+  char* d_tables = reinterpret_cast<char*>(ws + wl.tables);
+  HIP_TRY(h, hipMemcpyAsync(d_tables, blob.data(), blob.size(), hipMemcpyHostToDevice, s));
+  double* vthr = reinterpret_cast<double*>(ws + wl.vthr);
   if (h_vote_thres) HIP_TRY(h, hipMemcpyAsync(vthr, h_vote_thres, C * sizeof(double), hipMemcpyHostToDevice, s));
-  FrontendParams p{};
-  p.audio = d_audio;
-  p.clip_stride = L_clip;
-  p.n_clips = (int32_t)n_clips;
-  p.n_win = wg.n_win;
-  p.win_start = wstart;
-  p.clip_len = wg.clip_len;
-  p.sig_len = wg.win_samples;
-  p.T = (int32_t)wg.g.T;
-  p.hop = h->cfg.hop_size;
-  p.twiddle = h->w.twiddle;
-  p.window = h->w.window;
-  p.mel_w = h->w.mel_w;
-  p.mel_tab = h->w.mel_tab;
-  set_mel_mt(p, h->w, h->mel_mfma);
-  p.mel_wmax = h->w.mel_wmax;
-  p.mel_off = h->w.mel_off;
-  p.mel_lo = h->w.mel_lo;
-  p.bn_scale = h->w.bn0_scale;
-  p.bn_mean = h->w.bn0_mean;
-  p.bn_bias = h->w.bn0_bias;
-  p.out = ws + l.x0;
+  const int64_t* d_start = reinterpret_cast<const int64_t*>(d_tables + wl.t_start);
   mark(h, 0, s);
-  launch_logmel(p, h->cfg.window_size, s);
-  st = run_body(h, items, wg.g, ws, l, fw, clip, nullptr, s);
-  if (st != SEDX_OK) return st;
-  launch_merge(fw, (int)n_clips, wg.n_win, (int)wg.Tw, C, wg.step, (int)wg.N, wg.interval, wg.sd,
-               h_vote_thres ? vthr : nullptr, d_merged, s);
+  for (size_t gi = 0; gi < wg.groups.size(); ++gi) {
+    const WinGroup& g = wg.groups[gi];
+    const WsLayout l = ws_layout(h, n_clips * g.nw, g.g);
+    FrontendParams p{};
+    p.audio = d_audio;
+    p.clip_stride = L_clip;
+    p.n_clips = (int32_t)n_clips;
+    p.n_win = g.nw;
+    p.win_start = d_start + g.w0;
+    p.clip_len = wg.clip_len;
+    p.sig_len = g.len;
+    p.T = (int32_t)g.g.T;
+    p.hop = h->cfg.hop_size;
+    p.twiddle = h->w.twiddle;
+    p.window = h->w.window;
+    p.mel_w = h->w.mel_w;
+    p.mel_tab = h->w.mel_tab;
+    set_mel_mt(p, h->w, h->mel_mfma);
+    p.mel_wmax = h->w.mel_wmax;
+    p.mel_off = h->w.mel_off;
+    p.mel_lo = h->w.mel_lo;
+    p.bn_scale = h->w.bn0_scale;
+    p.bn_mean = h->w.bn0_mean;
+    p.bn_bias = h->w.bn0_bias;
+    p.out = ws + l.x0;
+    launch_logmel(p, h->cfg.window_size, s);
+    st = run_body(h, n_clips * g.nw, g.g, ws, l, ws + wl.fw_off[gi], ws + wl.clip_off[gi], nullptr, s);
+    if (st != SEDX_OK) return st;
+  }
+  MergeArgs a{};
+  a.fw = ws + wl.model_bytes / sizeof(float);
+  a.wb = reinterpret_cast<const int64_t*>(d_tables + wl.t_wb);
+  a.wcs = reinterpret_cast<const int64_t*>(d_tables + wl.t_wcs);
+  a.off = reinterpret_cast<const int32_t*>(d_tables + wl.t_off);
+  a.src = reinterpret_cast<const int2*>(d_tables + wl.t_src);
+  a.div = reinterpret_cast<const int32_t*>(d_tables + wl.t_div);
+  a.vote_thr = h_vote_thres ? vthr : nullptr;
+  a.n_clips = (int32_t)n_clips;
+  a.N = (int32_t)wg.plan.N;
+  a.C = C;
+  a.merged = d_merged;
+  launch_merge_plan(a, s);
   return launch_status(h);
 }
 
 sedx_status sedx_window_workspace_size(const sedx_handle* h, int64_t n_clips, int64_t L_clip,
-                                       float sample_duration, float overlap_value,
-                                       int32_t pad_clip, size_t* bytes) {
+                                       const sedx_window_spec* spec, size_t* bytes) {
   if (!h || !bytes || n_clips <= 0) return SEDX_EINVAL;
   WinGeom wg;
-  sedx_status st = window_geometry(h, L_clip, sample_duration, overlap_value, pad_clip, &wg);
+  sedx_status st = window_geometry(h, L_clip, spec, false, &wg);
   if (st != SEDX_OK) return st;
-  *bytes = window_ws_bytes(h, n_clips, wg);
+  *bytes = win_layout(h, n_clips, wg).total_bytes;
   return SEDX_OK;
 }
 
-sedx_status sedx_forward_windows(sedx_handle* h, const float* d_audio, int64_t n_clips,
-                                 int64_t L_clip, float sample_duration, float overlap_value,
-                                 int32_t pad_clip, float* d_merged, void* d_workspace,
+sedx_status sedx_forward_windows(sedx_handle* h, const float* d_audio, int64_t n_clips, int64_t L_clip,
+                                 const sedx_window_spec* spec, float* d_merged, void* d_workspace,
                                  size_t workspace_bytes, void* stream) {
-  return forward_windows_impl(h, d_audio, n_clips, L_clip, sample_duration, overlap_value, pad_clip,
-                              nullptr, d_merged, d_workspace, workspace_bytes, stream);
+  return forward_windows_impl(h, d_audio, n_clips, L_clip, spec, nullptr, d_merged, d_workspace, workspace_bytes,
+                              stream);
 }
 
-sedx_status sedx_forward_windows_vote(sedx_handle* h, const float* d_audio, int64_t n_clips,
-                                      int64_t L_clip, float sample_duration, float overlap_value,
-                                      int32_t pad_clip, const double* bin_thres, float* d_votes,
+sedx_status sedx_forward_windows_vote(sedx_handle* h, const float* d_audio, int64_t n_clips, int64_t L_clip,
+                                      const sedx_window_spec* spec, const double* bin_thres, float* d_votes,
                                       void* d_workspace, size_t workspace_bytes, void* stream) {
   if (!bin_thres) return fail(h, SEDX_EINVAL, "vote mode needs the per-class binarisation thresholds");
-  return forward_windows_impl(h, d_audio, n_clips, L_clip, sample_duration, overlap_value, pad_clip,
-                              bin_thres, d_votes, d_workspace, workspace_bytes, stream);
+  return forward_windows_impl(h, d_audio, n_clips, L_clip, spec, bin_thres, d_votes, d_workspace, workspace_bytes,
+                              stream);
 }
 
 sedx_status sedx_events_workspace_size(int64_t n_clips, int64_t T, int64_t C, size_t* bytes) {
@@ -1372,15 +1438,19 @@ sedx_status sedx_events_workspace_size(int64_t n_clips, int64_t T, int64_t C, si
 sedx_status sedx_events_device(const float* d_x, int64_t n_clips, int64_t T, int64_t C,
                                const double* high_thres, const double* low_thres,
                                int32_t use_low_thres, const int64_t* n_smooth, const int64_t* n_salt,
-                               int32_t mode, float overlap_value, int32_t sample_duration,
+                               int32_t mode, double overlap_value, int32_t sample_duration,
                                int32_t* d_events, int64_t capacity, int64_t* d_info,
                                void* d_workspace, size_t workspace_bytes, void* stream) {
   if (n_clips < 0 || T < 0 || C <= 0 || !d_info || !n_smooth || !n_salt || (mode != 0 && mode != 1) ||
       (n_clips > 0 && !d_x) || (capacity > 0 && !d_events) || capacity < 0 ||
       (use_low_thres && !low_thres) || (mode == 0 && !high_thres))
     return SEDX_EINVAL;
-  const int64_t step = (int64_t)(100 * (double)overlap_value);
-  if (mode == 1 && (step <= 0 || sample_duration <= 0)) return SEDX_EINVAL;
+  // int(100 * overlap_value) in float64 (vad.py:63)
+  if (mode == 1 && !(std::fabs(100.0 * overlap_value) < 1e9)) return SEDX_EINVAL;
+  const int64_t step = mode == 1 ? (int64_t)(100.0 * overlap_value) : 0;
+  // step 0: range(0, N - 0, 0) raises; step < 0: the range is empty, no
+  // frame is ever a candidate and the reference returns no events
+  if (mode == 1 && (step == 0 || sample_duration <= 0)) return SEDX_EINVAL;
   if (T > events_max_frames()) return SEDX_EINVAL;   // a series' two bitmaps live in LDS
   const size_t need = events_workspace_bytes(n_clips * C, T, C);
   if (!d_workspace || workspace_bytes < need) return SEDX_EINVAL;

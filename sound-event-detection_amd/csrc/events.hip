@@ -163,7 +163,8 @@ __global__ __launch_bounds__(64 * EV_WAVES) void events_series_kernel(EventArgs 
   const bool use_lo = a.use_lo != 0;
   // mode 1: scan limit and per-block vote requirement (vad.py:62-78)
   const int64_t step = a.step, sd = a.sd, interval = sd * 100 - step;
-  const int64_t lim = MODE == 0 ? T : ((T - step > 0) ? ((T - step + step - 1) / step) * step : 0);
+  // (step < 0: range(0, T - step, step) is empty, no candidate frame)
+  const int64_t lim = MODE == 0 ? T : ((step > 0 && T - step > 0) ? ((T - step + step - 1) / step) * step : 0);
 
   // pass 1: bitmaps, 8 words (512 frames) of loads in flight per lane
   for (int64_t w0 = 0; w0 < W; w0 += 8) {
@@ -181,8 +182,9 @@ __global__ __launch_bounds__(64 * EV_WAVES) void events_series_kernel(EventArgs 
       if (MODE == 0) {
         on = t < T && v[j] > hi;                    // float32 compare (numpy f32 row vs python float)
       } else {
-        const int64_t i = (t / step) * step;
-        const int64_t nov = i < interval ? i / step + 1 : (i >= T - interval ? (T - i) / step + 1 : sd);
+        const int64_t st = step > 0 ? step : 1;
+        const int64_t i = (t / st) * st;
+        const int64_t nov = i < interval ? i / st + 1 : (i >= T - interval ? (T - i) / st + 1 : sd);
         on = t < lim && (double)v[j] >= (double)nov;
       }
       const bool below = t < T && (MODE == 0 ? (v[j] < lo_f) : ((double)v[j] < lo));

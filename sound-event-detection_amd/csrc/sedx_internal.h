@@ -17,6 +17,8 @@
 #include <utility>
 #include <vector>
 
+#include "../../include/sedx.h"
+
 namespace sedx {
 
 // ---- frontend -------------------------------------------------------------
@@ -279,19 +281,45 @@ void launch_att_head(const float* logits, int B, int T, int C, int ldl, int out_
 // embedding for the Transformer model: E [B][T][D] -> emb [B][D][T]
 void launch_transpose_btd(const float* E, int B, int T, int D, float* out, hipStream_t s);
 
-// window overlap-add + avg_merge schedule.  fw [n_clips*n_win][Tw][C] ->
-// merged [n_clips][N][C]; step = int(100*overlap) frames, interval =
-// sample_duration*100 - step, sd = sample_duration (utilities.py:425-446).
-// vote_thr != nullptr (device, [C] f64): inference_prob_vote merge instead —
-// every window binarised (x > thr[k], pytorch/main_strong.py:870-883) and
-// summed, no avg_merge division (main_strong.py:1082-1097).
-void launch_merge(const float* fw, int n_clips, int n_win, int Tw, int C, int step, int N,
-                  int interval, int sd, const double* vote_thr, float* merged, hipStream_t s);
-// window sample offsets of predict.py's loop (:297-338): start = 0, then
-// start += overlap_value in float64, offset = int(start * sr) — the host's
-// sequence (api.cpp window_geometry), recomputed on the device so the table
-// of any length needs no host buffer that outlives the call
-void launch_window_starts(int n_win, double overlap_value, int sample_rate, int64_t* starts, hipStream_t s);
+// ---- windowed drivers (windows.cpp) ---------------------------------------
+// loop control of predict.py:297-338 / main_strong.py:786-832: the sample
+// offset of every window and the samples fed to the model for it
+struct WindowLoop {
+  std::vector<int64_t> start, len;
+};
+// nullptr on success, else why the reference's loop raises / never ends
+const char* window_loop(int sample_rate, int64_t L_clip, const sedx_window_spec& sp, WindowLoop* out);
+// utilities.merge replayed window by window on index lists, then avg_merge's
+// divisors: merged frame f = left fold, in order, of the values with packed
+// ids src[off[f] .. off[f+1]) (window w, frame t -> win_base[w] + t), divided
+// by div[f] when div[f] > 1.
+struct MergePlan {
+  int64_t N = 0;
+  std::vector<int32_t> win_base;   // [n_win + 1]
+  std::vector<int32_t> off;        // [N + 1]
+  std::vector<int32_t> src;
+  std::vector<int32_t> div;        // [N]
+};
+const char* build_merge_plan(const std::vector<int64_t>& frames, int64_t step, int sample_duration, bool avg,
+                             MergePlan* plan);
+// GPU merge of every clip by one plan.  Window w of clip c has its framewise
+// output at fw + wb[w] + c * wcs[w] (floats, frames of C classes); the plan's
+// tables (off, src as (window, frame) int2, div) live in device memory.
+// vote_thr != nullptr (device, [C] f64): every value binarised first (x >
+// thr[k] in float64, pytorch/main_strong.py:870-883); the plan then carries
+// no divisors (main_strong.py:1097 skips avg_merge).
+struct MergeArgs {
+  const float* fw;
+  const int64_t* wb;      // [n_win] float offset of window w's clip-0 output
+  const int64_t* wcs;     // [n_win] floats between clips for window w
+  const int32_t* off;     // [N + 1]
+  const int2* src;        // (window, frame)
+  const int32_t* div;     // [N]
+  const double* vote_thr;
+  int32_t n_clips, N, C;
+  float* merged;          // [n_clips][N][C]
+};
+void launch_merge_plan(const MergeArgs& a, hipStream_t s);
 
 // ---- events (events.hip) --------------------------------------------------
 struct EventArgs {

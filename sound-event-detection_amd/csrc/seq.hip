@@ -9,7 +9,7 @@
 //   att_head_kernel AttBlock finish (clamp, exp, normalise over T, sigmoid,
 //                   weighted sum) + x8 frame repeat + GRU last-frame padding
 //                   (pytorch/models.py:161-175, :84-95, :65-81)
-//   merge_kernel    overlap-add of window predictions + avg_merge divisors
+//   merge_plan_kernel  overlap-add of window predictions + avg_merge divisors (host plan)
 //                   (utils/utilities.py:405-446)
 #include "sedx_internal.h"
 
@@ -441,73 +441,39 @@ void launch_transpose_btd(const float* E, int B, int T, int D, float* out, hipSt
 }
 
 // ---------------------------------------------------------------------------
-// merge: merged[c][f][k] = (sum_w fw[c,w][f - w*step][k]) / div[f], summed in
-// window order exactly like the reference's incremental merge().
+// merge (utilities.py:405-446) by the host's plan (windows.cpp
+// build_merge_plan): merged[c][f][k] = left fold, in the plan's order, of the
+// window values numpy added into frame f, then / div[f].  One thread per
+// (clip, frame, class); a frame reads O(sample_duration / step) values.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void merge_kernel(const float* __restrict__ fw, int n_clips,
-                                                    int n_win, int Tw, int C, int step, int N,
-                                                    int interval, int sd,
-                                                    const double* __restrict__ vote_thr,
-                                                    float* __restrict__ merged) {
-  const int64_t total = (int64_t)n_clips * N * C;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * 256) {
-    const int k = (int)(i % C);
-    const int64_t cf = i / C;
-    const int f = (int)(cf % N);
-    const int64_t c = cf / N;
+__global__ __launch_bounds__(256) void merge_plan_kernel(MergeArgs a) {
+  const int64_t total = (int64_t)a.n_clips * a.N * a.C;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int k = (int)(i % a.C);
+    const int64_t cf = i / a.C;
+    const int f = (int)(cf % a.N);
+    const int64_t c = cf / a.N;
     float s = 0.f;
-    bool first = true;
-    // windows covering frame f: w * step <= f < w * step + Tw, ascending
-    // (the incremental merge's addition order); O(Tw / step) per frame for any
-    // number of windows
-    const int w_lo = f >= Tw ? (f - Tw) / step + 1 : 0;
-    const int w_hi = min(n_win - 1, f / step);
-    for (int w = w_lo; w <= w_hi; ++w) {
-      const int lf = f - w * step;
-      float v = fw[((c * n_win + w) * Tw + lf) * C + k];
-      // binarize_pred: float64 0/1 (the comparison of a float32 element with
-      // a float64 threshold is made in float64); sums of 0/1 are exact in f32
-      if (vote_thr) v = ((double)v > vote_thr[k]) ? 1.0f : 0.0f;
-      s = first ? v : s + v;
-      first = false;
+    const int j0 = a.off[f], j1 = a.off[f + 1];
+    for (int j = j0; j < j1; ++j) {
+      const int2 e = a.src[j];
+      float v = a.fw[a.wb[e.x] + c * a.wcs[e.x] + (int64_t)e.y * a.C + k];
+      // binarize_pred: float64 0/1 (a float32 element compared with a float64
+      // threshold is compared in float64); sums of 0/1 are exact in f32
+      if (a.vote_thr) v = ((double)v > a.vote_thr[k]) ? 1.0f : 0.0f;
+      s = j == j0 ? v : s + v;                 // prev_overlap + curr_overlap, window order
     }
-    if (vote_thr) {      // inference_prob_vote: no avg_merge (main_strong.py:1097)
-      merged[i] = s;
-      continue;
-    }
-    // avg_merge: blocks [i, i+step) for i in range(step, N-step, step)
-    const int blk = (f / step) * step;
-    int d = 1;
-    if (blk >= step && blk < N - step) {
-      if (blk < interval) d = blk / step + 1;
-      else if (blk >= N - interval) d = (N - blk) / step + 1;
-      else d = sd;
-    }
-    merged[i] = d > 1 ? s / (float)d : s;
+    const int d = a.div[f];
+    a.merged[i] = d > 1 ? s / (float)d : s;    // float32 /= int (utilities.py:435)
   }
 }
 
-__global__ void window_starts_kernel(int n_win, double ov, int sr, int64_t* __restrict__ starts) {
-  if (blockIdx.x != 0 || threadIdx.x != 0) return;
-  double start = 0.0;                 // predict.py:281, :302, :335-336 (float64 running sum)
-  for (int w = 0; w < n_win; ++w) {
-    starts[w] = (int64_t)(start * (double)sr);
-    start += ov;
-  }
-}
-
-void launch_window_starts(int n_win, double overlap_value, int sample_rate, int64_t* starts, hipStream_t s) {
-  hipLaunchKernelGGL(window_starts_kernel, dim3(1), dim3(64), 0, s, n_win, overlap_value, sample_rate, starts);
-}
-
-void launch_merge(const float* fw, int n_clips, int n_win, int Tw, int C, int step, int N,
-                  int interval, int sd, const double* vote_thr, float* merged, hipStream_t s) {
-  const int64_t total = (int64_t)n_clips * N * C;
+void launch_merge_plan(const MergeArgs& a, hipStream_t s) {
+  const int64_t total = (int64_t)a.n_clips * a.N * a.C;
+  if (total <= 0) return;
   int64_t blocks = (total + 255) / 256;
   if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(merge_kernel, dim3(blocks), dim3(256), 0, s, fw, n_clips, n_win, Tw, C, step,
-                     N, interval, sd, vote_thr, merged);
+  hipLaunchKernelGGL(merge_plan_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a);
 }
 
 }  // namespace sedx

@@ -23,7 +23,7 @@ EXPORTS = ['sedx_create', 'sedx_destroy', 'sedx_last_error', 'sedx_version', 'se
            'sedx_forward_windows_vote', 'sedx_events_workspace_size', 'sedx_events_device',
            'sedx_forward_i16', 'sedx_wav_parse', 'sedx_wav_decode_mono', 'sedx_resample_size',
            'sedx_resample_workspace_size', 'sedx_resample', 'sedx_gamma_workspace_size',
-           'sedx_set_tuning', 'sedx_set_capture']
+           'sedx_set_tuning', 'sedx_set_capture', 'sedx_window_starts', 'sedx_merge_host']
 TUNE_GRU_KERNEL, TUNE_GRU_HANDOFF, TUNE_WINO_BLOCK1, TUNE_MEL_MFMA = 0, 1, 2, 3
 PRECISION = {'exact': 0, 'x3': 1, 'winograd': 2}
 STAGES = ['frontend', 'b1c1', 'b1c2', 'b2c1', 'b2c2', 'b3c1', 'b3c2', 'b4c1', 'b4c2', 'seq', 'head']
@@ -37,6 +37,24 @@ class SedxWavInfo(ctypes.Structure):
 
 
 RESAMPLE = {'kaiser_best': 0, 'kaiser_fast': 1}
+
+DRIVER = {'predict': 0, 'main_strong': 1}
+
+
+class SedxWindowSpec(ctypes.Structure):
+    _fields_ = [('driver', ctypes.c_int32), ('overlap', ctypes.c_int32),
+                ('sample_duration', ctypes.c_int32), ('reserved', ctypes.c_int32),
+                ('overlap_value', ctypes.c_double), ('audio_duration', ctypes.c_double)]
+
+
+def window_spec(sample_duration, overlap_value, driver='predict', overlap=True, audio_duration=None):
+    """sedx_window_spec of one windowed-driver call (include/sedx.h)."""
+    if driver not in DRIVER:
+        raise ValueError('driver must be one of %s' % sorted(DRIVER))
+    if int(sample_duration) != sample_duration:
+        raise ValueError('sample_duration is an int number of seconds in the reference (predict.py:701)')
+    return SedxWindowSpec(DRIVER[driver], int(bool(overlap)), int(sample_duration), 0, float(overlap_value),
+                          float(audio_duration) if audio_duration is not None else 0.0)
 
 
 class SedxConfig(ctypes.Structure):
@@ -53,9 +71,11 @@ P = ctypes.c_void_p
 I64 = ctypes.c_int64
 I32 = ctypes.c_int32
 F32 = ctypes.c_float
+F64 = ctypes.c_double
 SZ = ctypes.c_size_t
 PI64 = ctypes.POINTER(ctypes.c_int64)
 PSZ = ctypes.POINTER(ctypes.c_size_t)
+PSPEC = ctypes.POINTER(SedxWindowSpec)
 
 
 def lib():
@@ -83,13 +103,15 @@ def lib():
         'sedx_gamma_workspace_size': ([P, I64, I64, PSZ], I32),
         'sedx_set_tuning': ([P, I32, I32], I32),
         'sedx_set_capture': ([P, I32, P, SZ], I32),
-        'sedx_window_geometry': ([P, I64, F32, F32, I32, PI64, PI64, PI64], I32),
-        'sedx_forward_windows': ([P, P, I64, I64, F32, F32, I32, P, P, SZ, P], I32),
-        'sedx_window_workspace_size': ([P, I64, I64, F32, F32, I32, PSZ], I32),
+        'sedx_window_starts': ([I32, I64, PSPEC, P, P, I64, PI64], I32),
+        'sedx_merge_host': ([P, P, I64, I64, I32, F64, I32, P, I64, PI64], I32),
+        'sedx_window_geometry': ([P, I64, PSPEC, PI64, PI64, PI64], I32),
+        'sedx_forward_windows': ([P, P, I64, I64, PSPEC, P, P, SZ, P], I32),
+        'sedx_window_workspace_size': ([P, I64, I64, PSPEC, PSZ], I32),
         'sedx_events': ([P, I64, I64, I64, P, P, I32, P, P, P, I64, PI64], I32),
-        'sedx_forward_windows_vote': ([P, P, I64, I64, F32, F32, I32, P, P, P, SZ, P], I32),
+        'sedx_forward_windows_vote': ([P, P, I64, I64, PSPEC, P, P, P, SZ, P], I32),
         'sedx_events_workspace_size': ([I64, I64, I64, PSZ], I32),
-        'sedx_events_device': ([P, I64, I64, I64, P, P, I32, P, P, I32, F32, I32, P, I64, P, P, SZ, P],
+        'sedx_events_device': ([P, I64, I64, I64, P, P, I32, P, P, I32, F64, I32, P, I64, P, P, SZ, P],
                                I32),
         'sedx_set_profiling': ([P, I32], I32),
         'sedx_set_precision': ([P, I32], I32),

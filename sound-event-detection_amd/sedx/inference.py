@@ -2,10 +2,15 @@
 inference (main_strong.py inference_prob), gammatone features and event
 extraction.  All compute goes through libsedx.
 
- - predict_windows   pytorch/predict.py:297-349 (pad_clip=False) and
-                     pytorch/main_strong.py:790-833 (pad_clip=True): every
-                     window of every clip in ONE native batch, GPU overlap-add
-                     + avg_merge divisor schedule (utils/utilities.py:405-446).
+ - predict_windows   pytorch/predict.py:297-349 (driver='predict': stride
+                     1 s with --overlap, else sample_duration) and
+                     pytorch/main_strong.py:786-835 (driver='main_strong':
+                     clip padded to 10 s, stride overlap_value): every window
+                     of every clip in ONE native batch, GPU merge at
+                     int(100 * overlap_value) frames + the avg_merge divisor
+                     schedule (utils/utilities.py:405-446).
+ - window_starts / merge_host   the same loop control and merge on the host
+                     (no GPU), for checks and host-side callers.
  - predict_windows_vote   inference_prob_vote (pytorch/main_strong.py:1058-1097):
                      binarised windows overlap-added on the GPU.
  - events_from_framewise   frame_prediction_to_event_prediction_v2
@@ -45,17 +50,58 @@ def _ptr(t):
     return ctypes.c_void_p(t.data_ptr())
 
 
-def window_geometry(model, clip_samples, sample_duration=5, overlap_value=1, pad_clip=False):
+def window_geometry(model, clip_samples, sample_duration=5, overlap_value=1.0, driver='predict', overlap=True,
+                    audio_duration=None):
+    """(windows per clip, samples per full window, merged frames) of one
+    windowed-driver call (sedx_window_geometry)."""
     nat = model.native(torch.device('cuda', torch.cuda.current_device()))
+    spec = _lib.window_spec(sample_duration, overlap_value, driver, overlap, audio_duration)
     nw, ws, nf = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
-    _lib.check(_lib.lib().sedx_window_geometry(nat.h, int(clip_samples), float(sample_duration),
-                                               float(overlap_value), int(bool(pad_clip)),
-                                               ctypes.byref(nw), ctypes.byref(ws), ctypes.byref(nf)),
-               nat.h, 'window_geometry')
+    _lib.check(_lib.lib().sedx_window_geometry(nat.h, int(clip_samples), ctypes.byref(spec), ctypes.byref(nw),
+                                               ctypes.byref(ws), ctypes.byref(nf)), nat.h, 'window_geometry')
     return nw.value, ws.value, nf.value
 
 
-def _windows(model, audio, sample_duration, overlap_value, pad_clip, vote_thres):
+def window_starts(sample_rate, clip_samples, sample_duration=5, overlap_value=1.0, driver='predict', overlap=True,
+                  audio_duration=None):
+    """The window loop of predict.py:297-338 / main_strong.py:786-832 on the
+    host (sedx_window_starts, no GPU): ([sample offset], [samples fed to the
+    model]) per window."""
+    spec = _lib.window_spec(sample_duration, overlap_value, driver, overlap, audio_duration)
+    L = _lib.lib()
+    n = ctypes.c_int64()
+    _lib.check(L.sedx_window_starts(int(sample_rate), int(clip_samples), ctypes.byref(spec), None, None, 0,
+                                    ctypes.byref(n)), None, 'window_starts')
+    st = np.zeros(max(n.value, 1), np.int64)
+    ln = np.zeros(max(n.value, 1), np.int64)
+    _lib.check(L.sedx_window_starts(int(sample_rate), int(clip_samples), ctypes.byref(spec),
+                                    st.ctypes.data_as(ctypes.c_void_p), ln.ctypes.data_as(ctypes.c_void_p),
+                                    n.value, ctypes.byref(n)), None, 'window_starts')
+    return st[:n.value].tolist(), ln[:n.value].tolist()
+
+
+def merge_host(windows, sample_duration, overlap_value=1.0, avg=True):
+    """utilities.merge over the windows in order, then avg_merge (avg=True),
+    on the host (sedx_merge_host): windows = list of [T_w, C] (or [1, T_w, C])
+    float32 arrays.  Returns [1, N, C] float32, as the reference's merged."""
+    ws = [np.ascontiguousarray(np.asarray(w, np.float32).reshape(-1, np.asarray(w).shape[-1])) for w in windows]
+    C = ws[0].shape[1]
+    frames = np.asarray([w.shape[0] for w in ws], np.int64)
+    cat = np.ascontiguousarray(np.concatenate(ws, axis=0)) if len(ws) > 1 else ws[0]
+    L = _lib.lib()
+    n = ctypes.c_int64()
+    st = L.sedx_merge_host(cat.ctypes.data_as(ctypes.c_void_p), frames.ctypes.data_as(ctypes.c_void_p), len(ws), C,
+                           int(sample_duration), float(overlap_value), int(bool(avg)), None, 0, ctypes.byref(n))
+    if st != _lib.SEDX_OK:
+        raise ValueError('sedx_merge_host: the reference raises here (numpy broadcast / zero range step)')
+    out = np.zeros((max(n.value, 0), C), np.float32)
+    _lib.check(L.sedx_merge_host(cat.ctypes.data_as(ctypes.c_void_p), frames.ctypes.data_as(ctypes.c_void_p),
+                                 len(ws), C, int(sample_duration), float(overlap_value), int(bool(avg)),
+                                 out.ctypes.data_as(ctypes.c_void_p), n.value, ctypes.byref(n)), None, 'merge_host')
+    return out[None]
+
+
+def _windows(model, audio, spec, vote_thres):
     if model.training:
         raise RuntimeError('call model.eval() first')
     if audio.device.type != 'cuda':
@@ -67,41 +113,52 @@ def _windows(model, audio, sample_duration, overlap_value, pad_clip, vote_thres)
     L = _lib.lib()
     n_clips, clip_len = x.shape
     nw, wsamp, nf = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
-    _lib.check(L.sedx_window_geometry(nat.h, clip_len, float(sample_duration), float(overlap_value),
-                                      int(bool(pad_clip)), ctypes.byref(nw), ctypes.byref(wsamp),
+    _lib.check(L.sedx_window_geometry(nat.h, clip_len, ctypes.byref(spec), ctypes.byref(nw), ctypes.byref(wsamp),
                                       ctypes.byref(nf)), nat.h, 'window_geometry')
     wsz = ctypes.c_size_t()
-    _lib.check(L.sedx_window_workspace_size(nat.h, n_clips, clip_len, float(sample_duration),
-                                            float(overlap_value), int(bool(pad_clip)),
-                                            ctypes.byref(wsz)), nat.h, 'window_workspace_size')
+    _lib.check(L.sedx_window_workspace_size(nat.h, n_clips, clip_len, ctypes.byref(spec), ctypes.byref(wsz)),
+               nat.h, 'window_workspace_size')
     ws = torch.empty(wsz.value, dtype=torch.uint8, device=x.device)
     merged = torch.empty((n_clips, nf.value, model.classes_num), dtype=torch.float32, device=x.device)
     stream = ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
     if vote_thres is None:
-        _lib.check(L.sedx_forward_windows(nat.h, _ptr(x), n_clips, clip_len, float(sample_duration),
-                                          float(overlap_value), int(bool(pad_clip)), _ptr(merged),
+        _lib.check(L.sedx_forward_windows(nat.h, _ptr(x), n_clips, clip_len, ctypes.byref(spec), _ptr(merged),
                                           _ptr(ws), wsz.value, stream), nat.h, 'forward_windows')
     else:
         thr = np.ascontiguousarray(_as_list(vote_thres, model.classes_num), dtype=np.float64)
-        _lib.check(L.sedx_forward_windows_vote(nat.h, _ptr(x), n_clips, clip_len, float(sample_duration),
-                                               float(overlap_value), int(bool(pad_clip)),
+        _lib.check(L.sedx_forward_windows_vote(nat.h, _ptr(x), n_clips, clip_len, ctypes.byref(spec),
                                                thr.ctypes.data_as(ctypes.c_void_p), _ptr(merged),
                                                _ptr(ws), wsz.value, stream), nat.h, 'forward_windows_vote')
     return merged
 
 
-def predict_windows(model, audio, sample_duration=5, overlap_value=1, pad_clip=False):
-    """audio: [n_clips, L] (HIP tensor, every clip L samples long).  Returns the
-    merged + averaged framewise predictions [n_clips, N, classes]."""
-    return _windows(model, audio, sample_duration, overlap_value, pad_clip, None)
+def predict_windows(model, audio, sample_duration=5, overlap_value=1.0, overlap=True, driver='predict',
+                    audio_duration=None):
+    """Windowed inference of every clip of audio [n_clips, L] (HIP tensor, every
+    clip L samples long) as ONE native batch; returns the merged + averaged
+    framewise predictions [n_clips, N, classes].
+
+    driver='predict'      pytorch/predict.py:297-349 with its arguments
+                          (--sample_duration, --overlap, --overlap_value;
+                          run.sh passes 5 / --overlap / 1): stride 1 s with
+                          overlap, else sample_duration s; every window
+                          pad_truncate'd; merged at int(100 * overlap_value)
+                          frames.
+    driver='main_strong'  inference_prob_overlap (main_strong.py:786-835):
+                          clip pad_truncate'd to 10 s, stride overlap_value s.
+    audio_duration        the loop bound (librosa.get_duration of the file);
+                          default L / sample_rate."""
+    spec = _lib.window_spec(sample_duration, overlap_value, driver, overlap, audio_duration)
+    return _windows(model, audio, spec, None)
 
 
-def predict_windows_vote(model, audio, sample_duration, overlap_value, bin_threshold, pad_clip=True):
-    """inference_prob_vote window loop (pytorch/main_strong.py:1058-1097): every
+def predict_windows_vote(model, audio, sample_duration, overlap_value, bin_threshold, audio_duration=None):
+    """inference_prob_vote window loop (pytorch/main_strong.py:1052-1100): every
     window binarised with ``bin_threshold`` (the reference passes
     sed_low_threshold, :1082) and overlap-added without averaging.  Returns
     the vote counts [n_clips, N, classes] (float32, exact integers)."""
-    return _windows(model, audio, sample_duration, overlap_value, pad_clip, bin_threshold)
+    spec = _lib.window_spec(sample_duration, overlap_value, 'main_strong', True, audio_duration)
+    return _windows(model, audio, spec, bin_threshold)
 
 
 def gamma_features(model, audio):
@@ -257,10 +314,10 @@ def sweep_overlap(model, audio, audio_names, params, combos=OVERLAP_SWEEP, vote=
     out = {}
     for ov, sd in combos:
         if vote:
-            votes = predict_windows_vote(model, audio, sd, ov, params['sed_low_threshold'], pad_clip=True)
+            votes = predict_windows_vote(model, audio, sd, ov, params['sed_low_threshold'])
             out[(ov, sd)] = events_from_votes(votes, ov, sd, params, list(audio_names))
         else:
-            merged = predict_windows(model, audio, sd, ov, pad_clip=True)
+            merged = predict_windows(model, audio, sd, ov, driver='main_strong')
             out[(ov, sd)] = events_from_framewise(merged, params, list(audio_names), sort=False)
     return out
 

@@ -284,11 +284,11 @@ def test_windowed_and_events(model, golden_dir):
     g = np.load(os.path.join(golden_dir, 'windowed_%s.npz' % mt))
     ev = json.load(open(os.path.join(golden_dir, 'events.json')))
     audio = torch.from_numpy(synth.make_waveforms(2, seconds=10.0, sample_rate=16000, seed=1234)[:1]).cuda()
-    merged = inference.predict_windows(m, audio, 5, 1, pad_clip=False).cpu().numpy()
+    merged = inference.predict_windows(m, audio, 5, 1.0, overlap=True, driver='predict').cpu().numpy()
     e = err(merged, g['merged_5_1'])
     print(mt, 'windowed 5/1 max|d| =', e)
     assert e <= TOL
-    merged_ms = inference.predict_windows(m, audio, 6, 0.5, pad_clip=True).cpu().numpy()
+    merged_ms = inference.predict_windows(m, audio, 6, 0.5, driver='main_strong').cpu().numpy()
     assert err(merged_ms, g['merged_6_05']) <= TOL
     for which in ('default', 'synthetic'):
         params = ev['params_' + which]
@@ -304,9 +304,10 @@ def test_windowed_and_events(model, golden_dir):
 @pytest.mark.parametrize('case', ['5_1', '6_05'])
 def test_long_file_windowed(model, golden_dir, case):
     """predict.py over a whole long file (183 windows of 5 s at 1 s stride over
-    187.37 s; 131 windows of 6 s at 0.5 s over 71.3 s): every window in one
-    native batch, the merge + avg_merge of any window count, and the events,
-    against goldens the reference produced (oracle/make_golden_long.py)."""
+    187.37 s; 66 windows of 6 s at 1 s stride merged 50 frames apart
+    (--overlap_value 0.5) over 71.3 s): every window in one native batch, the
+    merge + avg_merge of any window count, and the events, against goldens
+    the reference produced (oracle/make_golden_long.py)."""
     from sedx import inference
     mt, m = model
     ev = json.load(open(os.path.join(golden_dir, 'long_events.json')))
@@ -314,11 +315,13 @@ def test_long_file_windowed(model, golden_dir, case):
     g = np.load(os.path.join(golden_dir, 'long_%s.npz' % case))[mt]
     audio = synth.make_waveforms(1, seconds=c['samples'] / 16000., sample_rate=16000, seed=c['seed'])
     assert audio.shape[1] == c['samples']
-    nw, _, nf = inference.window_geometry(m, c['samples'], c['sample_duration'], c['overlap_value'])
-    assert nw == len(O.window_starts(c['samples'] / 16000., c['sample_duration'], c['overlap_value'])) > 64
+    nw, _, nf = inference.window_geometry(m, c['samples'], c['sample_duration'], c['overlap_value'],
+                                          c['driver'], c['overlap'])
+    stride = O.driver_stride(c['driver'], c['sample_duration'], c['overlap_value'], c['overlap'])
+    assert nw == len(O.window_starts(c['samples'] / 16000., c['sample_duration'], stride)) > 64
     assert nf == g.shape[1]
     merged = inference.predict_windows(m, torch.from_numpy(audio).cuda(), c['sample_duration'],
-                                       c['overlap_value'], pad_clip=False)
+                                       c['overlap_value'], c['overlap'], c['driver'])
     got = merged.cpu().numpy()
     assert np.isfinite(got).all()
     e = err(got, g)
@@ -334,6 +337,48 @@ def test_long_file_windowed(model, golden_dir, case):
                 margin = np.min(np.abs(g[0].astype(np.float64) - hi[None, :]))
                 pytest.fail('%s %s event mismatch (%s): %d vs %d events, min |x - high| = %g'
                             % (mt, case, which, len(ev_got), len(exp), margin))
+
+
+@pytest.mark.parametrize('case', ['p_ov05', 'p_noov', 'p_ov07', 'p_noov_ov13', 'p_short', 'p_ov10', 'p_ov6',
+                                  'ms_07', 'ms_09_6', 'ms_13_7', 'ms_short', 'ms_long'])
+def test_driver_windows(model, golden_dir, case):
+    """The reference's two window drivers with their own arguments
+    (oracle/make_golden_drivers.py, produced by the reference): predict.py
+    strides 1 s with --overlap and sample_duration s without, and merges at
+    int(100 * overlap_value) frames whatever the stride; main_strong strides
+    overlap_value (float64 running start: 0.7, 0.9, 1.3) over the clip padded
+    to 10 s and feeds windows past 10 s shorter (their own batch).  Merged
+    framewise within TOL, the same shape, identical events; where the
+    reference raised (numpy broadcast), sedx raises too.  Two clips per call
+    (the same audio twice): the batched merge of both equals the golden."""
+    from sedx import inference
+    mt, m = model
+    ev = json.load(open(os.path.join(golden_dir, 'drivers_events.json')))
+    assert case in ev['cases']
+    c = ev['cases'][case]
+    audio = synth.make_waveforms(1, seconds=c['samples'] / 16000., sample_rate=16000, seed=c['seed'])
+    audio = torch.from_numpy(np.concatenate([audio, audio])).cuda()
+    args = (m, audio, c['sample_duration'], c['overlap_value'], c['overlap'], c['driver'])
+    if 'raises' in c[mt]:
+        with pytest.raises(RuntimeError):
+            inference.predict_windows(*args)
+        return
+    g = np.load(os.path.join(golden_dir, 'drivers_%s.npz' % mt))[case]
+    merged = inference.predict_windows(*args)
+    got = merged.cpu().numpy()
+    assert got.shape == (2,) + g.shape[1:], (got.shape, g.shape)
+    e = max(err(got[:1], g), err(got[1:], g))
+    print(mt, case, 'merged', got.shape, 'max|d| =', e)
+    assert e <= TOL
+    for which in ('default', 'synthetic'):
+        params = ev['params_' + which]
+        exp = c[mt][which]
+        ev_got = inference.events_from_framewise(merged[:1], params)
+        if ev_got != exp:
+            hi = np.broadcast_to(np.asarray(params['sed_high_threshold'], np.float64), (25,))
+            margin = np.min(np.abs(g[0].astype(np.float64) - hi[None, :]))
+            pytest.fail('%s %s event mismatch (%s): %d vs %d events, min |x - high| = %g'
+                        % (mt, case, which, len(ev_got), len(exp), margin))
 
 
 def test_windowed_multi_clip_matches_single(model):

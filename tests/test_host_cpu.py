@@ -118,6 +118,81 @@ def test_window_geometry_host_rules():
     assert O.window_starts(3.0, 5, 1) == [0]
 
 
+DRIVER_CASES = [  # (driver, overlap, sample_duration, overlap_value, seconds)
+    ('predict', True, 5, 1.0, 10.0), ('predict', True, 5, 0.5, 23.0), ('predict', False, 5, 1.0, 23.0),
+    ('predict', False, 5, 0.7, 17.3), ('predict', True, 6, 0.5, 71.3), ('predict', True, 5, 1.0, 187.37),
+    ('predict', True, 5, 1.0, 3.2), ('main_strong', True, 5, 0.7, 10.0), ('main_strong', True, 6, 0.9, 10.0),
+    ('main_strong', True, 7, 1.3, 10.0), ('main_strong', True, 5, 0.1, 10.0), ('main_strong', True, 5, 0.3, 9.9),
+    ('main_strong', True, 5, 1.0, 12.3), ('main_strong', True, 6, 0.5, 8.7), ('main_strong', True, 7, 0.9, 14.1)]
+
+
+@pytest.mark.parametrize('driver,overlap,sd,ov,secs', DRIVER_CASES)
+def test_native_window_starts_match_reference_loops(driver, overlap, sd, ov, secs):
+    """sedx_window_starts (host C++, no GPU) against the reference's loop
+    control restated in the oracle: predict.py:297-338 strides 1 s with
+    --overlap, else sample_duration; main_strong.py:790-832 strides
+    overlap_value (float64 running start) over the clip padded to 10 s and
+    feeds windows past 10 s shorter."""
+    from sedx import inference
+    L = int(round(secs * 16000))
+    starts, lens = inference.window_starts(16000, L, sd, ov, driver, overlap)
+    ref = O.window_starts(L / 16000., sd, O.driver_stride(driver, sd, ov, overlap))
+    assert starts == [int(s * 16000) for s in ref]
+    for s, n in zip(starts, lens):
+        want = sd * 16000 if driver == 'predict' else max(0, min(s + sd * 16000, 160000) - s)
+        assert n == want
+
+
+def _ref_merge_all(wins, sd, ov, avg):
+    merged = wins[0].copy()
+    for k in range(2, len(wins) + 1):
+        merged = O.merge(merged if k > 2 else wins[0], wins[k - 1], sd, k, ov)
+    return O.avg_merge(merged, sd, ov) if avg else merged
+
+
+@pytest.mark.parametrize('seed', range(40))
+def test_native_merge_matches_numpy_merge(seed):
+    """sedx_merge_host (the host plan the GPU merge runs by) against
+    utilities.merge / avg_merge (restated in the oracle, numpy semantics) on
+    random windows, bit for bit: random window counts and lengths (incl.
+    ragged last windows), steps below / at / above the window length
+    (numpy's clamped slicing concatenates; broadcasting of a 1-frame
+    operand), float and zero steps; where numpy raises, sedx raises."""
+    from sedx import inference
+    rng = np.random.default_rng(seed)
+    n = int(rng.integers(1, 12))
+    tw = int(rng.choice([1, 2, 40, 96, 100, 296, 400, 496, 500]))
+    frames = [tw] * n
+    if rng.random() < 0.4:                     # shorter trailing windows (main_strong past 10 s)
+        for j in range(int(rng.integers(1, 3))):
+            frames[-1 - j % n] = int(rng.integers(1, tw + 1))
+    sd = int(rng.integers(1, 8))
+    ov = float(rng.choice([0.5, 0.7, 0.9, 1.0, 1.3, 1.4, 1.9, 2.0, 3.0, 4.99, 5.0, 6.0, 10.0, 0.004, -0.5]))
+    avg = bool(rng.random() < 0.7)
+    C = 3
+    wins = [rng.uniform(0, 1, (1, f, C)).astype(np.float32) for f in frames]
+    try:
+        ref = _ref_merge_all(wins, sd, ov, avg)
+    except ValueError:
+        with pytest.raises(ValueError):
+            inference.merge_host(wins, sd, ov, avg)
+        return
+    got = inference.merge_host(wins, sd, ov, avg)
+    assert got.shape == ref.shape
+    np.testing.assert_array_equal(got, ref.astype(np.float32))
+
+
+def test_native_merge_float_overlap_steps():
+    """int(100 * overlap_value) in float64: 70 / 90 / 130 / 140 / 190
+    frames (a float32 overlap_value would give 69 / 89 / ...)."""
+    from sedx import inference
+    for ov, step in ((0.7, 70), (0.9, 90), (1.3, 130), (1.4, 140), (1.9, 190)):
+        assert int(100 * ov) == step
+        wins = [np.ones((1, 500, 1), np.float32)] * 3
+        got = inference.merge_host(wins, 5, ov, avg=False)
+        assert got.shape[1] == 500 + 2 * step
+
+
 def test_no_packed_fp32_in_any_kernel():
     """Every kernel's gfx950 ISA is free of packed FP32 VALU (v_pk_add/mul/
     fma_f32): measured on MI355X, packed FP32 beside MFMA waves on the same

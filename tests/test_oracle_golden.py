@@ -68,9 +68,9 @@ def test_windowed_and_events(golden_dir, mt):
     ev = json.load(open(os.path.join(golden_dir, 'events.json')))
     audio = synth.make_waveforms(2, seconds=10.0, sample_rate=16000, seed=1234)[0]
     sd = _sd(mt)
-    merged = O.predict_windows(sd, mt, audio, 16000, 5, 1, None)
+    merged = O.predict_windows(sd, mt, audio, 16000, 5, 1, 'predict', overlap=True)
     _close(merged, g['merged_5_1'], 1e-5, 'merged_5_1')
-    merged_ms = O.predict_windows(sd, mt, audio, 16000, 6, 0.5, 160000)
+    merged_ms = O.predict_windows(sd, mt, audio, 16000, 6, 0.5, 'main_strong')
     _close(merged_ms, g['merged_6_05'], 1e-5, 'merged_6_05')
     for which in ('default', 'synthetic'):
         got = O.events_from_framewise(g['merged_5_1'], ev['params_' + which])
@@ -81,13 +81,16 @@ def test_windowed_and_events(golden_dir, mt):
 def test_long_file_windowed(golden_dir, mt):
     """Long files (predict.py's unbounded loop, oracle/make_golden_long.py):
     the oracle's window count and merged length match the reference golden,
-    the oracle reproduces the 131-window 6 s / 0.5 s merge, and its events
-    match the reference's on both long goldens."""
+    the oracle reproduces the 66-window predict.py --sample_duration 6
+    --overlap --overlap_value 0.5 merge (1 s stride, windows 50 frames apart
+    in the merged output), and its events match the reference's on both long
+    goldens."""
     ev = json.load(open(os.path.join(golden_dir, 'long_events.json')))
     for case, c in sorted(ev['cases'].items()):
         g = np.load(os.path.join(golden_dir, 'long_%s.npz' % case))[mt]
         secs = c['samples'] / 16000.
-        starts = O.window_starts(secs, c['sample_duration'], c['overlap_value'])
+        starts = O.window_starts(secs, c['sample_duration'],
+                                 O.driver_stride(c['driver'], c['sample_duration'], c['overlap_value'], c['overlap']))
         step = int(100 * c['overlap_value'])
         assert len(starts) > 64
         # N = Tw + (n_win - 1) * step, Tw = a window's framewise length
@@ -96,12 +99,36 @@ def test_long_file_windowed(golden_dir, mt):
         if mt == GRU:
             tw = O.roundup(tw)
         assert g.shape[1] == tw + (len(starts) - 1) * step
-        if case == '6_05':   # 131 batch-1 forwards: ~4-8 s on the CPU
+        if case == '6_05':   # 66 batch-1 forwards: a few s on the CPU
             audio = synth.make_waveforms(1, seconds=secs, sample_rate=16000, seed=c['seed'])[0]
-            merged = O.predict_windows(_sd(mt), mt, audio, 16000, c['sample_duration'], c['overlap_value'])
+            merged = O.predict_windows(_sd(mt), mt, audio, 16000, c['sample_duration'], c['overlap_value'],
+                                       c['driver'], overlap=c['overlap'])
             _close(merged, g, 1e-5, 'long_' + case)
         for which in ('default', 'synthetic'):
             assert O.events_from_framewise(g, ev['params_' + which]) == c[mt][which], (case, which)
+
+
+@pytest.mark.parametrize('mt', [GRU, TRF])
+def test_driver_windows(golden_dir, mt):
+    """Every window-driver case the reference produced (oracle/
+    make_golden_drivers.py: predict.py with and without --overlap and with
+    merge steps 50 / 70 / 100 / 130 / 1000, main_strong at 0.7 / 0.9 / 1.3,
+    clips shorter and longer than 10 s): the oracle's loop gives the same
+    merged output and events, and raises where the reference raised."""
+    ev = json.load(open(os.path.join(golden_dir, 'drivers_events.json')))
+    g = np.load(os.path.join(golden_dir, 'drivers_%s.npz' % mt))
+    sd = _sd(mt)
+    for case, c in sorted(ev['cases'].items()):
+        audio = synth.make_waveforms(1, seconds=c['samples'] / 16000., sample_rate=16000, seed=c['seed'])[0]
+        args = (sd, mt, audio, 16000, c['sample_duration'], c['overlap_value'], c['driver'])
+        if 'raises' in c[mt]:
+            with pytest.raises(ValueError):
+                O.predict_windows(*args, overlap=c['overlap'])
+            continue
+        merged = O.predict_windows(*args, overlap=c['overlap'])
+        _close(merged, g[case], 1e-5, case)
+        for which in ('default', 'synthetic'):
+            assert O.events_from_framewise(g[case], ev['params_' + which]) == c[mt][which], (case, which)
 
 
 def test_merge_kat(golden_dir):
