@@ -4,6 +4,13 @@
                     [--mode clip|window] [--batch 32] [--precision winograd|exact|x3]
                     [--no-cpu-baseline] [--no-side]
 
+With --gpus N > 1 and no WORLD_SIZE in the environment (a plain
+``python bench.py --gpus 8``) the process launches N ranks itself before it
+touches the GPU: N child processes of this script with RANK / LOCAL_RANK /
+WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT set (the contract torchrun
+gives them; under torch.distributed.run the script runs as that rank
+directly), prints rank 0's JSON line and exits non-zero if any rank fails.
+
 One step = one forward of the hot path over one batch of synthetic 10 s @
 16 kHz clips per GPU (clip mode = main_strong inference_prob semantics, B=32
 per GPU: BASELINE.json configs[1]), inputs already resident in HBM, weights
@@ -12,10 +19,9 @@ throughout (no operand narrower than fp32): every GEMM on fp32 operands with
 fp32 accumulation (v_mfma_f32_32x32x2_f32, GRU recurrence on fp32 MFMA), block
 1's conv2 and blocks 2-4's convs as Winograd F(2x2,3x3) with fp32 transforms
 (--precision winograd, the library's default arithmetic).  For
-N > 1 (launched by torch.distributed.run, one process per GPU) every rank
-runs its own shard of clips (weak scaling) and the framewise outputs are
-gathered to rank 0 over RCCL inside each step — the path's only collective.
-Rank 0 prints ONE JSON line.
+N > 1 (one process per GPU) every rank runs its own shard of clips (weak
+scaling) and the framewise outputs are gathered to rank 0 over RCCL inside
+each step — the path's only collective.  Rank 0 prints ONE JSON line.
 
 At N = 1 the line also carries, each with its own roofline:
   value_exact         the same workload with the direct fp32 conv everywhere
@@ -31,17 +37,34 @@ At N = 1 the line also carries, each with its own roofline:
                       threshold margin)
 """
 import argparse
+import contextlib
 import ctypes
 import json
 import os
+import socket
 import statistics
+import subprocess
 import sys
+import tempfile
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 T_START = time.perf_counter()
-# SEDX_PKG: an alternative build of the package (A/B runs of kernel variants)
-for _p in (REPO, os.environ.get('SEDX_PKG') or os.path.join(REPO, 'sound-event-detection_amd')):
+
+
+def _ab_package(argv):
+    """--ab-package DIR (A/B runs of kernel variants, tools/ab_build.sh): an
+    alternative build of the package, named on the command line and recorded
+    in the JSON line ('library'); the default is the in-tree package."""
+    for i, a in enumerate(argv):
+        if a == '--ab-package' and i + 1 < len(argv):
+            return os.path.abspath(argv[i + 1])
+        if a.startswith('--ab-package='):
+            return os.path.abspath(a.split('=', 1)[1])
+    return None
+
+
+for _p in (REPO, _ab_package(sys.argv[1:]) or os.path.join(REPO, 'sound-event-detection_amd')):
     if _p not in sys.path:
         sys.path.insert(0, _p)
 
@@ -69,6 +92,8 @@ DTYPE = {'exact': 'f32',
 # separate conv1 launch, 2 computes conv1 inside the Winograd launch)
 WINO_BLOCK1 = 2
 WINO_MUL = 16.0 / 36.0
+# SEDX_TUNE_GRU_KERNEL values (include/sedx.h)
+GRU_KERNELS = {'coop': 0, 'simple': 1, 'tag16': 2, 'tag8': 3, 'coop16': 4, 'auto': 5}
 
 
 def wino_stages():
@@ -246,42 +271,49 @@ def measure(step, args, world, dev, model=None, B=32):
     requests), so one batch's GRU / MHA + head overlap the next batch's conv
     stack.  Every step is a complete forward of its own batch.  Returns
     (clips/s over all ranks, elapsed s, per-stage ms over the timed region)."""
-    streams = [torch.cuda.Stream(dev) for _ in range(max(1, args.streams))]
+    cuda = dev.type == 'cuda'
+    streams = [torch.cuda.Stream(dev) if cuda else None for _ in range(max(1, args.streams))]
+
+    def on(st):
+        return torch.cuda.stream(st) if cuda else contextlib.nullcontext()
+
     if model is not None:
         # conv stacks in issue order (sedx_set_pipelined): without it the
         # batches in flight can fall into lockstep, two conv stacks splitting
         # the chip and the GRUs running side by side on 32 CUs
         model.set_pipelined(len(streams) > 1 and not args.no_pipeline)
-    torch.cuda.synchronize()
+    sync(dev)
     for i in range(args.warmup):
-        with torch.cuda.stream(streams[i % len(streams)]):
+        with on(streams[i % len(streams)]):
             step()
-    torch.cuda.synchronize()
+    sync(dev)
     if world > 1:
         dist.barrier()
     nat = L = None
-    if model is not None:
+    prof = model is not None and getattr(model, 'stage_profiling', True)
+    if prof:
         # per-stage HIP events over the timed region: libsedx records them on
         # the stream each forward's kernels are launched on, one event set per
         # forward (accumulate mode), averaged by sedx_stage_times afterwards
         nat, L = model.native(dev), _lib.lib()
         _lib.check(L.sedx_set_profiling(nat.h, 2), nat.h, 'set_profiling')
-    torch.cuda.synchronize()
+    sync(dev)
     t0 = time.perf_counter()
     for i in range(args.steps):
-        with torch.cuda.stream(streams[i % len(streams)]):
+        with on(streams[i % len(streams)]):
             step()
-    torch.cuda.synchronize()
+    sync(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     stage_ms = None
-    if model is not None:
+    if prof:
         ms = (ctypes.c_float * len(_lib.STAGES))()
         n = ctypes.c_int32()
         _lib.check(L.sedx_stage_times(nat.h, ms, len(_lib.STAGES), ctypes.byref(n)), nat.h, 'stage_times')
         _lib.check(L.sedx_set_profiling(nat.h, 0), nat.h, 'set_profiling')
         stage_ms = {s_: round(float(v), 4) for s_, v in zip(_lib.STAGES, ms[:])}
+    if model is not None:
         model.set_pipelined(False)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -290,14 +322,20 @@ def measure(step, args, world, dev, model=None, B=32):
     return world * B * args.steps / elapsed, elapsed, stage_ms
 
 
-def latency(step_fn, B, reps):
+def sync(dev):
+    if dev.type == 'cuda':
+        torch.cuda.synchronize(dev)
+
+
+def latency(step_fn, B, reps, dev=None):
     """p50 / p99 of (batch wall time / clips), one batch at a time."""
+    dev = dev or torch.device('cuda', torch.cuda.current_device())
     lat = []
     for _ in range(reps):
-        torch.cuda.synchronize()
+        sync(dev)
         a = time.perf_counter()
         step_fn()
-        torch.cuda.synchronize()
+        sync(dev)
         lat.append((time.perf_counter() - a) * 1e3 / B)
     lat.sort()
     return statistics.median(lat), lat[min(len(lat) - 1, int(0.99 * len(lat)))]
@@ -503,7 +541,7 @@ def clip_leg(model, wave, args, world, rank, dev, precision, isolated=False):
                 distributed.gather_to_rank0(fw, world, rank)
 
     value, elapsed, stage_ms = measure(step, args, world, dev, model, B)
-    p50, p99 = latency(step, B, max(5, min(args.steps, 20)))
+    p50, p99 = latency(step, B, max(5, min(args.steps, 20)), dev)
     iso = stage_times_isolated(model, wave, dev, max(3, min(args.steps, 10))) if isolated else None
     return value, elapsed, stage_ms, p50, p99, iso
 
@@ -583,6 +621,108 @@ def events_side(model, wave):
     return {'events_ms_per_batch': round((time.perf_counter() - t0) / reps * 1e3, 4), 'events_per_batch': n_ev}
 
 
+# ---------------------------------------------------------------------------
+# N ranks from a plain `python bench.py --gpus N` (no torchrun around it)
+# ---------------------------------------------------------------------------
+def _free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(('127.0.0.1', 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(n, argv):
+    """Start n ranks of this script (one process per GPU, the environment
+    torch.distributed.run gives each: RANK, LOCAL_RANK, WORLD_SIZE,
+    LOCAL_WORLD_SIZE, MASTER_ADDR=127.0.0.1, MASTER_PORT), wait for all of
+    them, print rank 0's stdout (the JSON line) and return the exit code: the
+    first failing rank's, after stopping the others (they would wait at the
+    next collective).  Lines rank 0's libraries print to stdout (gloo's
+    connection notes) go to stderr, so stdout holds the one JSON line.  The caller has not touched the GPU (no HIP call in this
+    process); the ranks are child processes, never an exec of this one."""
+    port = _free_port()
+    out = tempfile.TemporaryFile(mode='w+')
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK='0', MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+        env.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')   # dmabuf IPC for RCCL on this host driver
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
+                                      stdout=out if r == 0 else subprocess.DEVNULL))
+    rc = 0
+    try:
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [c for c in codes if c not in (None, 0)]
+            if bad:
+                rc = bad[0]
+                break
+            if all(c == 0 for c in codes):
+                break
+            time.sleep(0.2)
+    finally:
+        for p in procs:                       # exactly the processes started here
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    out.seek(0)
+    for line in out:          # the JSON record to stdout; library chatter on rank 0's stdout to stderr
+        (sys.stdout if line.startswith('{"metric"') else sys.stderr).write(line)
+    sys.stdout.flush()
+    if rc:
+        print('bench: a rank exited with %d' % rc, file=sys.stderr)
+    return rc if rc > 0 else (1 if rc else 0)
+
+
+class StubModel:
+    """CPU stand-in for the model (tests/test_bench_cpu.py drives the N-rank
+    launcher and the N > 1 measurement path with it over gloo): a fixed
+    framewise-shaped output from a small CPU computation per call."""
+    stage_profiling = False
+
+    def __init__(self):
+        self.w = torch.linspace(-1, 1, 25)
+
+    def set_precision(self, p):
+        return self
+
+    def set_pipelined(self, on):
+        pass
+
+    def __call__(self, wave):
+        x = wave[:, :1000].reshape(wave.shape[0], 1000, 1)
+        return {'framewise_output': torch.sigmoid(x * self.w)}
+
+
+def stub_main(args, world, rank):
+    """--stub: the launcher + clip_leg's N > 1 branch (gather to rank 0 in
+    every step, barrier, all_reduce(MAX) of the elapsed time) on the CPU."""
+    dev = torch.device('cpu')
+    if rank == args.stub_fail_rank:
+        sys.exit(3)
+    B = args.batch
+    wave = torch.from_numpy(synth.make_waveforms(B, 0.1, 16000, seed=1234 + rank))
+    value, elapsed, _, p50, _, _ = clip_leg(StubModel(), wave, args, world, rank, dev, args.precision)
+    env = {k: os.environ.get(k) for k in ('RANK', 'LOCAL_RANK', 'WORLD_SIZE', 'MASTER_ADDR')}
+    envs = [None] * world if rank == 0 else None
+    if world > 1:
+        dist.gather_object(env, envs, dst=0)
+    else:
+        envs = [env]
+    if rank == 0:
+        print(json.dumps({'metric': 'stub', 'value': round(value, 3), 'unit': 'clips/s', 'n_gpus': world,
+                          'steps': args.steps, 'warmup': args.warmup,
+                          'ms_per_step': round(elapsed / args.steps * 1e3, 4), 'stub': True,
+                          'rank_env': envs}))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -604,16 +744,33 @@ def main():
                     help='headline only (no x3 / config 3 / config 4 / window legs, no latency_b1): '
                          'profiling passes use it so per-kernel rocprof averages cover only the headline')
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
-    ap.add_argument('--gru-kernel', choices=['coop', 'tag16', 'tag8', 'simple', 'coop16'], default='coop',
-                    help='GRU recurrence kernel (SEDX_TUNE_GRU_KERNEL; A/B runs)')
+    ap.add_argument('--gru-kernel', choices=list(GRU_KERNELS), default='auto',
+                    help='GRU recurrence kernel (SEDX_TUNE_GRU_KERNEL; A/B runs); auto: the library default '
+                         '(the 8-slice kernel on a pipelined handle, 16 slices one batch at a time)')
+    ap.add_argument('--ab-package', default=None,
+                    help='A/B runs: load sedx from this package directory instead of the in-tree build '
+                         '(recorded in the JSON line as "library")')
+    ap.add_argument('--stub', action='store_true',
+                    help='CPU stand-in model (tests of the N-rank launcher and the N > 1 measurement path)')
+    ap.add_argument('--stub-fail-rank', type=int, default=-1,
+                    help='with --stub: this rank exits with status 3 after the process group is up (launcher test)')
     ap.add_argument('--wino-block1', type=int, choices=[0, 1, 2], default=None,
                     help='winograd precision: block 1 as Winograd with conv1 inside the launch (2), fed by a '
                          'separate conv1 launch (1), or as the direct fused kernel (0); default: WINO_BLOCK1')
     args = ap.parse_args()
 
-    world, rank, local = distributed.init()
-    if world != args.gpus and rank == 0:
-        print('warning: --gpus %d but WORLD_SIZE %d' % (args.gpus, world), file=sys.stderr)
+    if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
+        # a plain `python bench.py --gpus N`: start the N ranks here, before
+        # anything in this process touches the GPU
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    world, rank, local = distributed.init('gloo' if args.stub else None)
+    if world != args.gpus:
+        if rank == 0:
+            print('bench: --gpus %d but WORLD_SIZE %d' % (args.gpus, world), file=sys.stderr)
+        sys.exit(2)
+    if args.stub:
+        stub_main(args, world, rank)
+        return
     dev = torch.device('cuda', local)
     torch.cuda.set_device(dev)
     name = MODEL_NAMES[args.model]
@@ -621,9 +778,7 @@ def main():
     if args.wino_block1 is not None:
         WINO_BLOCK1 = args.wino_block1
     model = build_model(name, dev)
-    gk = {'coop': 0, 'simple': 1, 'tag16': 2, 'tag8': 3, 'coop16': 4}[args.gru_kernel]
-    if gk:
-        model.set_tuning(_lib.TUNE_GRU_KERNEL, gk)
+    model.set_tuning(_lib.TUNE_GRU_KERNEL, GRU_KERNELS[args.gru_kernel])
     B = args.batch
     wave = torch.from_numpy(synth.make_waveforms(B, 10.0, 16000, seed=1234 + rank)).to(dev)
 
@@ -741,7 +896,8 @@ def main():
                        'sample_rate': 16000, 'mode': args.mode, 'precision': args.precision,
                        'parallelism': 'dp%d clip-sharded, RCCL gather of framewise' % world,
                        'streams': args.streams,
-                       'pipelined': args.streams > 1 and not args.no_pipeline},
+                       'pipelined': args.streams > 1 and not args.no_pipeline,
+                       'gru_kernel': args.gru_kernel if args.model == 'gru' else None},
             'ms_per_clip_p99': round(p99, 4) if p99 is not None else None,
             'ms_per_clip_p50_note': 'per batch, one at a time, from pinned host input (H2D on a copy '
                                     'stream) to framewise in pinned host memory on rank 0',
@@ -749,7 +905,7 @@ def main():
             'ms_per_clip_p50_i16_input': round(p50_i16, 4) if p50_i16 is not None else None,
             'ms_per_clip_p99_device': round(p99_dev, 4) if p99_dev is not None else None,
             'roofline': roof, 'cpu_baseline': cpu, 'stage_ms': stage_ms,
-            # the libsedx.so this run loaded (SEDX_PKG selects another build for A/B runs)
+            # the libsedx.so this run loaded (--ab-package selects another build for A/B runs)
             'library': os.path.relpath(_lib.LIB_PATH, REPO), 'library_version': _lib.lib().sedx_version().decode(),
         }
         line.update(extra)

@@ -2,7 +2,10 @@
 roofline.achieved (26.03 GFLOP of conv per 10 s clip) and
 the roofline record built from per-stage times."""
 import importlib.util
+import json
 import os
+import subprocess
+import sys
 
 import pytest
 
@@ -107,3 +110,45 @@ def test_roofline_fracs_are_fractions(bench):
     assert not any(k.endswith('_algorithmic') for k in w)
     t = bench.roofline(stage, 32, 'winograd')              # no isolated pass: the timed region
     assert t['avg_launch_ms'] == round(stage['b1c2'], 4)
+
+
+def _bench_env():
+    env = dict(os.environ)
+    for k in ('WORLD_SIZE', 'RANK', 'LOCAL_RANK', 'MASTER_ADDR', 'MASTER_PORT', 'LOCAL_WORLD_SIZE'):
+        env.pop(k, None)
+    env['OMP_NUM_THREADS'] = '1'
+    return env
+
+
+@pytest.mark.parametrize('n', [2, 8])
+def test_bench_launches_n_ranks(n):
+    """`python bench.py --gpus N` with no torchrun around it starts N ranks
+    itself (the driver's BENCH form): each child gets RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_ADDR, the N > 1 measurement path runs (gather of the
+    framewise output to rank 0 every step, barrier, all_reduce(MAX) of the
+    elapsed time; gloo and a CPU stand-in model here), and exactly one JSON
+    line comes back, with n_gpus = N."""
+    B, steps = 4, 3
+    r = subprocess.run([sys.executable, os.path.join(REPO, 'bench.py'), '--gpus', str(n), '--stub', '--steps',
+                        str(steps), '--warmup', '1', '--batch', str(B), '--streams', '1'],
+                       capture_output=True, text=True, timeout=600, cwd=REPO, env=_bench_env())
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d['n_gpus'] == n and d['stub'] and d['steps'] == steps
+    assert sorted(int(e['RANK']) for e in d['rank_env']) == list(range(n))
+    for e in d['rank_env']:
+        assert e['WORLD_SIZE'] == str(n) and e['LOCAL_RANK'] == e['RANK'] and e['MASTER_ADDR'] == '127.0.0.1'
+    # whole-job clips/s over all ranks from the max-over-ranks elapsed time
+    assert abs(d['value'] - n * B * steps / (d['ms_per_step'] * steps / 1e3)) <= 0.01 * d['value'] + 1e-3
+
+
+def test_bench_launcher_fails_when_a_rank_fails():
+    """A failing rank makes the launcher stop the other ranks (they would wait
+    at the next collective) and exit non-zero, with no JSON line."""
+    r = subprocess.run([sys.executable, os.path.join(REPO, 'bench.py'), '--gpus', '3', '--stub', '--steps', '2',
+                        '--warmup', '1', '--batch', '2', '--streams', '1', '--stub-fail-rank', '1'],
+                       capture_output=True, text=True, timeout=300, cwd=REPO, env=_bench_env())
+    assert r.returncode != 0
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith('{')]

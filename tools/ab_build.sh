@@ -1,7 +1,7 @@
 #!/bin/bash
 # Build an A/B variant of the package into sound-event-detection_amd/build/ab/<name>
 # (python sources copied, libsedx.so compiled with extra flags), for
-# SEDX_PKG=<that dir> python bench.py ... in the same GPU call as the tree's build.
+# python bench.py --ab-package <that dir> ... in the same GPU call as the tree's build.
 #   tools/ab_build.sh <name> "<extra hipcc flags>"
 set -e
 cd "$(dirname "$0")/.."

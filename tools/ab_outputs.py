@@ -1,6 +1,6 @@
 """Save a fixed forward's outputs (both models, both precisions, B=1 and B=32)
 for bit-exactness checks between two builds of the package:
-    SEDX_PKG=<pkg dir> python tools/ab_outputs.py out.npz
+    python tools/ab_outputs.py out.npz --ab-package <pkg dir>
     python tools/ab_outputs.py --compare a.npz b.npz"""
 import os
 import sys
@@ -17,7 +17,7 @@ if sys.argv[1] == '--compare':
     sys.exit(1 if bad else 0)
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), '..'))
-import bench  # noqa: E402  (honours SEDX_PKG)
+import bench  # noqa: E402  (honours --ab-package in sys.argv)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 from sedx import synth  # noqa: E402

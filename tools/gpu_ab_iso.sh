@@ -6,8 +6,8 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 for r in 1 2; do
   for v in tree ${VARIANTS}; do
-    if [ $v = tree ]; then P=""; else P="$PWD/sound-event-detection_amd/build/ab/$v"; fi
-    SEDX_PKG=$P timeout -k 10 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline ${BENCH_ARGS} \
+    if [ $v = tree ]; then P=""; else P="--ab-package $PWD/sound-event-detection_amd/build/ab/$v"; fi
+    timeout -k 10 300 python bench.py $P --steps 20 --warmup 3 --no-cpu-baseline ${BENCH_ARGS} \
       > gpurun_out/abi_$v$r.log 2>&1 || exit $?
     python3 -c "
 import json

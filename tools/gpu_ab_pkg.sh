@@ -1,13 +1,13 @@
 #!/bin/bash
 # A/B of the headline between the tree's build (B) and variant packages built
-# by tools/ab_build.sh (SEDX_PKG), alternating rounds in one GPU call.
+# by tools/ab_build.sh (bench.py --ab-package), alternating rounds in one GPU call.
 #   VARIANTS="nb4 ..." bash tools/gpu_ab_pkg.sh
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 for r in ${ROUNDS:-1 2}; do
   for v in tree ${VARIANTS}; do
-    if [ $v = tree ]; then P=""; else P="$PWD/sound-event-detection_amd/build/ab/$v"; fi
-    SEDX_PKG=$P timeout -k 10 300 python bench.py --steps ${STEPS:-30} --warmup 3 --no-cpu-baseline ${BENCH_ARGS:---no-side} \
+    if [ $v = tree ]; then P=""; else P="--ab-package $PWD/sound-event-detection_amd/build/ab/$v"; fi
+    timeout -k 10 300 python bench.py $P --steps ${STEPS:-30} --warmup 3 --no-cpu-baseline ${BENCH_ARGS:---no-side} \
       > gpurun_out/abp_$v$r.log 2>&1 || exit $?
     python3 -c "
 import json

@@ -12,8 +12,8 @@ tail -25 gpurun_out/t2.log
 for r in 1 2; do
   for v in tree:1 tree:2 ${VARIANTS:-pre:2}; do
     pkg=${v%%:*}; wb=${v##*:}
-    if [ $pkg = tree ]; then P=""; else P="$PWD/sound-event-detection_amd/build/ab/$pkg"; fi
-    SEDX_PKG=$P timeout -k 10 200 python bench.py --steps 20 --warmup 3 --no-side --no-cpu-baseline --wino-block1 $wb \
+    if [ $pkg = tree ]; then P=""; else P="--ab-package $PWD/sound-event-detection_amd/build/ab/$pkg"; fi
+    timeout -k 10 200 python bench.py $P --steps 20 --warmup 3 --no-side --no-cpu-baseline --wino-block1 $wb \
       > gpurun_out/ab_${pkg}_$wb$r.log 2>&1 || exit $?
     python3 -c "
 import json
