@@ -280,12 +280,25 @@ sedx_status sedx_set_precision(sedx_handle* h, int32_t mode);
  *                         exists), conv2 as Winograd F(2x2,3x3), pool;
  *                         1: the same conv2 fed by a separate conv1 launch
  *                         (the activation through HBM; bit-identical to 2);
- *                         0: block 1 as the direct fused fp32 kernel. */
+ *                         0: block 1 as the direct fused fp32 kernel.
+ *  SEDX_TUNE_GRU_SPIN     bound of every GRU hand-off spin, in polls (0, the
+ *                         default: 2^24).  A spin that runs out turns that
+ *                         forward's outputs into NaN and is reported by
+ *                         sedx_check_error (tests force it with a bound of 1).
+ *
+ * Co-residency: the cooperative GRU kernels need all workgroups of a
+ * (32-clip group, direction) resident at once — 8 CUs (COOP) or 16 (COOP16)
+ * per pair, one workgroup per CU — and spin on each other.  AUTO picks COOP16
+ * only for a handle that is not pipelined; a caller that runs several
+ * forwards concurrently on other streams without sedx_set_pipelined leaves
+ * fewer CUs free for it: the spins are bounded (SEDX_TUNE_GRU_SPIN), so the
+ * worst case is a NaN batch reported by sedx_check_error, never a hang. */
 typedef enum {
   SEDX_TUNE_GRU_KERNEL = 0,
   SEDX_TUNE_GRU_HANDOFF = 1,
   SEDX_TUNE_WINO_BLOCK1 = 2,
-  SEDX_TUNE_MEL_MFMA = 3
+  SEDX_TUNE_MEL_MFMA = 3,
+  SEDX_TUNE_GRU_SPIN = 4
 } sedx_tuning_knob;
 enum {
   SEDX_GRU_KERNEL_COOP = 0,
@@ -297,6 +310,14 @@ enum {
 };
 enum { SEDX_GRU_HANDOFF_AUTO = 0, SEDX_GRU_HANDOFF_GLOBAL = 1 };
 sedx_status sedx_set_tuning(sedx_handle* h, int32_t knob, int32_t value);
+
+/* Asynchronous failures of forwards already issued: a GRU recurrence whose
+ * bounded hand-off spin ran out wrote NaN outputs and set a host-mapped word.
+ * Call after the work of the forwards in question has completed (a stream
+ * sync, or a device-to-host copy of their outputs): SEDX_EHIP (and
+ * sedx_last_error names it) when one of them failed, clearing the word;
+ * SEDX_OK otherwise.  Every forward entry point also checks it on entry. */
+sedx_status sedx_check_error(sedx_handle* h);
 
 /* Serving with several batches in flight (one stream per request): when on,
  * the conv stack of every forward on this handle starts only after the conv

@@ -92,6 +92,7 @@ struct sedx_handle {
   int gru_handoff = SEDX_GRU_HANDOFF_AUTO;
   int wino_block1 = 2;                     // SEDX_TUNE_WINO_BLOCK1 (2: conv1 inside the Winograd launch)
   int mel_mfma = 0;                        // SEDX_TUNE_MEL_MFMA (measured slower: opt-in)
+  unsigned gru_spin = 0;                   // SEDX_TUNE_GRU_SPIN (0: the default bound)
   // sedx_set_capture: copy one stage's output of every later forward
   int cap_stage = -1;
   float* cap_buf = nullptr;
@@ -442,7 +443,7 @@ sedx_status run_body(sedx_handle* h, int64_t B, const Geometry& g, float* ws, co
                       // kernel holds half the CUs; one batch at a time 16 slices halve
                       // the recurrence's serial product
                       : h->gru_kernel == SEDX_GRU_KERNEL_AUTO ? (h->pipelined ? 2 : 3) : 2,
-                      h->gru_err_dev, s);
+                      h->gru_err_dev, h->gru_spin, s);
   } else {
     linear(S, w.wqkv, w.wqkv_x3, 1536, 128, w.bqkv, G, 0);
     launch_mha(G, iB, (int)g.T3, O, s);
@@ -632,10 +633,19 @@ sedx_status sedx_set_tuning(sedx_handle* h, int32_t knob, int32_t value) {
       if (value != 0 && value != 1) break;
       h->mel_mfma = value;
       return SEDX_OK;
+    case SEDX_TUNE_GRU_SPIN:
+      if (value < 0) break;
+      h->gru_spin = (unsigned)value;
+      return SEDX_OK;
     default:
       return fail(h, SEDX_EINVAL, "unknown tuning knob %d", (int)knob);
   }
   return fail(h, SEDX_EINVAL, "bad value %d for tuning knob %d", (int)value, (int)knob);
+}
+
+sedx_status sedx_check_error(sedx_handle* h) {
+  if (!h) return SEDX_EINVAL;
+  return check_async_error(h);
 }
 
 sedx_status sedx_create(const sedx_config* cfg, int device, sedx_handle** out) {

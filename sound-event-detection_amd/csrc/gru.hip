@@ -84,7 +84,9 @@ constexpr int GRU_HV_LD = 260;        // Hv row stride (floats): 8 rows fit the 
 static_assert(GRU_VALU_CLIPS * GRU_HV_LD <= 16 * 32 * 4 * 4, "Hv inside Aimg");
 // VALU granules [2 pairs][2 parities][clips][256] u64 at the start of the exchange space
 static_assert(2 * 2 * GRU_VALU_CLIPS * 256 * 8 <= 8 * 2 * 32 * 256 * 4, "granules inside X");
-constexpr unsigned GRU_SPIN = 1u << 24;
+// bound of every hand-off spin (polls); sedx_set_tuning(SEDX_TUNE_GRU_SPIN)
+// lowers it (tests force a timeout with it)
+constexpr unsigned GRU_SPIN_DEFAULT = 1u << 24;
 
 struct GruSync {                      // zeroed every launch
   unsigned err;
@@ -98,9 +100,11 @@ struct GruSync {                      // zeroed every launch
 };
 // a bounded spin timed out: the launch's own flag word and the handle's
 // host-mapped word (sedx_forward* returns SEDX_EHIP on the next call)
+// (a plain system-scope store of the code with bit 31 set: any nonzero word
+// reports the failure, and a store needs no PCIe / xGMI atomics on host memory)
 __device__ __forceinline__ void gru_fail(GruSync* sync, unsigned* host_err, unsigned code) {
   atomicOr(&sync->err, code);
-  if (host_err) __hip_atomic_fetch_or(host_err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (host_err) __hip_atomic_store(host_err, code | 0x80000000u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 // the workgroup's timeout word (a __shared__ int): read as an LDS access
 // (a generic volatile pointer would become a flat load, which the compiler
@@ -129,7 +133,7 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
                                                        const float* __restrict__ bhh,
                                                        float* __restrict__ H, float* X,
                                                        GruSync* sync, int nslots, int allow_fast,
-                                                       unsigned* host_err) {
+                                                       unsigned* host_err, unsigned spin_limit) {
   __shared__ uint4 Aimg[16 * 32 * 4];          // h_{s-1} hi/lo, [kstep][clip][4 slots]
   // partial gate pre-activations: K quarters (x3) / eighths (exact: two
   // independent chains per wave, summed in order in the gate phase)
@@ -160,7 +164,7 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
     unsigned spins = 0;
     while (g_ld(&sync->ready[pair][0]) < (unsigned)NS) {
       __builtin_amdgcn_s_sleep(1);
-      if (++spins > GRU_SPIN) {
+      if (++spins > spin_limit) {
         gru_fail(sync, host_err, 1u);
         s_err = 1;
         break;
@@ -266,7 +270,7 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
           if (tid < NS) {
             unsigned spins = 0;
             while (!gru_dead(&s_err) && g_ld(Fl + tid * 16) < (unsigned)gs) {
-              if (++spins > GRU_SPIN) {
+              if (++spins > spin_limit) {
                 gru_fail(sync, host_err, 2u);
                 s_err = 1;
                 break;
@@ -278,7 +282,7 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
           unsigned spins = 0;
           while (!gru_dead(&s_err) && g_ld(C) < target) {
             __builtin_amdgcn_s_sleep(1);
-            if (++spins > GRU_SPIN) {
+            if (++spins > spin_limit) {
               gru_fail(sync, host_err, 1u);
               s_err = 1;
               break;
@@ -307,7 +311,7 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
           if (it < nc * 256) {
             unsigned spins = 0;
             while (!gru_dead(&s_err) && (unsigned)(w[k] >> 32) != (unsigned)gs) {
-              if (++spins > GRU_SPIN) {
+              if (++spins > spin_limit) {
                 gru_fail(sync, host_err, 4u);
                 s_err = 1;
                 break;
@@ -592,7 +596,8 @@ __device__ __forceinline__ void gru_lds_barrier() { asm volatile("s_waitcnt lgkm
 template <int NS>
 __global__ __launch_bounds__(gru_tag_threads<NS>()) void gru_tag_kernel(
     const float* __restrict__ G, int B, int T, const float* __restrict__ whh, const float* __restrict__ bhh,
-    float* __restrict__ H, unsigned long long* X, GruSync* sync, int nslots, unsigned* host_err) {
+    float* __restrict__ H, unsigned long long* X, GruSync* sync, int nslots, unsigned* host_err,
+    unsigned spin_limit) {
   constexpr int U = 256 / NS;          // hidden units per slice
   constexpr int RT = U / 16;           // 16-row tiles per gate
   constexpr int PB = 8 * 3 * U * GRU_PLD;   // floats per partial buffer
@@ -659,7 +664,7 @@ __global__ __launch_bounds__(gru_tag_threads<NS>()) void gru_tag_kernel(
           w[0] = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           while ((unsigned)(w[0] >> 32) != (unsigned)gs && !gru_dead(&s_err)) {
             __builtin_amdgcn_s_sleep(1);
-            if (++spins > GRU_SPIN) {
+            if (++spins > spin_limit) {
               gru_fail(sync, host_err, 4u);
               s_err = 1;
               break;
@@ -675,7 +680,7 @@ __global__ __launch_bounds__(gru_tag_threads<NS>()) void gru_tag_kernel(
             for (int st = 0; st < 8; ++st) ok &= (unsigned)(w[st] >> 32) == (unsigned)gs;
             if (ok || gru_dead(&s_err)) break;
             __builtin_amdgcn_s_sleep(1);
-            if (++spins > GRU_SPIN) {
+            if (++spins > spin_limit) {
               gru_fail(sync, host_err, 4u);
               s_err = 1;
               break;
@@ -776,7 +781,8 @@ size_t gru_coop_workspace_bytes(int B) {
 
 template <int NS>
 static void launch_gru_tag(const float* G, int B, int T, const float* whh, const float* bhh, float* H, GruSync* sync,
-                           unsigned long long* X, size_t sync_bytes, unsigned* host_err, hipStream_t s) {
+                           unsigned long long* X, size_t sync_bytes, unsigned* host_err, unsigned spin,
+                           hipStream_t s) {
   const int ngroups = (B + 15) / 16;
   const int nslots = ngroups < GRU_MAX_SLOTS ? ngroups : GRU_MAX_SLOTS;
   const LaunchInfo li =
@@ -785,11 +791,13 @@ static void launch_gru_tag(const float* G, int B, int T, const float* whh, const
   // sync block + the granules of the pairs in use (every tag 0)
   (void)hipMemsetAsync(sync, 0, sync_bytes + (size_t)2 * nslots * 2 * 16 * 256 * 8, s);
   hipLaunchKernelGGL(gru_tag_kernel<NS>, dim3(8 * NS), dim3(gru_tag_threads<NS>()), li.dyn, s, G, B, T, whh, bhh, H, X, sync, nslots,
-                     host_err);
+                     host_err, spin);
 }
 
 void launch_gru_coop(const float* G, int B, int T, const float* whh, const float* bhh, float* H,
-                     void* ws, bool exact, bool allow_fast, int variant, unsigned* host_err, hipStream_t s) {
+                     void* ws, bool exact, bool allow_fast, int variant, unsigned* host_err, unsigned spin,
+                     hipStream_t s) {
+  if (spin == 0) spin = GRU_SPIN_DEFAULT;
   GruSync* sync = static_cast<GruSync*>(ws);
   const size_t sync_bytes = (sizeof(GruSync) + 255) & ~size_t(255);
   float* X = reinterpret_cast<float*>(static_cast<char*>(ws) + sync_bytes);
@@ -797,9 +805,9 @@ void launch_gru_coop(const float* G, int B, int T, const float* whh, const float
   if (exact && !valu && variant != 2 && variant != 3) {
     auto* Xg = reinterpret_cast<unsigned long long*>(X);
     if (variant == 1)
-      launch_gru_tag<8>(G, B, T, whh, bhh, H, sync, Xg, sync_bytes, host_err, s);
+      launch_gru_tag<8>(G, B, T, whh, bhh, H, sync, Xg, sync_bytes, host_err, spin, s);
     else
-      launch_gru_tag<16>(G, B, T, whh, bhh, H, sync, Xg, sync_bytes, host_err, s);
+      launch_gru_tag<16>(G, B, T, whh, bhh, H, sync, Xg, sync_bytes, host_err, spin, s);
     return;
   }
   const int ngroups = (B + 31) / 32;
@@ -809,16 +817,16 @@ void launch_gru_coop(const float* G, int B, int T, const float* whh, const float
   (void)hipMemsetAsync(sync, 0, sync_bytes + (valu ? (size_t)2 * 2 * GRU_VALU_CLIPS * 256 * 8 : 0), s);
   if (valu)
     launch_kernel(gru_coop_kernel<true, true>, dim3(64), 768, s, G, B, T, whh, bhh, H, X, sync, nslots,
-                  allow_fast ? 1 : 0, host_err);
+                  allow_fast ? 1 : 0, host_err, spin);
   else if (exact && variant == 3)   // 16 slices per (group, direction)
     launch_kernel(gru_coop_kernel<true, false, 16>, dim3(128), 768, s, G, B, T, whh, bhh, H, X, sync, nslots,
-                  allow_fast ? 1 : 0, host_err);
+                  allow_fast ? 1 : 0, host_err, spin);
   else if (exact)
     launch_kernel(gru_coop_kernel<true, false>, dim3(64), 768, s, G, B, T, whh, bhh, H, X, sync, nslots,
-                  allow_fast ? 1 : 0, host_err);
+                  allow_fast ? 1 : 0, host_err, spin);
   else
     launch_kernel(gru_coop_kernel<false, false>, dim3(64), 768, s, G, B, T, whh, bhh, H, X, sync, nslots,
-                  allow_fast ? 1 : 0, host_err);
+                  allow_fast ? 1 : 0, host_err, spin);
 }
 
 }  // namespace sedx

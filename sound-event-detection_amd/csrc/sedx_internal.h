@@ -34,7 +34,7 @@ struct FrontendParams {
   int32_t n_clips;          // items = n_clips * n_win
   int32_t n_win;            // windows per clip (1 in clip mode)
   const int64_t* win_start; // [n_win] device table of window sample offsets
-                            // (launch_window_starts); nullptr: every item starts at 0
+                            // (the windowed driver's host table); nullptr: every item starts at 0
   int64_t clip_len;         // valid samples per clip (beyond => zeros; pad_truncate)
   int64_t sig_len;          // samples per item fed to the STFT (L or window length)
   int32_t T;                // frames per item = sig_len / hop + 1
@@ -269,8 +269,10 @@ size_t gru_coop_workspace_bytes(int B);
 // bounded hand-off spin times out (outputs of that launch are then NaN).
 // variant (exact, B > 8): 2 the 32-clip flag hand-off kernel (default; x3
 // always), 0 the 16-clip data-tagged kernel with 16 slices, 1 with 8 slices.
+// spin: bound of every hand-off spin in polls (0: the default, 2^24).
 void launch_gru_coop(const float* G, int B, int T, const float* whh, const float* bhh, float* H,
-                     void* ws, bool exact, bool allow_fast, int variant, unsigned* host_err, hipStream_t s);
+                     void* ws, bool exact, bool allow_fast, int variant, unsigned* host_err, unsigned spin,
+                     hipStream_t s);
 
 // MHA core: QKV [B][T][1536] (q|k|v, head h = cols 64h..64h+63) -> O [B][T][512]
 void launch_mha(const float* QKV, int B, int T, float* O, hipStream_t s);

@@ -23,8 +23,8 @@ EXPORTS = ['sedx_create', 'sedx_destroy', 'sedx_last_error', 'sedx_version', 'se
            'sedx_forward_windows_vote', 'sedx_events_workspace_size', 'sedx_events_device',
            'sedx_forward_i16', 'sedx_wav_parse', 'sedx_wav_decode_mono', 'sedx_resample_size',
            'sedx_resample_workspace_size', 'sedx_resample', 'sedx_gamma_workspace_size',
-           'sedx_set_tuning', 'sedx_set_capture', 'sedx_window_starts', 'sedx_merge_host']
-TUNE_GRU_KERNEL, TUNE_GRU_HANDOFF, TUNE_WINO_BLOCK1, TUNE_MEL_MFMA = 0, 1, 2, 3
+           'sedx_set_tuning', 'sedx_set_capture', 'sedx_window_starts', 'sedx_merge_host', 'sedx_check_error']
+TUNE_GRU_KERNEL, TUNE_GRU_HANDOFF, TUNE_WINO_BLOCK1, TUNE_MEL_MFMA, TUNE_GRU_SPIN = 0, 1, 2, 3, 4
 PRECISION = {'exact': 0, 'x3': 1, 'winograd': 2}
 STAGES = ['frontend', 'b1c1', 'b1c2', 'b2c1', 'b2c2', 'b3c1', 'b3c2', 'b4c1', 'b4c2', 'seq', 'head']
 
@@ -102,6 +102,7 @@ def lib():
         'sedx_gamma_features': ([P, P, I64, I64, P, PI64, P, SZ, P], I32),
         'sedx_gamma_workspace_size': ([P, I64, I64, PSZ], I32),
         'sedx_set_tuning': ([P, I32, I32], I32),
+        'sedx_check_error': ([P], I32),
         'sedx_set_capture': ([P, I32, P, SZ], I32),
         'sedx_window_starts': ([I32, I64, PSPEC, P, P, I64, PI64], I32),
         'sedx_merge_host': ([P, P, I64, I64, I32, F64, I32, P, I64, PI64], I32),

@@ -376,6 +376,7 @@ def inference_prob(model, waveforms, batch_size=32, device=None):
             o = model(x)
             outs['clipwise_output'].append(o['clipwise_output'].cpu().numpy())
             outs['framewise_output'].append(o['framewise_output'].cpu().numpy())
+            model.check_error()     # the batch is complete: an asynchronous failure surfaces here
     return {k: np.concatenate(v, axis=0) for k, v in outs.items()}
 
 

@@ -334,6 +334,16 @@ class _SedModel(nn.Module):
         self.pipelined = bool(on)
         return self
 
+    def check_error(self):
+        """Raise if an earlier forward failed asynchronously (a GRU hand-off
+        spin ran out: its outputs are NaN; sedx_check_error).  Call once the
+        outputs in question are complete (after a sync or a copy to the
+        host); the drivers in sedx.inference call it after every batch they
+        copy back."""
+        L = _lib.lib()
+        for nat in list(self._natives.values()):
+            _lib.check(L.sedx_check_error(nat.h), nat.h, 'asynchronous GRU failure')
+
     def _check_eval(self, mixup_lambda, timeshift):
         if self.training:
             raise RuntimeError('sedx models are inference-only: call model.eval() first '

@@ -130,7 +130,9 @@ def test_concurrent_streams_bit_identical(model, pipelined):
     GRU / head overlapping the next batch's conv stack, whose workgroups then
     claim tiles dynamically) give bit-identical outputs to one batch at a time,
     with and without the conv stacks ordered across streams
-    (sedx_set_pipelined)."""
+    (sedx_set_pipelined).  Unpipelined, the default GRU kernel (AUTO) is the
+    16-slice cooperative one, which needs 32 co-resident workgroups beside the
+    other stream's work: no NaN, no reported failure."""
     mt, m = model
     waves = [torch.from_numpy(synth.make_waveforms(32, seconds=10.0, sample_rate=16000, seed=s)).cuda()
              for s in (5, 6, 7, 8)]
@@ -146,6 +148,7 @@ def test_concurrent_streams_bit_identical(model, pipelined):
                     with torch.cuda.stream(streams[i % 2]):
                         outs.append(m(w)['framewise_output'])
                 torch.cuda.synchronize()
+                m.check_error()
                 for i, (a, b) in enumerate(zip(outs, ref)):
                     assert torch.equal(a, b), (mt, rep, i, float((a - b).abs().max()))
         finally:
@@ -213,6 +216,48 @@ def test_gru_tag_kernels_bit_identical(n_clips):
     assert np.isfinite(outs[0]).all()
     for knob in (2, 3, 4, 5):
         assert np.array_equal(outs[knob], outs[0]), knob
+
+
+@pytest.mark.parametrize('kernel,n_clips', [(0, 32), (4, 32), (0, 4), (2, 40)])
+def test_gru_spin_timeout_surfaces(kernel, n_clips):
+    """A GRU hand-off spin that runs out (forced with SEDX_TUNE_GRU_SPIN = 1
+    poll) turns that forward's outputs into NaN and is reported by
+    sedx_check_error / model.check_error() once the batch is complete — for
+    the 8- and 16-slice cooperative kernels, the small-batch VALU kernel and
+    the data-tagged one; with the default bound the same handle is clean and
+    exact again."""
+    from sedx import _lib
+    m = build(GRU).set_precision('exact')
+    _tune(m, _lib.TUNE_GRU_KERNEL, kernel)
+    wave = torch.from_numpy(synth.make_waveforms(n_clips, seconds=2.0, sample_rate=16000, seed=31)).cuda()
+    with torch.no_grad():
+        ref = m(wave)['framewise_output'].clone()
+        torch.cuda.synchronize()
+        m.check_error()
+        failed = 0
+        _tune(m, _lib.TUNE_GRU_SPIN, 1)
+        try:
+            for _ in range(3):
+                out = m(wave)['framewise_output']
+                torch.cuda.synchronize()
+                nan = bool(torch.isnan(out).any())
+                try:
+                    m.check_error()
+                    reported = False
+                except RuntimeError as e:
+                    reported = 'GRU' in str(e)
+                assert nan == reported, (nan, reported)
+                failed += nan
+        finally:
+            _tune(m, _lib.TUNE_GRU_SPIN, 0)
+            _tune(m, _lib.TUNE_GRU_KERNEL, 5)
+        assert failed >= 1
+        _tune(m, _lib.TUNE_GRU_KERNEL, kernel)
+        out = m(wave)['framewise_output']
+        torch.cuda.synchronize()
+        m.check_error()
+        _tune(m, _lib.TUNE_GRU_KERNEL, 5)
+    assert torch.equal(out, ref)
 
 
 def test_gru_exact_recurrence_is_fp32():
