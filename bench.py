@@ -747,6 +747,8 @@ def main():
     ap.add_argument('--gru-kernel', choices=list(GRU_KERNELS), default='auto',
                     help='GRU recurrence kernel (SEDX_TUNE_GRU_KERNEL; A/B runs); auto: the library default '
                          '(the 8-slice kernel on a pipelined handle, 16 slices one batch at a time)')
+    ap.add_argument('--wino-order', type=int, choices=[0, 1], default=None,
+                    help='SEDX_TUNE_WINO_ORDER (A/B runs): Winograd item order on the 512-channel layers')
     ap.add_argument('--ab-package', default=None,
                     help='A/B runs: load sedx from this package directory instead of the in-tree build '
                          '(recorded in the JSON line as "library")')
@@ -779,6 +781,8 @@ def main():
         WINO_BLOCK1 = args.wino_block1
     model = build_model(name, dev)
     model.set_tuning(_lib.TUNE_GRU_KERNEL, GRU_KERNELS[args.gru_kernel])
+    if args.wino_order is not None:
+        model.set_tuning(_lib.TUNE_WINO_ORDER, args.wino_order)
     B = args.batch
     wave = torch.from_numpy(synth.make_waveforms(B, 10.0, 16000, seed=1234 + rank)).to(dev)
 

@@ -281,10 +281,18 @@ sedx_status sedx_set_precision(sedx_handle* h, int32_t mode);
  *                         1: the same conv2 fed by a separate conv1 launch
  *                         (the activation through HBM; bit-identical to 2);
  *                         0: block 1 as the direct fused fp32 kernel.
- *  SEDX_TUNE_GRU_SPIN     bound of every GRU hand-off spin, in polls (0, the
- *                         default: 2^24).  A spin that runs out turns that
+ *  SEDX_TUNE_GRU_SPIN     bound of every GRU hand-off spin, in polls (default
+ *                         2^24 = 16777216).  A spin that runs out turns that
  *                         forward's outputs into NaN and is reported by
- *                         sedx_check_error (tests force it with a bound of 1).
+ *                         sedx_check_error (tests force it with 0: the first
+ *                         poll that finds the data not yet there fails).
+ *  SEDX_TUNE_WINO_ORDER   (winograd) 1 (default): the 512-channel layers run
+ *                         each XCD's rounds of 32 concurrent items as 4 tile
+ *                         blocks x 8 channel groups (8 weight slabs + 4 halos
+ *                         per round through the XCD's L2 instead of 16 + 2:
+ *                         b4c2 576 -> 383 MB of L2 fills per B = 32 launch,
+ *                         b4c1 288 -> 192 MB, 1 % faster); 0: tile block
+ *                         major.  Bit-identical outputs.
  *
  * Co-residency: the cooperative GRU kernels need all workgroups of a
  * (32-clip group, direction) resident at once — 8 CUs (COOP) or 16 (COOP16)
@@ -298,7 +306,8 @@ typedef enum {
   SEDX_TUNE_GRU_HANDOFF = 1,
   SEDX_TUNE_WINO_BLOCK1 = 2,
   SEDX_TUNE_MEL_MFMA = 3,
-  SEDX_TUNE_GRU_SPIN = 4
+  SEDX_TUNE_GRU_SPIN = 4,
+  SEDX_TUNE_WINO_ORDER = 5
 } sedx_tuning_knob;
 enum {
   SEDX_GRU_KERNEL_COOP = 0,

@@ -92,7 +92,8 @@ struct sedx_handle {
   int gru_handoff = SEDX_GRU_HANDOFF_AUTO;
   int wino_block1 = 2;                     // SEDX_TUNE_WINO_BLOCK1 (2: conv1 inside the Winograd launch)
   int mel_mfma = 0;                        // SEDX_TUNE_MEL_MFMA (measured slower: opt-in)
-  unsigned gru_spin = 0;                   // SEDX_TUNE_GRU_SPIN (0: the default bound)
+  unsigned gru_spin = 1u << 24;            // SEDX_TUNE_GRU_SPIN: bound of every GRU hand-off spin (polls)
+  int wino_order = 1;                      // SEDX_TUNE_WINO_ORDER (4 x 8 rounds on the 512-channel layers)
   // sedx_set_capture: copy one stage's output of every later forward
   int cap_stage = -1;
   float* cap_buf = nullptr;
@@ -404,7 +405,7 @@ sedx_status run_body(sedx_handle* h, int64_t B, const Geometry& g, float* ws, co
                         sched + i * CONV_SCHED_INTS, s);
     else if (h->precision == SEDX_PRECISION_WINOGRAD)
       launch_conv3x3_wino(c.in, iB, c.T, c.F, c.cin, c.cout, w.wu[c.idx], w.cb[c.idx], c.out, c.epi, w.zero, w.trash,
-                          s);
+                          s, h->wino_order);
     else
       launch_conv3x3(c.in, iB, c.T, c.F, c.cin, c.cout, w.wp[c.idx], w.cb[c.idx], c.out, c.epi, w.zero, s);
     const size_t px = c.epi == EPI_STORE ? (size_t)c.T * c.F : c.epi == EPI_POOL2 ? (size_t)(c.T / 2) * (c.F / 2)
@@ -636,6 +637,10 @@ sedx_status sedx_set_tuning(sedx_handle* h, int32_t knob, int32_t value) {
     case SEDX_TUNE_GRU_SPIN:
       if (value < 0) break;
       h->gru_spin = (unsigned)value;
+      return SEDX_OK;
+    case SEDX_TUNE_WINO_ORDER:
+      if (value != 0 && value != 1) break;
+      h->wino_order = value;
       return SEDX_OK;
     default:
       return fail(h, SEDX_EINVAL, "unknown tuning knob %d", (int)knob);

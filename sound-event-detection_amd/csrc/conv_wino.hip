@@ -138,7 +138,8 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
                                           const float* __restrict__ U, const float* __restrict__ bias,
                                           float* __restrict__ out, const float* __restrict__ zero16,
                                           float* __restrict__ trash, int tb_per_clip, int ngroups,
-                                          const float* __restrict__ w1, const float* __restrict__ b1) {
+                                          const float* __restrict__ w1, const float* __restrict__ b1,
+                                          int order2d = 0) {
   constexpr int ph = PH;
   using G = WinoGeom<F, TG, NG, C1>;
   constexpr int WAVES = G::WAVES;
@@ -164,14 +165,30 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
   // item decode: item -> XCD id & 7; on one XCD, tile blocks in order, each
   // with its channel groups consecutive.  Padding items (tile blocks rounded
   // up to a multiple of 8) come last on their XCD.
+  // order2d (launcher: 16+ channel groups, whole rounds of 32 items per XCD,
+  // no padding tile blocks): each round of 32 consecutive items on an XCD —
+  // the ones its 32 resident workgroups run together — is 4 tile blocks x 8
+  // channel groups instead of 2 x 16, so per round the XCD's L2 streams 8
+  // weight slabs and 4 halos instead of 16 and 2 (fewer L2 misses on the
+  // 512-channel layers; a workgroup's successive items keep their slot in
+  // the round)
   auto decode = [&](int item, int& b_, int& t0_, int& n0_) -> bool {
     const int xcd = item & 7, j = item >> 3;
-    const int jb = j / ngroups;
+    int jb, cgi;
+    if (order2d) {
+      const int idx = j & 31, r = j >> 5, ncg = ngroups >> 3;
+      const int tbg = r / ncg;
+      jb = 4 * tbg + (idx & 3);
+      cgi = 8 * (r - tbg * ncg) + (idx >> 2);
+    } else {
+      jb = j / ngroups;
+      cgi = j - jb * ngroups;
+    }
     const int tb = jb * 8 + xcd;
     if (tb >= B * tb_per_clip) return false;
     b_ = tb / tb_per_clip;
     t0_ = 2 * (tb - b_ * tb_per_clip) * G::TRW;   // first row (2 x first tile row)
-    n0_ = (j - jb * ngroups) * 32 * NG;
+    n0_ = cgi * 32 * NG;
     return true;
   };
   // this workgroup's 128 trash floats (spread: the dummy and out-of-range
@@ -677,13 +694,13 @@ template <int F, int EPI, int TG>
 __global__ __launch_bounds__(128 * TG, TG == 4 ? 1 : 2) void conv3x3_wino_kernel(
     const float* __restrict__ in, int B, int T, int Cin, int Cout, const float* __restrict__ U,
     const float* __restrict__ bias, float* __restrict__ out, const float* __restrict__ zero16,
-    float* __restrict__ trash, int tb_per_clip, int ngroups) {
+    float* __restrict__ trash, int tb_per_clip, int ngroups, int order2d) {
   if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) < TG)
     wino_body<F, EPI, TG, 0, 1, false>(in, B, T, Cin, Cout, U, bias, out, zero16, trash, tb_per_clip, ngroups,
-                                       nullptr, nullptr);
+                                       nullptr, nullptr, order2d);
   else
     wino_body<F, EPI, TG, 1, 1, false>(in, B, T, Cin, Cout, U, bias, out, zero16, trash, tb_per_clip, ngroups,
-                                       nullptr, nullptr);
+                                       nullptr, nullptr, order2d);
 }
 
 // Block 1 in one launch: conv1 (computed into the halo images) + Winograd
@@ -720,7 +737,7 @@ constexpr int WINO_ITEMS_B1 = SEDX_WINO_ITEMS_B1;
 
 template <int F, int TG>
 static void launch_wino_w(const float* in, int B, int T, int Cin, int Cout, const float* U, const float* bias,
-                          float* out, int epi, const float* zero16, float* trash, hipStream_t s) {
+                          float* out, int epi, const float* zero16, float* trash, int order, hipStream_t s) {
   using G = WinoGeom<F, TG>;
   // tile rows of a clip: POOL2 drops an odd last row (floor), the others keep it
   const int trows = epi == EPI_POOL2 ? T / 2 : (T + 1) / 2;
@@ -740,12 +757,17 @@ static void launch_wino_w(const float* in, int B, int T, int Cin, int Cout, cons
   const int64_t per = (nitems + WINO_ITEMS - 1) / WINO_ITEMS;
   const int64_t nwg = std::min<int64_t>(nitems, std::max<int64_t>(std::max<int64_t>(8, resident), (per + 7) / 8 * 8));
   dim3 grid((unsigned)nwg);
+  // 4 x 8 rounds: 16+ channel groups in whole groups of 8, whole groups of 4
+  // tile blocks per XCD with no padding, and a grid of whole 32-item rounds
+  // per XCD (a workgroup keeps its slot in the round from item to item)
+  const int order2d = order && ngroups >= 16 && ngroups % 8 == 0 && tblocks % 32 == 0 && nwg % 256 == 0 &&
+                      (nitems / 8) % 32 == 0;
 #define SEDX_WG_LAUNCH(E)                                                                              \
   {                                                                                                    \
     auto* k_ = conv3x3_wino_kernel<F, E, TG>;                                                          \
     if (!launch_info(reinterpret_cast<const void*>(k_), G::THREADS, G::LDS_BYTES).ok) return;          \
     hipLaunchKernelGGL(k_, grid, dim3(G::THREADS), G::LDS_BYTES, s, in, B, T, Cin, Cout, U, bias, out, zero16, \
-                       trash, tb_per_clip, ngroups);                                                   \
+                       trash, tb_per_clip, ngroups, order2d);                                          \
     return;                                                                                            \
   }
   if constexpr (F == 8) {
@@ -764,20 +786,21 @@ static void launch_wino_w(const float* in, int B, int T, int Cin, int Cout, cons
 // else 1: the same per-wave work, bit-identical outputs
 template <int F>
 static void launch_wino_f(const float* in, int B, int T, int Cin, int Cout, const float* U, const float* bias,
-                          float* out, int epi, const float* zero16, float* trash, hipStream_t s) {
+                          float* out, int epi, const float* zero16, float* trash, int order, hipStream_t s) {
   const int64_t ncu = wino_device_cus();
   const int trows = epi == EPI_POOL2 ? T / 2 : (T + 1) / 2;
   auto wgs = [&](int trw) { return (int64_t)B * ((trows + trw - 1) / trw) * (Cout / 32); };
   if (wgs(WinoGeom<F, 4>::TRW) >= ncu)
-    launch_wino_w<F, 4>(in, B, T, Cin, Cout, U, bias, out, epi, zero16, trash, s);
+    launch_wino_w<F, 4>(in, B, T, Cin, Cout, U, bias, out, epi, zero16, trash, order, s);
   else if (wgs(WinoGeom<F, 2>::TRW) >= ncu)
-    launch_wino_w<F, 2>(in, B, T, Cin, Cout, U, bias, out, epi, zero16, trash, s);
+    launch_wino_w<F, 2>(in, B, T, Cin, Cout, U, bias, out, epi, zero16, trash, order, s);
   else
-    launch_wino_w<F, 1>(in, B, T, Cin, Cout, U, bias, out, epi, zero16, trash, s);
+    launch_wino_w<F, 1>(in, B, T, Cin, Cout, U, bias, out, epi, zero16, trash, order, s);
 }
 
 void launch_conv3x3_wino(const float* in, int B, int T, int F, int Cin, int Cout, const float* U,
-                         const float* bias, float* out, int epi, const float* zero16, float* trash, hipStream_t s) {
+                         const float* bias, float* out, int epi, const float* zero16, float* trash, hipStream_t s,
+                         int order) {
   // halo lanes outside the clip step through the zero block by the chunk's
   // channel offset: it must hold Cin + 4 floats
   if (Cin % 8 != 0 || Cin < 32 || Cout % 32 != 0 || B <= 0 || T <= 0 || Cin + 4 > ZERO_BLOCK_FLOATS)
@@ -795,10 +818,10 @@ void launch_conv3x3_wino(const float* in, int B, int T, int F, int Cin, int Cout
     const float* in_s = in + b0 * in_clip;
     float* out_s = out + b0 * out_clip;
     switch (F) {
-      case 64: launch_wino_f<64>(in_s, bs, T, Cin, Cout, U, bias, out_s, epi, zero16, trash, s); break;
-      case 32: launch_wino_f<32>(in_s, bs, T, Cin, Cout, U, bias, out_s, epi, zero16, trash, s); break;
-      case 16: launch_wino_f<16>(in_s, bs, T, Cin, Cout, U, bias, out_s, epi, zero16, trash, s); break;
-      case 8: launch_wino_f<8>(in_s, bs, T, Cin, Cout, U, bias, out_s, epi, zero16, trash, s); break;
+      case 64: launch_wino_f<64>(in_s, bs, T, Cin, Cout, U, bias, out_s, epi, zero16, trash, order, s); break;
+      case 32: launch_wino_f<32>(in_s, bs, T, Cin, Cout, U, bias, out_s, epi, zero16, trash, order, s); break;
+      case 16: launch_wino_f<16>(in_s, bs, T, Cin, Cout, U, bias, out_s, epi, zero16, trash, order, s); break;
+      case 8: launch_wino_f<8>(in_s, bs, T, Cin, Cout, U, bias, out_s, epi, zero16, trash, order, s); break;
       default: return note_launch_error(hipErrorInvalidValue);
     }
   }

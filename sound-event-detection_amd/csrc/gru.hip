@@ -84,9 +84,9 @@ constexpr int GRU_HV_LD = 260;        // Hv row stride (floats): 8 rows fit the 
 static_assert(GRU_VALU_CLIPS * GRU_HV_LD <= 16 * 32 * 4 * 4, "Hv inside Aimg");
 // VALU granules [2 pairs][2 parities][clips][256] u64 at the start of the exchange space
 static_assert(2 * 2 * GRU_VALU_CLIPS * 256 * 8 <= 8 * 2 * 32 * 256 * 4, "granules inside X");
-// bound of every hand-off spin (polls); sedx_set_tuning(SEDX_TUNE_GRU_SPIN)
-// lowers it (tests force a timeout with it)
-constexpr unsigned GRU_SPIN_DEFAULT = 1u << 24;
+// bound of every hand-off spin, in polls: the handle's SEDX_TUNE_GRU_SPIN
+// (2^24 by default; tests force a timeout with 0 — fail at the first poll
+// that finds the data not there yet)
 
 struct GruSync {                      // zeroed every launch
   unsigned err;
@@ -797,7 +797,6 @@ static void launch_gru_tag(const float* G, int B, int T, const float* whh, const
 void launch_gru_coop(const float* G, int B, int T, const float* whh, const float* bhh, float* H,
                      void* ws, bool exact, bool allow_fast, int variant, unsigned* host_err, unsigned spin,
                      hipStream_t s) {
-  if (spin == 0) spin = GRU_SPIN_DEFAULT;
   GruSync* sync = static_cast<GruSync*>(ws);
   const size_t sync_bytes = (sizeof(GruSync) + 255) & ~size_t(255);
   float* X = reinterpret_cast<float*>(static_cast<char*>(ws) + sync_bytes);

@@ -118,9 +118,12 @@ void launch_conv3x3(const float* in, int B, int T, int F, int Cin, int Cout,
 // launch_conv1_nhwc).
 // zero16 here: >= Cin + 4 floats of zeros; trash: >= 64 x 128 floats of device scratch; out-of-range epilogue stores land
 // there (every store is issued, so the persistent kernel's counted waits are exact).
+// order: 1 = the 4 tile blocks x 8 channel groups round order on the
+// 512-channel layers where it applies (SEDX_TUNE_WINO_ORDER), 0 = tile block
+// major.  Same per-item work either way: bit-identical outputs.
 void launch_conv3x3_wino(const float* in, int B, int T, int F, int Cin, int Cout,
                          const float* U, const float* bias, float* out, int epi,
-                         const float* zero16, float* trash, hipStream_t s);
+                         const float* zero16, float* trash, hipStream_t s, int order = 0);
 void pack_conv_wino(const double* wf, int Cin, int Cout, float* U);   // U: Cin * Cout * 16 floats
 // block 1 as one Winograd launch: conv1 (w1 [64][9] folded, b1 [64], ReLU)
 // computed into conv2's halo images in LDS, conv2 (U of block 1's conv2) +
@@ -269,7 +272,7 @@ size_t gru_coop_workspace_bytes(int B);
 // bounded hand-off spin times out (outputs of that launch are then NaN).
 // variant (exact, B > 8): 2 the 32-clip flag hand-off kernel (default; x3
 // always), 0 the 16-clip data-tagged kernel with 16 slices, 1 with 8 slices.
-// spin: bound of every hand-off spin in polls (0: the default, 2^24).
+// spin: bound of every hand-off spin in polls (the handle's SEDX_TUNE_GRU_SPIN, 2^24 by default).
 void launch_gru_coop(const float* G, int B, int T, const float* whh, const float* bhh, float* H,
                      void* ws, bool exact, bool allow_fast, int variant, unsigned* host_err, unsigned spin,
                      hipStream_t s);

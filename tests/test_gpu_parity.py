@@ -220,8 +220,8 @@ def test_gru_tag_kernels_bit_identical(n_clips):
 
 @pytest.mark.parametrize('kernel,n_clips', [(0, 32), (4, 32), (0, 4), (2, 40)])
 def test_gru_spin_timeout_surfaces(kernel, n_clips):
-    """A GRU hand-off spin that runs out (forced with SEDX_TUNE_GRU_SPIN = 1
-    poll) turns that forward's outputs into NaN and is reported by
+    """A GRU hand-off spin that runs out (forced with SEDX_TUNE_GRU_SPIN = 0
+    polls: any wait that is not satisfied at once) turns that forward's outputs into NaN and is reported by
     sedx_check_error / model.check_error() once the batch is complete — for
     the 8- and 16-slice cooperative kernels, the small-batch VALU kernel and
     the data-tagged one; with the default bound the same handle is clean and
@@ -235,9 +235,9 @@ def test_gru_spin_timeout_surfaces(kernel, n_clips):
         torch.cuda.synchronize()
         m.check_error()
         failed = 0
-        _tune(m, _lib.TUNE_GRU_SPIN, 1)
+        _tune(m, _lib.TUNE_GRU_SPIN, 0)
         try:
-            for _ in range(3):
+            for _ in range(4):
                 out = m(wave)['framewise_output']
                 torch.cuda.synchronize()
                 nan = bool(torch.isnan(out).any())
@@ -249,7 +249,7 @@ def test_gru_spin_timeout_surfaces(kernel, n_clips):
                 assert nan == reported, (nan, reported)
                 failed += nan
         finally:
-            _tune(m, _lib.TUNE_GRU_SPIN, 0)
+            _tune(m, _lib.TUNE_GRU_SPIN, 1 << 24)
             _tune(m, _lib.TUNE_GRU_KERNEL, 5)
         assert failed >= 1
         _tune(m, _lib.TUNE_GRU_KERNEL, kernel)
@@ -695,6 +695,25 @@ def test_winograd_block1_knob(wino_block1):
     odd = synth.make_waveforms(3, seconds=7.33, sample_rate=16000, seed=5)
     ref_o = O.forward(O.full_state(synth.make_state_dict(GRU, seed=SEEDS[GRU])), GRU, wave=odd)
     assert err(run(m, odd)['framewise_output'], ref_o['framewise_output'].numpy()) <= 2e-5
+
+
+def test_wino_order_bit_identical():
+    """SEDX_TUNE_WINO_ORDER 1 (4 tile blocks x 8 channel groups per round of
+    32 items on the 512-channel layers) runs the same items with the same
+    arithmetic: bit-identical to the default order (B = 32 x 10 s, where it
+    applies, and B = 3, where the launcher keeps the default)."""
+    from sedx import _lib
+    m = build(GRU).set_precision('winograd')
+    for n in (32, 3):
+        wave = torch.from_numpy(synth.make_waveforms(n, seconds=10.0, sample_rate=16000, seed=40 + n)).cuda()
+        outs = []
+        for order in (0, 1):
+            _tune(m, _lib.TUNE_WINO_ORDER, order)
+            with torch.no_grad():
+                outs.append(m(wave)['framewise_output'].clone())
+        _tune(m, _lib.TUNE_WINO_ORDER, 0)
+        assert torch.isfinite(outs[0]).all()
+        assert torch.equal(outs[0], outs[1]), n
 
 
 def test_wino_block1_knob_errors():
