@@ -414,6 +414,11 @@ def stage_times_isolated(model, wave, dev, reps):
 # tools/pmc_summary.py; FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE),
 # committed under profiles/.
 PROFILE_SUMMARY = os.path.join(REPO, 'profiles', 'r03d_kernel_summary.json')
+# the same passes over the config-4 leg (bench.py --mode gamma: B = 32 x 10 s
+# @ 32 kHz, T = 994 frames)
+GAMMA_PROFILE_SUMMARY = os.path.join(REPO, 'profiles', 'r03c_config4_kernel_summary.json')
+GAMMA_KERNELS = ('sedx::gamma_init_kernel', 'sedx::gamma_spec_kernel<2048>', 'sedx::gamma_erb_kernel',
+                 'sedx::gamma_quant_kernel')
 
 
 # block 1's conv1 (Cin 1 -> 64) computed inside the b1c2 launch (winograd
@@ -440,11 +445,11 @@ def conv_kernel_name(stage, precision):
     return 'sedx::conv3x3_kernel<%d, %d, %d, %s, 8, 64>' % (F, bn, epi, 'true' if stage == 'b1c2' else 'false')
 
 
-def profiled(kernel):
+def profiled(kernel, summary=PROFILE_SUMMARY):
     """(HBM bytes per launch, rocprofv3 average ms, MFMA busy fraction,
     effective clock GHz) of ``kernel`` from the committed summary."""
     try:
-        with open(PROFILE_SUMMARY) as f:
+        with open(summary) as f:
             v = json.load(f).get(kernel, {})
     except (OSError, ValueError):
         return None, None, None, None
@@ -454,7 +459,7 @@ def profiled(kernel):
             round(util, 4) if util else None, round(clk, 3) if clk else None)
 
 
-def roofline(stage_ms, B, precision, T=1001, iso_ms=None):
+def roofline(stage_ms, B, precision, T=1001, iso_ms=None, summary=None):
     """MFMA roofline of the dominant conv launch.
 
     achieved = FLOPs the launch executes on the matrix pipe (direct conv:
@@ -469,7 +474,8 @@ def roofline(stage_ms, B, precision, T=1001, iso_ms=None):
     direct-conv-equivalent rate (what a direct conv would need for this time;
     can exceed the peak for Winograd) as ``direct_conv_equiv_tflops``.
     Profile-derived fields (traffic, rocprof time, MFMA busy) come from the
-    committed summary of the B=32, 10 s shapes only."""
+    committed summary of the same shapes: ``summary`` (config 4's passes), or
+    for the B=32, 10 s @ 16 kHz shapes PROFILE_SUMMARY."""
     conv = {s_: stage_ms[s_] for s_ in CONV_STAGES}
     dom = max(conv, key=conv.get)
     wino = precision == 'winograd'
@@ -486,7 +492,9 @@ def roofline(stage_ms, B, precision, T=1001, iso_ms=None):
     total_direct = sum(conv_flops(st, B, T) for st in CONV_STAGES) + conv1
     conv_ms = sum(conv.values()) + stage_ms.get('b1c1', 0.0)
     kname = conv_kernel_name(dom, precision)
-    traffic, rocprof_ms, mfma_util, clock = profiled(kname) if (B, T) == (32, 1001) else (None,) * 4
+    if summary is None and (B, T) == (32, 1001):
+        summary = PROFILE_SUMMARY
+    traffic, rocprof_ms, mfma_util, clock = profiled(kname, summary) if summary else (None,) * 4
     direct = flops / mul[dom]
     out = {'bound': 'mfma', 'kernel': '%s (%s)' % (kname, dom),
            'arith': {'exact': 'fp32 MFMA v_mfma_f32_32x32x2_f32 (f32 in, f32 acc)',
@@ -496,7 +504,7 @@ def roofline(stage_ms, B, precision, T=1001, iso_ms=None):
            'achieved': round(achieved, 2), 'peak': round(peak, 1), 'unit': 'TFLOP/s',
            'frac': round(achieved / peak, 4),
            'traffic': traffic, 'traffic_unit': 'bytes/launch (HBM, rocprofv3 PMC)',
-           'traffic_source': os.path.relpath(PROFILE_SUMMARY, REPO) if traffic is not None else None,
+           'traffic_source': os.path.relpath(summary, REPO) if traffic is not None else None,
            'flops_per_launch': flops, 'avg_launch_ms': round(t, 4),
            'timing': ('avg_launch_ms: HIP events on the launch stream, one batch at a time, measured live in this '
                       'run (sedx_set_profiling 1)' if t_iso else
@@ -511,7 +519,7 @@ def roofline(stage_ms, B, precision, T=1001, iso_ms=None):
            'frac_rocprof': round(flops / (rocprof_ms * 1e-3) / 1e12 / peak, 4) if rocprof_ms else None,
            'mfma_busy_frac_pmc': mfma_util, 'clock_ghz_pmc': clock,
            'rocprof_source': ('rocprofv3 --kernel-trace --stats of bench.py --streams 1 --no-side, %s'
-                              % os.path.relpath(PROFILE_SUMMARY, REPO)) if rocprof_ms else None,
+                              % os.path.relpath(summary, REPO)) if rocprof_ms else None,
            # the reference's algorithmic FLOPs (the direct conv's)
            # over the same time: a rate, not a roofline fraction (> peak for
            # Winograd, which executes 16/36 of the multiplies)
@@ -579,15 +587,25 @@ def gamma_leg(args, dev, precision):
     T = 994
     flops = B * (T * (5.0 * 1024 * 10 + 8.0 * 1025) + 2.0 * 64 * 1025 * T)   # FFT + unpack/|X| + ERB product
     bytes_ = B * (320000 * 4 + 64 * T * 4)
+    # HBM bytes per batch of the frontend's launches (PMC passes of --mode gamma)
+    prof = [profiled(k, GAMMA_PROFILE_SUMMARY) for k in GAMMA_KERNELS] if B == 32 else []
+    traffic = sum(p[0] for p in prof) if prof and all(p[0] is not None for p in prof) else None
+    rocprof_fe = sum(p[1] for p in prof) if prof and all(p[1] is not None for p in prof) else None
     return {'workload': 'Cnn_9layers_Gru_FrameAtt gammatone 32k, %d x 10 s @ 32 kHz clips per step '
                         '(float64 gammatone features + forward)' % B,
             'value': round(value, 2), 'unit': 'clips/s', 'dtype': DTYPE[precision] + '; gammatone frontend f64',
             'ms_per_step': round(elapsed / args.steps * 1e3, 4),
-            'roofline': roofline(stage_ms, B, precision, T=T, iso_ms=iso),
+            'roofline': roofline(stage_ms, B, precision, T=T, iso_ms=iso,
+                                 summary=GAMMA_PROFILE_SUMMARY if B == 32 else None),
             'gamma_frontend': {'ms_per_batch': round(fe_ms, 4), 'bound': 'fp64',
                                'achieved': round(flops / (fe_ms * 1e-3) / 1e12, 3), 'peak': PEAK_FP64_TF,
                                'unit': 'TFLOP/s (f64)', 'frac': round(flops / (fe_ms * 1e-3) / 1e12 / PEAK_FP64_TF, 4),
                                'hbm_gbps_algorithmic': round(bytes_ / (fe_ms * 1e-3) / 1e9, 1),
+                               'bytes_algorithmic': bytes_, 'traffic': traffic,
+                               'traffic_unit': 'bytes/batch (HBM, rocprofv3 PMC, %s)' % ', '.join(GAMMA_KERNELS),
+                               'ms_per_batch_rocprof': round(rocprof_fe, 4) if rocprof_fe else None,
+                               'traffic_source': (os.path.relpath(GAMMA_PROFILE_SUMMARY, REPO)
+                                                  if traffic is not None else None),
                                'note': 'algorithmic f64 FLOPs: 5 N log2 N complex FFT (N=1024) + unpack '
                                        '+ 64 x 1025 ERB product per frame; bytes: audio in + features out'}}
 

@@ -102,6 +102,44 @@ struct WinoGeom {
   static_assert(!C1 || (F == 64 && PLP <= 64 * WAVES && UX <= WAVES && NBUF == 3), "C1: block 1 (64 bins), a conv1 group per wave");
 };
 
+// Diagnostic builds only (tools/wino_b1_bench.cpp, tools/gpu_r04d.sh; never
+// the library): SEDX_WINO_STAMPS accumulates per-wave s_memtime intervals by
+// phase, from every wave of every 16th workgroup, into g_wino_stamps:
+//   [0] prologue  [1] item top (chunk 0 reads + transform, next item's DMA
+//   sources)  [2] chunk steps (MFMAs with the next chunk's LDS reads,
+//   transform and C1's conv1 interleaved)  [3] barrier waits  [4] DMA issue
+//   (+ C1's X0 tile)  [5] C1's window load  [6] epilogue  [7] whole wave
+//   [8] waves sampled
+// SEDX_WINO_ABL (a bit mask) removes one piece of work — results WRONG,
+// timing only: 1 conv1, 2 the input transform, 4 the patch LDS reads, 8 the U
+// LDS reads, 16 the DMAs of the chunk operands.
+#ifndef SEDX_WINO_ABL
+#define SEDX_WINO_ABL 0
+#endif
+#ifdef SEDX_WINO_STAMPS
+__device__ unsigned long long g_wino_stamps[16];
+#define WS_DECL                                      \
+  unsigned long long ws_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; \
+  unsigned long long ws_t = __builtin_amdgcn_s_memtime();  \
+  const unsigned long long ws_t0 = ws_t;
+#define WS_MARK(i)                                           \
+  {                                                          \
+    const unsigned long long n_ = __builtin_amdgcn_s_memtime(); \
+    ws_acc[i] += n_ - ws_t;                                  \
+    ws_t = n_;                                               \
+  }
+#define WS_FLUSH()                                                           \
+  if (lane == 0 && (blockIdx.x & 15) == 0) {                                 \
+    ws_acc[7] = __builtin_amdgcn_s_memtime() - ws_t0;                        \
+    for (int i_ = 0; i_ < 8; ++i_) atomicAdd(&g_wino_stamps[i_], ws_acc[i_]); \
+    atomicAdd(&g_wino_stamps[8], 1ull);                                      \
+  }
+#else
+#define WS_DECL
+#define WS_MARK(i)
+#define WS_FLUSH()
+#endif
+
 // raw workgroup barrier behind "this wave's DMAs older than its N youngest
 // VMEM ops landed, its LDS operations done" (__syncthreads() would drain
 // every DMA in flight); N = VM x y for y = min(younger, Y) chunks in flight
@@ -156,6 +194,7 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  WS_DECL
   // (tile group, channel group) of the wave: waves q, q + NGW are its
   // position halves 0, 1 (one SIMD)
   const int tg = wv % TG;
@@ -250,7 +289,7 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
             (uint32_t)(size_t)(__attribute__((address_space(3))) float*)(smem + buf_ * G::BUF + dlds[k]);
         const float* src = is_w(k) ? U + 2 * n0_ + off[k] + (int64_t)chunk_ * (64 * Cout)
                                      : (off[k] >= 0 ? in + off[k] + chunk_ * KC : zero16);
-        sedx_glds16(src, __builtin_amdgcn_readfirstlane(m0_));
+        if constexpr (!(SEDX_WINO_ABL & 16)) sedx_glds16(src, __builtin_amdgcn_readfirstlane(m0_));
       }
     }
     asm volatile("" ::: "memory");
@@ -272,7 +311,7 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
         const uint32_t m0_ =
             (uint32_t)(size_t)(__attribute__((address_space(3))) float*)(smem + buf_ * G::BUF + dlds[k]);
         const int64_t stp = is_w(k) ? (int64_t)64 * Cout : KC;
-        sedx_glds16(dptr[k] + chunk_ * stp, __builtin_amdgcn_readfirstlane(m0_));
+        if constexpr (!(SEDX_WINO_ABL & 16)) sedx_glds16(dptr[k] + chunk_ * stp, __builtin_amdgcn_readfirstlane(m0_));
       }
     }
     asm volatile("" ::: "memory");
@@ -376,10 +415,25 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
 #pragma unroll
     for (int i = 0; i < 3; ++i)
 #pragma unroll
-      for (int jj = 0; jj < 4; ++jj)
-        pd[i][jj] = *reinterpret_cast<const float2*>(sm + a_base + a_off(ph + i, jj));
+      for (int jj = 0; jj < 4; ++jj) {
+        if constexpr (SEDX_WINO_ABL & 4) {
+          float2 z = make_float2((float)i, (float)jj);
+          asm volatile("" : "+v"(z.x), "+v"(z.y));
+          pd[i][jj] = z;
+        } else {
+          pd[i][jj] = *reinterpret_cast<const float2*>(sm + a_base + a_off(ph + i, jj));
+        }
+      }
 #pragma unroll
-    for (int p = 0; p < 8; ++p) un[p] = *reinterpret_cast<const float2*>(sm + b_base + p * 128 * NG);
+    for (int p = 0; p < 8; ++p) {
+      if constexpr (SEDX_WINO_ABL & 8) {
+        float2 z = make_float2((float)p, 1.0f);
+        asm volatile("" : "+v"(z.x), "+v"(z.y));
+        un[p] = z;
+      } else {
+        un[p] = *reinterpret_cast<const float2*>(sm + b_base + p * 128 * NG);
+      }
+    }
   };
   // V rows 2 ph, 2 ph + 1 of B^T d B from patch rows ph .. ph + 2
   //   ph 0: d0 - d2, d1 + d2      ph 1: d2 - d1, d1 - d3
@@ -393,7 +447,10 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
         for (int jj = 0; jj < 4; ++jj) x[i][jj] = ks ? pd[i][jj].y : pd[i][jj].x;
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) {
-        if constexpr (PH == 0) {
+        if constexpr (SEDX_WINO_ABL & 2) {
+          vn[ks][jj] = x[0][jj];
+          vn[ks][4 + jj] = x[1][jj];
+        } else if constexpr (PH == 0) {
           vn[ks][jj] = x[0][jj] - x[2][jj];
           vn[ks][4 + jj] = x[1][jj] + x[2][jj];
         } else {
@@ -401,8 +458,10 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
           vn[ks][4 + jj] = x[0][jj] - x[2][jj];
         }
       }
-      wino_bt4(&vn[ks][0]);
-      wino_bt4(&vn[ks][4]);
+      if constexpr (!(SEDX_WINO_ABL & 2)) {
+        wino_bt4(&vn[ks][0]);
+        wino_bt4(&vn[ks][4]);
+      }
     }
     // pin V here: otherwise the compiler sinks each value's transform to the
     // MFMA that consumes it (next chunk), a VALU -> MFMA chain in front of
@@ -426,7 +485,7 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
     float2 pd[3][4];
     issue_reads(nbuf, pd, un);
     transform(pd, vn);
-    if constexpr (C1) conv1(cc, cb);
+    if constexpr (C1 && !(SEDX_WINO_ABL & 1)) conv1(cc, cb);
     // (measured slower: every LDS read ahead of the MFMAs, -10 %: the
     // transform then waits at the end of the chunk with nothing to overlap;
     // C1's conv1 beside the first MFMAs with its weights loaded a chunk
@@ -481,6 +540,7 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
   }
   // chunk 0 landed: younger chunks 1 .. NB - 1 and the S stores may be in flight
   wino_bar<G::VM_MIN, NB - 1, S>(NB - 1);
+  WS_MARK(0)
 
   // ---- epilogue pieces.  Register r of every position tile = MFMA row
   // m = (r & 3) + 8 (r >> 2) + 4 khalf (tile 32 tg + m), column lane & 31.
@@ -528,6 +588,7 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
       issue_reads(buf, pd, ua);
       transform(pd, va);
     }
+    WS_MARK(1)
 #pragma unroll
     for (int p = 0; p < 8; ++p)
 #pragma unroll
@@ -554,25 +615,34 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
       // C1: conv1 runs two chunks ahead — chunk + 2 into b2, chunk + 3 into
       // buf; over the last pair those are the next item's chunks 0 and 1,
       // from its window (its X0 tile was DMA'd with chunk nchunks - 1)
+      WS_MARK(2)
       if constexpr (MID) {
         wino_bar_n<G::VM_MIN * (NB - 2) + (FIRST ? S : 0)>();
+        WS_MARK(3)
         dma_cur(chunk + NB, buf);
       } else {
         wino_bar<G::VM_MIN, NB - 2, FIRST ? S : 0>(has_next ? NB - 2 : max(0, min(NB - 2, nchunks - chunk - 2)));
+        WS_MARK(3)
         issue(chunk + NB, buf);
         // (without a next item: the current item's tile again, unused — the
         // pipeline stays branch-free; so are the window and conv1 below)
-        if constexpr (C1 && !LAST) x0_dma(has_next ? nb_ : b, has_next ? nt0 : t0, xpar ^ 1);
+        if constexpr (C1 && !LAST && !(SEDX_WINO_ABL & 16)) x0_dma(has_next ? nb_ : b, has_next ? nt0 : t0, xpar ^ 1);
       }
+      WS_MARK(4)
       if constexpr (C1 && LAST) load_window(has_next ? nt0 : t0, xpar ^ 1);
+      WS_MARK(5)
       step(va, ua, b1, vb, ubv, C1 ? (LAST ? 0 : chunk + 2) : -1, b2);
+      WS_MARK(2)
       if constexpr (MID) {
         wino_bar_n<G::VM_MIN * (NB - 2) + (FIRST ? S : 0)>();
+        WS_MARK(3)
         dma_cur(chunk + 1 + NB, b1);
       } else {
         wino_bar<G::VM_MIN, NB - 2, FIRST ? S : 0>(has_next ? NB - 2 : max(0, min(NB - 2, nchunks - chunk - 3)));
+        WS_MARK(3)
         issue(chunk + 1 + NB, b1);
       }
+      WS_MARK(4)
       if constexpr (!LAST) {
         step(vb, ubv, b2, va, ua, C1 ? chunk + 3 : -1, buf);
       } else {
@@ -580,7 +650,7 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
         for (int p = 0; p < 8; ++p) acc[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(vb[0][p], ubv[p].x, acc[p], 0, 0, 0);
 #pragma unroll
         for (int p = 0; p < 8; ++p) acc[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(vb[1][p], ubv[p].y, acc[p], 0, 0, 0);
-        if constexpr (C1) conv1(1, buf);
+        if constexpr (C1 && !(SEDX_WINO_ABL & 1)) conv1(1, buf);
       }
       buf = b2;
     };
@@ -591,6 +661,7 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
       pair(chunk, std::false_type{}, std::false_type{}, std::true_type{});
     pair(nchunks - 4, std::false_type{}, std::false_type{}, std::false_type{});
     pair(nchunks - 2, std::false_type{}, std::true_type{}, std::false_type{});
+    WS_MARK(2)
 
     // ---- epilogue ----
     const int tr0 = t0 / 2;
@@ -674,6 +745,7 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
         }
       }
     }
+    WS_MARK(6)
     if (!has_next) break;
     // the partner's reads of this item's exchange slots finish before the
     // next item's epilogue overwrites them: many barriers lie between
@@ -688,6 +760,7 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
       ptrs(doff, n0);
     }
   }
+  WS_FLUSH()
 }
 
 template <int F, int EPI, int TG>
@@ -922,6 +995,18 @@ void launch_conv1_nhwc(const float* x0, int B, int T, const float* w1, const flo
   if (B <= 0 || T <= 0 || blocks > INT32_MAX || (int64_t)T * 64 > INT32_MAX) return note_launch_error(hipErrorInvalidValue);
   hipLaunchKernelGGL(conv1_nhwc_kernel, dim3((unsigned)blocks), dim3(256), 0, s, x0, T, rb, w1, b1, out);
 }
+
+#ifdef SEDX_WINO_STAMPS
+// diagnostic builds: the stamp sums (host side, this translation unit)
+void wino_stamps_rw(unsigned long long* h, bool reset) {
+  if (reset) {
+    static const unsigned long long z[16] = {};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_wino_stamps), z, sizeof(z));
+  } else {
+    (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_wino_stamps), 16 * sizeof(unsigned long long));
+  }
+}
+#endif
 
 // U = G g G^T per (input channel, output channel) in float64 from the
 // BN-folded weights, rounded once to fp32, packed [Cin/4][16 p][2 h][Cout][2 ks]

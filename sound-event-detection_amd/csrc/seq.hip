@@ -252,17 +252,24 @@ void launch_gru(const float* G, int B, int T, const float* whhT, const float* bh
 // (lane quarter g = lane & 3 owns dims 16g..16g+15), so a row's serial dot /
 // p.v chain is 16 long instead of 64 and a single clip fills 32x more
 // threads.  q.k = the 4 partial dots summed in a fixed order (quad shuffles);
-// exact two-pass softmax as before.
+// exact two-pass softmax as before.  XCD-aware grid: the nqb query blocks of
+// one (clip, head) are workgroups n, n + 8, ... of one XCD, so that head's
+// K / V rows (read by every query block, K twice) come from HBM once per
+// clip-head instead of once per query block (round-robin dispatch put the
+// blocks of a head on different XCDs: 111 MB per B = 32 launch against 33 MB
+// algorithmic, profiles/r03c_config3_kernel_summary.md).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(128) void mha_kernel(const float* __restrict__ QKV, int T,
+__global__ __launch_bounds__(128) void mha_kernel(const float* __restrict__ QKV, int T, int nqb,
                                                   float* __restrict__ O) {
   constexpr int KC = 64, DG = 16;
   __shared__ float Ks[KC][68];
   __shared__ float Vs[KC][68];
-  const int bh = blockIdx.y;
+  const int n = blockIdx.x, j = n >> 3;
+  const int qb = j % nqb;
+  const int bh = (j / nqb) * 8 + (n & 7);   // heads per clip = 8: B * 8 is a multiple of the 8 XCDs
   const int b = bh >> 3, head = bh & 7;
   const int g = threadIdx.x & 3;
-  const int qi = blockIdx.x * 32 + (threadIdx.x >> 2);
+  const int qi = qb * 32 + (threadIdx.x >> 2);
   const bool valid = qi < T;
   const float* base = QKV + (int64_t)b * T * 1536;
   float q[DG], o[DG];
@@ -318,7 +325,9 @@ __global__ __launch_bounds__(128) void mha_kernel(const float* __restrict__ QKV,
 }
 
 void launch_mha(const float* QKV, int B, int T, float* O, hipStream_t s) {
-  hipLaunchKernelGGL(mha_kernel, dim3((T + 31) / 32, B * 8), dim3(128), 0, s, QKV, T, O);
+  const int nqb = (T + 31) / 32;
+  if (B <= 0 || T <= 0 || (int64_t)nqb * B * 8 > INT32_MAX) return note_launch_error(hipErrorInvalidValue);
+  hipLaunchKernelGGL(mha_kernel, dim3((unsigned)(nqb * B * 8)), dim3(128), 0, s, QKV, T, nqb, O);
 }
 
 // ---------------------------------------------------------------------------
