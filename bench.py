@@ -439,8 +439,8 @@ def conv_kernel_name(stage, precision):
     if precision == 'winograd' and stage == 'b1c2' and WINO_BLOCK1 == 2:
         return 'sedx::wino_block1_kernel<2>'
     if precision == 'winograd' and stage in wino_stages():
-        # 4 tile groups (8 waves) at the bench shapes
-        return 'sedx::conv3x3_wino_kernel<%d, %d, 4>' % (F, epi)
+        # 2 tile groups x 64 channels (8 row waves) at the bench shapes
+        return 'sedx::conv3x3_wino_kernel<%d, %d, 2, 2>' % (F, epi)
     # exact: 8-wave 64x64 wave tiles at the bench shapes (4-wave / 32x32 only for small grids)
     return 'sedx::conv3x3_kernel<%d, %d, %d, %s, 8, 64>' % (F, bn, epi, 'true' if stage == 'b1c2' else 'false')
 

@@ -12,21 +12,23 @@
 // (Lavin & Gray 2016; B^T = [1 0 -1 0; 0 1 1 0; 0 -1 1 0; 0 1 0 -1],
 // G = [1 0 0; 1/2 1/2 1/2; 1/2 -1/2 1/2; 0 0 1], A^T = [1 1 1 0; 0 1 -1 -1]).
 //
-// Waves: a tile group = 32 tiles x 32 output channels, computed by a PAIR of
-// waves on one SIMD, wave half h owning the 8 positions of V rows i = 2h,
-// 2h+1 (8 MFMA accumulator tiles, 128 registers): two waves per SIMD, so one
-// wave's transform VALU, LDS reads and barrier wait run under its partner's
-// MFMAs (with all 16 positions in one wave — 256 accumulators, one wave per
-// SIMD — the matrix pipe idled through each of them: 0.60 of peak).
-// The input transform is in-lane: lane (tile m, k-half kh) reads the 3 patch
-// rows its V rows need (12 pixels, channels 2 kh and 2 kh + 1 of a 4-channel
-// chunk: 12 ds_read_b64) and its 8 transformed values per channel ARE its A
-// fragments — V never exists in LDS or HBM.  The output transform too: a
-// lane's register r holds the same (tile, channel) in all of its 8 position
-// tiles, so each wave reduces its rows to a partial 2x2 Y in registers; the
-// two halves meet once, in the epilogue, through LDS (each finishes half of
-// the registers, summing Y_0 + Y_1 in that order).
-// A workgroup is TG tile groups (2 TG waves) x 32 channels; per 4-channel
+// Waves (round 4: "row waves"): a tile group = 32 tiles x 32 NT output
+// channels (NT = 2 channel tiles, 1 for small grids), computed by FOUR waves,
+// wave ROW owning the 4 positions of V row ROW for every channel tile
+// (4 NT MFMA accumulator tiles, 128 registers at NT = 2): one V fragment
+// feeds NT MFMAs, so the in-lane input transform and the patch reads are
+// paid once per 64 channels (round 3's layout — a wave pair per 32 channels,
+// each wave two V rows — computed every V twice per 64 channels: block 1's
+// two channel groups, blocks 2-4's consecutive channel-group items).
+// The input transform is in-lane: lane (tile m, k-half kh) reads the 2 patch
+// rows its V row needs (8 pixels, channels 2 kh and 2 kh + 1 of a 4-channel
+// chunk: 8 ds_read_b64) and its 4 transformed values per channel ARE its A
+// fragments — V never exists in LDS or HBM.  The output transform: a lane's
+// register r holds the same (tile, channel) in all of its position tiles, so
+// each wave reduces its row to z = (M A)_ROW in registers; Y = A^T M A then
+// sums the four rows' z — the row waves swap their z through LDS, one channel
+// tile per round, and each finishes a quarter of the registers.
+// A workgroup is TG tile groups (4 TG waves) x 32 NT channels; per 4-channel
 // chunk the raw halo ([pixel][4 ch], 16 B per pixel, four parity planes) and
 // the chunk's U slab ([p][h][n][ks]) are copied global -> LDS by LDS-DMA into
 // a 3-buffer ring, NBUF - 1 chunks ahead, one counted-vmcnt barrier per chunk
@@ -37,9 +39,9 @@
 // of one tile block are consecutive workgroups of one XCD (same halo, one
 // L2), so the halo comes from HBM once per layer.
 //
-// Every shape (TG = 4 / 2 / 1) performs the same operations in the same order
-// for each (tile, channel), so outputs do not depend on the batch size or the
-// shape chosen.
+// Every shape (TG = 2 / 1, NT = 2 / 1) performs the same operations in the
+// same order for each (tile, channel), so outputs do not depend on the batch
+// size or the shape chosen.
 #include <type_traits>
 
 #include "sedx_internal.h"
@@ -48,15 +50,15 @@ namespace sedx {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-// TG tile groups x NG channel groups of 32 per workgroup (2 TG NG waves).
+// TG tile groups (32 tiles each) x 32 NT channels per workgroup, 4 TG waves.
 // C1 (block 1, F = 64): the input is the bn0 output X0 [B][T][64] and conv1
 // (Cin 1 -> 64, BN folded, ReLU) is computed into each chunk's halo image in
 // LDS (below): conv1's 64-channel activation never exists in HBM.
-template <int F, int TG, int NG = 1, bool C1 = false>
+template <int F, int TG, int NT = 2, bool C1 = false>
 struct WinoGeom {
-  static constexpr int NGW = TG * NG;                // waves per position half
-  static constexpr int WAVES = 2 * NGW;
+  static constexpr int WAVES = 4 * TG;               // row waves 0..3 of each tile group
   static constexpr int THREADS = 64 * WAVES;
+  static constexpr int NCH = 32 * NT;                // output channels per workgroup
   static constexpr int P = 32 * TG;                  // tiles per workgroup
   static constexpr int FT = F / 2;                   // tiles per tile row
   static constexpr int TRW = P / FT;                 // tile rows per workgroup
@@ -65,23 +67,22 @@ struct WinoGeom {
   static constexpr int PLP = (PL + 63) / 64 * 64;    // whole 64-pixel DMA units
   // floats: [pixel][4 ch] (C1: a 64-pixel conv1 group for every wave; the
   // groups past the halo write zeros into the padding)
-  static constexpr int A_SZ = KC * (C1 && PLP < 128 * TG * NG ? 128 * TG * NG : PLP);
-  static constexpr int W_SZ = 16 * KC * 32 * NG;     // floats: [p][h][n 32 NG][ks]
+  static constexpr int A_SZ = KC * (C1 && PLP < 64 * WAVES ? 64 * WAVES : PLP);
+  static constexpr int W_SZ = 16 * KC * NCH;         // floats: [p][h][n NCH][ks]
   static constexpr int BUF = A_SZ + W_SZ;
 #ifndef SEDX_WINO_NBUF
 #define SEDX_WINO_NBUF 3
 #endif
-#ifndef SEDX_WINO_NBUF64
-#define SEDX_WINO_NBUF64 SEDX_WINO_NBUF
-#endif
-  // ring depth (F = 64: block 1's conv2 streams its 525 MB input from HBM)
-  static constexpr int NBUF = TG == 4 ? (F == 64 ? SEDX_WINO_NBUF64 : SEDX_WINO_NBUF) : 3;
+  static constexpr int NBUF = SEDX_WINO_NBUF;        // ring depth
   static constexpr int UW = W_SZ / 256;              // 1-KiB DMA units per chunk
   static constexpr int UA = C1 ? 0 : PLP / 64;       // halo units (C1 computes the halo instead)
   static constexpr int U = UW + UA;
   static constexpr int UPW = (U + WAVES - 1) / WAVES;
   static constexpr int VM_MIN = U / WAVES;           // units of the wave with the fewest
-  static constexpr int XCH = WAVES * 8 * 4 * 64;     // floats: epilogue exchange, [wave][r 8][4][lane]
+  // epilogue exchange, one channel tile per round: per tile group
+  // [finisher row 4][other row 3][register 4][z 2][lane 64] floats
+  static constexpr int XTG = 4 * 3 * 4 * 2 * 64;
+  static constexpr int XCH = TG * XTG;
   // C1: an item's X0 rows t0 - 2 .. t0 + RT - 1 ([row][F], zero rows outside
   // the clip), two buffers by item parity, in 1-KiB DMA units; the conv1
   // halo pixels in 64-pixel groups, one group per wave
@@ -89,17 +90,17 @@ struct WinoGeom {
   static constexpr int UX = C1 ? (XROWS * F + 255) / 256 : 0;
   static constexpr int X0_SZ = 256 * UX;
   static constexpr int XA_OFF = NBUF * BUF + XCH;
-  static constexpr int NGRP = C1 ? WAVES : 0;
   // the layer's biases (Cout <= 512), LDS-DMA'd once in the prologue: read
   // from LDS, the epilogue's bias needs no vmcnt wait (which would also wait
   // for the next item's DMAs in flight)
   static constexpr int BIAS_OFF = XA_OFF + 2 * X0_SZ, BIAS_MAX = 512;
   static constexpr int LDS_BYTES = 4 * (BIAS_OFF + BIAS_MAX);   // ring, epilogue exchange, X0 tiles, biases
   static constexpr int WG_PER_CU = WAVES == 8 || LDS_BYTES > 80 * 1024 ? 1 : 2;
+  static_assert(NT == 1 || NT == 2, "channel tiles per wave");
   static_assert(P % FT == 0, "whole tile rows per workgroup");
   static_assert(VM_MIN * (NBUF - 1) <= 63, "vmcnt field");
   static_assert(LDS_BYTES <= 160 * 1024, "LDS per workgroup");
-  static_assert(!C1 || (F == 64 && PLP <= 64 * WAVES && UX <= WAVES && NBUF == 3), "C1: block 1 (64 bins), a conv1 group per wave");
+  static_assert(!C1 || (F == 64 && NT == 2 && PLP <= 64 * WAVES && UX <= WAVES && NBUF >= 3), "C1: block 1 (64 bins), a conv1 group per wave");
 };
 
 // Diagnostic builds only (tools/wino_b1_bench.cpp, tools/gpu_r04d.sh; never
@@ -115,6 +116,13 @@ struct WinoGeom {
 // LDS reads, 16 the DMAs of the chunk operands.
 #ifndef SEDX_WINO_ABL
 #define SEDX_WINO_ABL 0
+#endif
+// VALU instructions per MFMA in the second half of a chunk step (tuning builds)
+#ifndef SEDX_WINO_VG
+#define SEDX_WINO_VG 3
+#endif
+#ifndef SEDX_WINO_VG1
+#define SEDX_WINO_VG1 9
 #endif
 #ifdef SEDX_WINO_STAMPS
 __device__ unsigned long long g_wino_stamps[16];
@@ -169,17 +177,16 @@ __device__ __forceinline__ void wino_bt4(float* x) {
   x[0] = e0; x[1] = e1; x[2] = e2; x[3] = e3;
 }
 
-// the kernel body for position half PH (wave-uniform; a template parameter so
-// the transform, the U rows and the patch offsets are static per wave)
-template <int F, int EPI, int TG, int PH, int NG, bool C1>
+// the kernel body for V row ROW (wave-uniform; a template parameter so the
+// transform, the U rows and the patch offsets are static per wave)
+template <int F, int EPI, int TG, int NT, int ROW, bool C1>
 __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, int T, int Cin, int Cout,
                                           const float* __restrict__ U, const float* __restrict__ bias,
                                           float* __restrict__ out, const float* __restrict__ zero16,
                                           float* __restrict__ trash, int tb_per_clip, int ngroups,
                                           const float* __restrict__ w1, const float* __restrict__ b1,
                                           int order2d = 0) {
-  constexpr int ph = PH;
-  using G = WinoGeom<F, TG, NG, C1>;
+  using G = WinoGeom<F, TG, NT, C1>;
   constexpr int WAVES = G::WAVES;
   // unit u = wv + WAVES k of this wave: a weight unit, a halo unit, or none.
   // Folded at compile time where k alone decides (UW a multiple of WAVES:
@@ -195,10 +202,9 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
   const int lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   WS_DECL
-  // (tile group, channel group) of the wave: waves q, q + NGW are its
-  // position halves 0, 1 (one SIMD)
+  // tile group of the wave: waves tg, tg + TG, tg + 2 TG, tg + 3 TG are its
+  // V rows 0..3
   const int tg = wv % TG;
-  const int cg = NG == 1 ? 0 : (wv % G::NGW) / TG;
   // Persistent: workgroup g takes items g, g + gridDim.x, ... (gridDim.x a
   // multiple of 8, so every item of a workgroup is on its XCD).  XCD-aware
   // item decode: item -> XCD id & 7; on one XCD, tile blocks in order, each
@@ -227,7 +233,7 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
     if (tb >= B * tb_per_clip) return false;
     b_ = tb / tb_per_clip;
     t0_ = 2 * (tb - b_ * tb_per_clip) * G::TRW;   // first row (2 x first tile row)
-    n0_ = cgi * 32 * NG;
+    n0_ = cgi * G::NCH;
     return true;
   };
   // this workgroup's 128 trash floats (spread: the dummy and out-of-range
@@ -248,9 +254,9 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
   const int pt = 32 * tg + (lane & 31);
   const int a_base = ((pt / FT) * HC + (pt % FT)) * KC + 2 * khalf;
   auto a_off = [&](int i, int jj) { return ((((i & 1) << 1) | (jj & 1)) * Q + (i >> 1) * HC + (jj >> 1)) * KC; };
-  // B side: U slab [p][h][n][ks], lane (h = khalf, n = 32 cg + (lane & 31)),
-  // this wave's positions 8 ph .. 8 ph + 7 (rows of 64 NG floats)
-  const int b_base = G::A_SZ + 8 * ph * 128 * NG + khalf * 64 * NG + 64 * cg + 2 * (lane & 31);
+  // B side: U slab [p][h][n NCH][ks], lane (h = khalf, n = 32 nt + (lane & 31)),
+  // this wave's positions 4 ROW .. 4 ROW + 3 (rows of 2 NCH floats)
+  const int b_base = G::A_SZ + 4 * ROW * 4 * G::NCH + khalf * 2 * G::NCH + 2 * (lane & 31);
 
   // ---- LDS-DMA units of this wave (unit u -> wave u % WAVES): LDS offsets
   // fixed, sources per item ----
@@ -269,7 +275,7 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
       const int u = wv + WAVES * k;
       off[k] = -1;
       if (is_w(k)) {
-        constexpr int LPR = 16 * NG;   // lanes per (p, h) row of 2 x 32 NG floats
+        constexpr int LPR = G::NCH / 2;   // lanes per (p, h) row of 2 NCH floats
         const int row = (64 / LPR) * u + lane / LPR;
         off[k] = row * 2 * Cout + 4 * (lane % LPR);
       } else if (present(k, wv)) {
@@ -399,21 +405,27 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
     conv1w(wq, cb);
   };
 
-  f32x16 acc[8];
+  f32x16 acc[4][NT];
 #pragma unroll
-  for (int p = 0; p < 8; ++p)
+  for (int j = 0; j < 4; ++j)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[p][r] = 0.0f;
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[j][nt][r] = 0.0f;
 
-  // a chunk's operands in registers: V of this wave's 8 positions (both
+  // a chunk's operands in registers: V of this wave's 4 positions (both
   // k-steps) and the U fragments; two sets, ping-pong
-  float va[2][8], vb[2][8];
-  float2 ua[8], ubv[8];
+  float va[2][4], vb[2][4];
+  float2 ua[4][NT], ubv[4][NT];
+  // V row ROW of B^T d from patch rows RA, RB:
+  //   ROW 0: d0 - d2   1: d1 + d2   2: d2 - d1   3: d1 - d3
+  constexpr int RA = ROW == 0 ? 0 : 1;
+  constexpr int RB = ROW == 3 ? 3 : 2;
   // read chunk's patch rows + U fragments from LDS buffer buf (issue only)
-  auto issue_reads = [&](int buf, float2 (&pd)[3][4], float2 (&un)[8]) {
+  auto issue_reads = [&](int buf, float2 (&pd)[2][4], float2 (&un)[4][NT]) {
     const float* sm = smem + buf * G::BUF;
 #pragma unroll
-    for (int i = 0; i < 3; ++i)
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) {
         if constexpr (SEDX_WINO_ABL & 4) {
@@ -421,47 +433,39 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
           asm volatile("" : "+v"(z.x), "+v"(z.y));
           pd[i][jj] = z;
         } else {
-          pd[i][jj] = *reinterpret_cast<const float2*>(sm + a_base + a_off(ph + i, jj));
+          pd[i][jj] = *reinterpret_cast<const float2*>(sm + a_base + a_off(i ? RB : RA, jj));
         }
       }
 #pragma unroll
-    for (int p = 0; p < 8; ++p) {
-      if constexpr (SEDX_WINO_ABL & 8) {
-        float2 z = make_float2((float)p, 1.0f);
-        asm volatile("" : "+v"(z.x), "+v"(z.y));
-        un[p] = z;
-      } else {
-        un[p] = *reinterpret_cast<const float2*>(sm + b_base + p * 128 * NG);
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        if constexpr (SEDX_WINO_ABL & 8) {
+          float2 z = make_float2((float)j, (float)nt);
+          asm volatile("" : "+v"(z.x), "+v"(z.y));
+          un[j][nt] = z;
+        } else {
+          un[j][nt] = *reinterpret_cast<const float2*>(sm + b_base + j * 4 * G::NCH + 64 * nt);
+        }
       }
-    }
   };
-  // V rows 2 ph, 2 ph + 1 of B^T d B from patch rows ph .. ph + 2
-  //   ph 0: d0 - d2, d1 + d2      ph 1: d2 - d1, d1 - d3
-  auto transform = [&](const float2 (&pd)[3][4], float (&vn)[2][8]) {
+  auto transform = [&](const float2 (&pd)[2][4], float (&vn)[2][4]) {
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      float x[3][4];
-#pragma unroll
-      for (int i = 0; i < 3; ++i)
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) x[i][jj] = ks ? pd[i][jj].y : pd[i][jj].x;
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) {
-        if constexpr (SEDX_WINO_ABL & 2) {
-          vn[ks][jj] = x[0][jj];
-          vn[ks][4 + jj] = x[1][jj];
-        } else if constexpr (PH == 0) {
-          vn[ks][jj] = x[0][jj] - x[2][jj];
-          vn[ks][4 + jj] = x[1][jj] + x[2][jj];
-        } else {
-          vn[ks][jj] = x[1][jj] - x[0][jj];
-          vn[ks][4 + jj] = x[0][jj] - x[2][jj];
-        }
+        const float a = ks ? pd[0][jj].y : pd[0][jj].x;   // patch row RA
+        const float b = ks ? pd[1][jj].y : pd[1][jj].x;   // patch row RB
+        if constexpr (SEDX_WINO_ABL & 2)
+          vn[ks][jj] = a;
+        else if constexpr (ROW == 1)
+          vn[ks][jj] = a + b;
+        else if constexpr (ROW == 2)
+          vn[ks][jj] = b - a;
+        else
+          vn[ks][jj] = a - b;
       }
-      if constexpr (!(SEDX_WINO_ABL & 2)) {
-        wino_bt4(&vn[ks][0]);
-        wino_bt4(&vn[ks][4]);
-      }
+      if constexpr (!(SEDX_WINO_ABL & 2)) wino_bt4(&vn[ks][0]);
     }
     // pin V here: otherwise the compiler sinks each value's transform to the
     // MFMA that consumes it (next chunk), a VALU -> MFMA chain in front of
@@ -469,43 +473,50 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-      for (int q = 0; q < 8; ++q) asm volatile("" : "+v"(vn[ks][q]));
+      for (int q = 0; q < 4; ++q) asm volatile("" : "+v"(vn[ks][q]));
   };
-  // the 16 MFMAs of one chunk from (vc, uc) — k-step 0 (channel 2 khalf) then
-  // k-step 1 (2 khalf + 1) — with the next chunk's LDS reads spread over the
-  // first 8 and its transform over the last 8.  (Keeping the two k-steps of
-  // an accumulator apart with a scheduling barrier measured 6 % slower.)
-  // C1: then conv1 of channel chunk cc into ring buffer cb
-  auto step = [&](const float (&vc)[2][8], const float2 (&uc)[8], int nbuf, float (&vn)[2][8], float2 (&un)[8],
-                  int cc = -1, int cb = 0) {
+  // the 8 NT MFMAs of one chunk from (vc, uc) — k-step 0 (channel 2 khalf) then
+  // k-step 1 (2 khalf + 1), one V fragment per position for all NT channel
+  // tiles — with the next chunk's LDS reads spread over the first half and
+  // its transform over the second.  C1: then conv1 of channel chunk cc into
+  // ring buffer cb
+  auto mfmas = [&](const float (&vc)[2][4], const float2 (&uc)[4][NT]) {
 #pragma unroll
-    for (int p = 0; p < 8; ++p) acc[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(vc[0][p], uc[p].x, acc[p], 0, 0, 0);
+    for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-    for (int p = 0; p < 8; ++p) acc[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(vc[1][p], uc[p].y, acc[p], 0, 0, 0);
-    float2 pd[3][4];
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+          acc[j][nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(vc[ks][j], ks ? uc[j][nt].y : uc[j][nt].x, acc[j][nt], 0, 0, 0);
+  };
+  auto step = [&](const float (&vc)[2][4], const float2 (&uc)[4][NT], int nbuf, float (&vn)[2][4],
+                  float2 (&un)[4][NT], int cc = -1, int cb = 0) {
+    mfmas(vc, uc);
+    float2 pd[2][4];
     issue_reads(nbuf, pd, un);
     transform(pd, vn);
     if constexpr (C1 && !(SEDX_WINO_ABL & 1)) conv1(cc, cb);
-    // (measured slower: every LDS read ahead of the MFMAs, -10 %: the
-    // transform then waits at the end of the chunk with nothing to overlap;
-    // C1's conv1 beside the first MFMAs with its weights loaded a chunk
-    // ahead, b1c2 +5 %: the reads then issue late)
+    // (round 3, measured slower: every LDS read ahead of the MFMAs, -10 %:
+    // the transform then waits at the end of the chunk with nothing to
+    // overlap; C1's conv1 beside the first MFMAs with its weights loaded a
+    // chunk ahead, b1c2 +5 %: the reads then issue late)
+    constexpr int NM = 8 * NT, NR = 8 + 4 * NT;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
-      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // 2 LDS reads
+    for (int i = 0; i < NM / 2; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                        // 1 MFMA
+      __builtin_amdgcn_sched_group_barrier(0x100, (NR + NM / 2 - 1) / (NM / 2), 0);   // LDS reads
     }
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
-      __builtin_amdgcn_sched_group_barrier(0x002, C1 ? 11 : 5, 0);   // 5 VALU (C1: + conv1's)
+    for (int i = 0; i < NM / 2; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                        // 1 MFMA
+      __builtin_amdgcn_sched_group_barrier(0x002, C1 ? SEDX_WINO_VG1 : (NT == 2 ? SEDX_WINO_VG : 5), 0);   // VALU (C1: + conv1's)
     }
   };
 
   const int nchunks = Cin / KC;   // even (Cin % 8 == 0, checked by the launcher)
   constexpr int NB = G::NBUF;
   // epilogue stores per wave (all issued: out-of-range ones go to trash)
-  constexpr int S = EPI == EPI_FMEAN ? 4 : EPI == EPI_POOL2 ? 8 : 32;
+  constexpr int S = NT * (EPI == EPI_FMEAN ? 2 : EPI == EPI_POOL2 ? 4 : 16);
   static_assert(G::VM_MIN * (NB - 2) + S <= 63, "vmcnt field");
   static_assert(!C1 || G::VM_MIN * NB + S <= 63, "vmcnt field");
   int xpar = 0;   // C1: the current item's X0 tile
@@ -543,35 +554,22 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
   WS_MARK(0)
 
   // ---- epilogue pieces.  Register r of every position tile = MFMA row
-  // m = (r & 3) + 8 (r >> 2) + 4 khalf (tile 32 tg + m), column lane & 31.
-  // Each wave reduces its V rows i to a partial Y = A^T M A: with
-  // T_a[j] = sum_i A^T[a][i] M[i][j] over its rows (ph 0: T_0 = m0 + m1,
-  // T_1 = m1; ph 1: T_0 = m2, T_1 = -m2 - m3), Y[a] = (T_a0 + T_a1 + T_a2,
-  // T_a1 - T_a2 - T_a3).  Wave half h finishes registers 8 h .. 8 h + 7:
-  // it hands its partial of the other half's registers over through LDS
-  // (an exchange area of its own, after the ring, so the next item's chunks
-  // can already be landing) and sums Y_0 + Y_1 (in that order) for its own.
-  auto partial = [&](int r, float y[4]) {
-    float t[2][4];
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      const float m0 = acc[jj][r], m1 = acc[4 + jj][r];
-      if constexpr (PH == 0) {
-        t[0][jj] = m0 + m1;
-        t[1][jj] = m1;
-      } else {
-        t[0][jj] = m0;
-        t[1][jj] = -m0 - m1;
-      }
-    }
-#pragma unroll
-    for (int a = 0; a < 2; ++a) {
-      y[2 * a] = (t[a][0] + t[a][1]) + t[a][2];
-      y[2 * a + 1] = (t[a][1] - t[a][2]) - t[a][3];
-    }
+  // m = (r & 3) + 8 (r >> 2) + 4 khalf (tile 32 tg + m), column lane & 31 of
+  // channel tile nt.  This wave holds V row ROW of M: per register its row of
+  // M A, z = (m0 + m1 + m2, m1 - m2 - m3) (A^T = [1 1 1 0; 0 1 -1 -1]), and
+  // Y = A^T M A sums the rows: Y[0] = z_0 + z_1 + z_2, Y[1] = z_1 - z_2 - z_3
+  // (in that order).  Wave ROW finishes registers 4 ROW .. 4 ROW + 3 of each
+  // channel tile; the four row waves of a tile group hand each other their z
+  // through LDS (an exchange area after the ring, so the next item's chunks
+  // can already be landing), one channel tile per round.
+  auto zrow = [&](int nt, int r, float (&z)[2]) {
+    const float m0 = acc[0][nt][r], m1 = acc[1][nt][r], m2 = acc[2][nt][r], m3 = acc[3][nt][r];
+    z[0] = (m0 + m1) + m2;
+    z[1] = (m1 - m2) - m3;
   };
-  float* const xo = smem + NB * G::BUF + wv * (8 * 4 * 64);                    // this wave's slots [r 8][4][lane]
-  const float* const xi = smem + NB * G::BUF + (wv % G::NGW + G::NGW * (1 - ph)) * (8 * 4 * 64);   // the partner's
+  // this tile group's exchange area: [finisher row f][other row][register k][z c][lane]
+  float* const xg = smem + NB * G::BUF + tg * G::XTG;
+  auto xslot = [](int f, int src) { return (f * 3 + (src < f ? src : src - 1)) * (4 * 2 * 64); };
 
   // top of chunk c: chunk c + 1 landed (c + 2 .. c + NB - 1 of the item
   // sequence may be in flight) and every wave has consumed chunk c's buffer
@@ -584,15 +582,17 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
     int nb_ = 0, nt0 = 0, nn0 = 0;
     const bool has_next = decode(nitem, nb_, nt0, nn0);
     {   // the item's chunk 0 (landed: the previous barrier waited for it)
-      float2 pd[3][4];
+      float2 pd[2][4];
       issue_reads(buf, pd, ua);
       transform(pd, va);
     }
     WS_MARK(1)
 #pragma unroll
-    for (int p = 0; p < 8; ++p)
+    for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[p][r] = 0.0f;
+      for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[j][nt][r] = 0.0f;
     auto issue = [&](int g, int bf) {
       if (g < nchunks) {
         dma_cur(g, bf);
@@ -646,10 +646,7 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
       if constexpr (!LAST) {
         step(vb, ubv, b2, va, ua, C1 ? chunk + 3 : -1, buf);
       } else {
-#pragma unroll
-        for (int p = 0; p < 8; ++p) acc[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(vb[0][p], ubv[p].x, acc[p], 0, 0, 0);
-#pragma unroll
-        for (int p = 0; p < 8; ++p) acc[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(vb[1][p], ubv[p].y, acc[p], 0, 0, 0);
+        mfmas(vb, ubv);
         if constexpr (C1 && !(SEDX_WINO_ABL & 1)) conv1(1, buf);
       }
       buf = b2;
@@ -670,84 +667,94 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
     float* const ob = EPI == EPI_FMEAN ? out + ((int64_t)b * T + t0) * Cout
                       : EPI == EPI_POOL2 ? out + ((int64_t)b * (T / 2) + tr0) * (F / 2) * Cout
                                          : out + ((int64_t)b * T + t0) * F * Cout;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      float y[4];
-      partial(8 * (1 - ph) + k, y);   // registers the partner finishes
-#pragma unroll
-      for (int e = 0; e < 4; ++e) xo[(k * 4 + e) * 64 + lane] = y[e];
-    }
-    // LDS-only barrier (__syncthreads() would drain the next item's DMAs)
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     // an opaque copy of the lane index: the store offsets below are computed
     // here instead of being hoisted out of the item loop as live registers
     int le = lane;
     asm volatile("" : "+v"(le));
     const int khe = le >> 5;
-    const int n = n0 + 32 * cg + (le & 31);
-    const float bv = smem[G::BIAS_OFF + n];
-    // full Y of register 8 ph + k (+ bias, ReLU), as y[a][b]
-    auto outtile = [&](int k, float y[2][2]) {
-      float mine[4];
-      partial(8 * ph + k, mine);
+    // registers 4 ROW + k: tiles 32 tg + 8 ROW + 4 khalf + k (k = 0..3)
+    const int pt0 = 32 * tg + 8 * ROW + 4 * khe;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float other = xi[(k * 4 + e) * 64 + lane];
-        const float sm = PH == 0 ? mine[e] + other : other + mine[e];
-        y[e >> 1][e & 1] = fmaxf(sm + bv, 0.0f);
+    for (int nt = 0; nt < NT; ++nt) {
+      // LDS-only barriers (__syncthreads() would drain the next item's DMAs):
+      // the previous round's reads are done before this round's writes
+      if (nt > 0) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {   // the other rows' registers
+        if (f == ROW) continue;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          float z[2];
+          zrow(nt, 4 * f + k, z);
+          xg[xslot(f, ROW) + (2 * k) * 64 + lane] = z[0];
+          xg[xslot(f, ROW) + (2 * k + 1) * 64 + lane] = z[1];
+        }
       }
-    };
-    if constexpr (EPI == EPI_FMEAN) {
-      // F = 8: registers 4q .. 4q + 3 are the 4 tiles (bins 0-7) of tile row
-      // 8 tg + 2 q + khalf; torch.mean over the 8 bins
-      static_assert(F == 8, "freq-mean epilogue: F = 8");
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      const int n = n0 + 32 * nt + (le & 31);
+      const float bv = smem[G::BIAS_OFF + n];
+      // full Y of register 4 ROW + k (+ bias, ReLU), as y[a][b]
+      auto outtile = [&](int k, float (&y)[2][2]) {
+        float z[4][2];
+        zrow(nt, 4 * ROW + k, z[ROW]);
 #pragma unroll
-      for (int qq = 0; qq < 2; ++qq) {
-        const int q = 2 * ph + qq;
+        for (int src = 0; src < 4; ++src) {
+          if (src == ROW) continue;
+          z[src][0] = xg[xslot(ROW, src) + (2 * k) * 64 + lane];
+          z[src][1] = xg[xslot(ROW, src) + (2 * k + 1) * 64 + lane];
+        }
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          y[0][c] = fmaxf(((z[0][c] + z[1][c]) + z[2][c]) + bv, 0.0f);
+          y[1][c] = fmaxf(((z[1][c] - z[2][c]) - z[3][c]) + bv, 0.0f);
+        }
+      };
+      if constexpr (EPI == EPI_FMEAN) {
+        // F = 8: the 4 registers are the 4 tiles (bins 0-7) of tile row
+        // 8 tg + 2 ROW + khalf; torch.mean over the 8 bins
+        static_assert(F == 8, "freq-mean epilogue: F = 8");
         float y[4][2][2];
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) outtile(4 * qq + jj, y[jj]);
-        const int trl = 8 * tg + 2 * q + khe;
+        for (int k = 0; k < 4; ++k) outtile(k, y[k]);
+        const int trl = pt0 / FT;
 #pragma unroll
         for (int a = 0; a < 2; ++a) {
           float sum = 0.0f;
 #pragma unroll
-          for (int jj = 0; jj < 4; ++jj) sum = (sum + y[jj][a][0]) + y[jj][a][1];
+          for (int k = 0; k < 4; ++k) sum = (sum + y[k][a][0]) + y[k][a][1];
           const int t = t0 + 2 * trl + a;
           float* dst = t < T ? ob + (2 * trl + a) * Cout + n : tr_lane;
           *dst = sum * (1.0f / F);
         }
-      }
-    } else {
+      } else {
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int r = 8 * ph + k;
-        const int m = (r & 3) + 8 * (r >> 2) + 4 * khe;
-        const int ptile = 32 * tg + m;
-        const int trl = ptile / FT, tf = ptile % FT;
-        float y[2][2];
-        outtile(k, y);
-        if constexpr (EPI == EPI_POOL2) {
-          const int To = T / 2;
-          const int to = tr0 + trl;
-          const float pv = (((y[0][0] + y[0][1]) + y[1][0]) + y[1][1]) * 0.25f;
-          float* dst = to < To ? ob + (trl * (F / 2) + tf) * Cout + n : tr_lane;
-          *dst = pv;
-        } else {
+        for (int k = 0; k < 4; ++k) {
+          const int ptile = pt0 + k;
+          const int trl = ptile / FT, tf = ptile % FT;
+          float y[2][2];
+          outtile(k, y);
+          if constexpr (EPI == EPI_POOL2) {
+            const int To = T / 2;
+            const int to = tr0 + trl;
+            const float pv = (((y[0][0] + y[0][1]) + y[1][0]) + y[1][1]) * 0.25f;
+            float* dst = to < To ? ob + (trl * (F / 2) + tf) * Cout + n : tr_lane;
+            *dst = pv;
+          } else {
 #pragma unroll
-          for (int a = 0; a < 2; ++a) {
-            const int t = t0 + 2 * trl + a;
-            float* o = t < T ? ob + ((2 * trl + a) * F + 2 * tf) * Cout + n : tr_lane;
-            const int64_t o1 = t < T ? Cout : 64;
-            o[0] = y[a][0];
-            o[o1] = y[a][1];
+            for (int a = 0; a < 2; ++a) {
+              const int t = t0 + 2 * trl + a;
+              float* o = t < T ? ob + ((2 * trl + a) * F + 2 * tf) * Cout + n : tr_lane;
+              const int64_t o1 = t < T ? Cout : 64;
+              o[0] = y[a][0];
+              o[o1] = y[a][1];
+            }
           }
         }
       }
     }
     WS_MARK(6)
     if (!has_next) break;
-    // the partner's reads of this item's exchange slots finish before the
+    // the other rows' reads of this item's exchange slots finish before the
     // next item's epilogue overwrites them: many barriers lie between
     item = nitem;
     xpar ^= 1;
@@ -763,32 +770,35 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
   WS_FLUSH()
 }
 
-template <int F, int EPI, int TG>
-__global__ __launch_bounds__(128 * TG, TG == 4 ? 1 : 2) void conv3x3_wino_kernel(
+// the V row of a wave (wave-uniform): one body instantiation per row
+#define SEDX_WINO_ROWS(F_, EPI_, TG_, NT_, C1_, ...)                                    \
+  switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) / TG_) {                    \
+    case 0: wino_body<F_, EPI_, TG_, NT_, 0, C1_>(__VA_ARGS__); break;                 \
+    case 1: wino_body<F_, EPI_, TG_, NT_, 1, C1_>(__VA_ARGS__); break;                 \
+    case 2: wino_body<F_, EPI_, TG_, NT_, 2, C1_>(__VA_ARGS__); break;                 \
+    default: wino_body<F_, EPI_, TG_, NT_, 3, C1_>(__VA_ARGS__); break;                \
+  }
+
+template <int F, int EPI, int TG, int NT>
+__global__ __launch_bounds__(256 * TG, (WinoGeom<F, TG, NT>::WG_PER_CU)) void conv3x3_wino_kernel(
     const float* __restrict__ in, int B, int T, int Cin, int Cout, const float* __restrict__ U,
     const float* __restrict__ bias, float* __restrict__ out, const float* __restrict__ zero16,
     float* __restrict__ trash, int tb_per_clip, int ngroups, int order2d) {
-  if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) < TG)
-    wino_body<F, EPI, TG, 0, 1, false>(in, B, T, Cin, Cout, U, bias, out, zero16, trash, tb_per_clip, ngroups,
-                                       nullptr, nullptr, order2d);
-  else
-    wino_body<F, EPI, TG, 1, 1, false>(in, B, T, Cin, Cout, U, bias, out, zero16, trash, tb_per_clip, ngroups,
-                                       nullptr, nullptr, order2d);
+  SEDX_WINO_ROWS(F, EPI, TG, NT, false, in, B, T, Cin, Cout, U, bias, out, zero16, trash, tb_per_clip, ngroups,
+                 nullptr, nullptr, order2d)
 }
 
 // Block 1 in one launch: conv1 (computed into the halo images) + Winograd
-// conv2 + 2x2 pool, TG tile groups x both 32-channel groups per workgroup
-// (the conv1 halo serves all 64 output channels)
+// conv2 + 2x2 pool, TG tile groups x 64 channels per workgroup (the conv1
+// halo serves all 64 output channels)
 template <int TG>
 __global__ __launch_bounds__(256 * TG, (WinoGeom<64, TG, 2, true>::WG_PER_CU)) void wino_block1_kernel(
     const float* __restrict__ x0, int B, int T, const float* __restrict__ U, const float* __restrict__ bias,
     float* __restrict__ out, const float* __restrict__ zero16, float* __restrict__ trash, int tb_per_clip,
     const float* __restrict__ w1, const float* __restrict__ b1) {
-  if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) < 2 * TG)
-    wino_body<64, EPI_POOL2, TG, 0, 2, true>(x0, B, T, 64, 64, U, bias, out, zero16, trash, tb_per_clip, 1, w1, b1);
-  else
-    wino_body<64, EPI_POOL2, TG, 1, 2, true>(x0, B, T, 64, 64, U, bias, out, zero16, trash, tb_per_clip, 1, w1, b1);
+  SEDX_WINO_ROWS(64, EPI_POOL2, TG, 2, true, x0, B, T, 64, 64, U, bias, out, zero16, trash, tb_per_clip, 1, w1, b1, 0)
 }
+#undef SEDX_WINO_ROWS
 
 static int wino_device_cus() {
   int dev = 0, ncu = 256;
@@ -808,25 +818,25 @@ constexpr int WINO_ITEMS = SEDX_WINO_ITEMS;
 #endif
 constexpr int WINO_ITEMS_B1 = SEDX_WINO_ITEMS_B1;
 
-template <int F, int TG>
+template <int F, int TG, int NT>
 static void launch_wino_w(const float* in, int B, int T, int Cin, int Cout, const float* U, const float* bias,
                           float* out, int epi, const float* zero16, float* trash, int order, hipStream_t s) {
-  using G = WinoGeom<F, TG>;
+  using G = WinoGeom<F, TG, NT>;
   // tile rows of a clip: POOL2 drops an odd last row (floor), the others keep it
   const int trows = epi == EPI_POOL2 ? T / 2 : (T + 1) / 2;
   const int tb_per_clip = (trows + G::TRW - 1) / G::TRW;
-  const int ngroups = Cout / 32;
+  const int ngroups = Cout / G::NCH;
   const int64_t tblocks = (int64_t)B * tb_per_clip;
   const int64_t nitems = (tblocks + 7) / 8 * 8 * ngroups;
   if (nitems > INT32_MAX || tblocks <= 0 || (int64_t)B * T * F * Cin >= INT32_MAX)   // 32-bit DMA offsets
     return note_launch_error(hipErrorInvalidValue);
-  // persistent workgroups: as many as are resident (1 per CU at TG 4, else
-  // 2), a multiple of 8 (XCD-aware item decode); each walks its items with
+  // persistent workgroups: as many as are resident, a multiple of 8
+  // (XCD-aware item decode); each walks its items with
   // the next item's first chunks landing during the current one's last
   // ~WINO_ITEMS items per workgroup, but at least one resident round: the
   // hardware dispatcher still balances the workgroups over the CUs (a CU
   // shared with another stream's kernel finishes its workgroups later)
-  const int64_t resident = (int64_t)wino_device_cus() * (TG == 4 ? 1 : 2) / 8 * 8;
+  const int64_t resident = (int64_t)wino_device_cus() * G::WG_PER_CU / 8 * 8;
   const int64_t per = (nitems + WINO_ITEMS - 1) / WINO_ITEMS;
   const int64_t nwg = std::min<int64_t>(nitems, std::max<int64_t>(std::max<int64_t>(8, resident), (per + 7) / 8 * 8));
   dim3 grid((unsigned)nwg);
@@ -837,7 +847,7 @@ static void launch_wino_w(const float* in, int B, int T, int Cin, int Cout, cons
                       (nitems / 8) % 32 == 0;
 #define SEDX_WG_LAUNCH(E)                                                                              \
   {                                                                                                    \
-    auto* k_ = conv3x3_wino_kernel<F, E, TG>;                                                          \
+    auto* k_ = conv3x3_wino_kernel<F, E, TG, NT>;                                                      \
     if (!launch_info(reinterpret_cast<const void*>(k_), G::THREADS, G::LDS_BYTES).ok) return;          \
     hipLaunchKernelGGL(k_, grid, dim3(G::THREADS), G::LDS_BYTES, s, in, B, T, Cin, Cout, U, bias, out, zero16, \
                        trash, tb_per_clip, ngroups, order2d);                                          \
@@ -855,20 +865,21 @@ static void launch_wino_w(const float* in, int B, int T, int Cin, int Cout, cons
 }
 
 
-// 4 tile groups (128 tiles) when that gives every CU a workgroup, else 2,
-// else 1: the same per-wave work, bit-identical outputs
+// 2 tile groups x 64 channels (8 waves) when that gives every CU a
+// workgroup, else 1 x 64, else 1 x 32: the same per-(tile, channel) work,
+// bit-identical outputs
 template <int F>
 static void launch_wino_f(const float* in, int B, int T, int Cin, int Cout, const float* U, const float* bias,
                           float* out, int epi, const float* zero16, float* trash, int order, hipStream_t s) {
   const int64_t ncu = wino_device_cus();
   const int trows = epi == EPI_POOL2 ? T / 2 : (T + 1) / 2;
-  auto wgs = [&](int trw) { return (int64_t)B * ((trows + trw - 1) / trw) * (Cout / 32); };
-  if (wgs(WinoGeom<F, 4>::TRW) >= ncu)
-    launch_wino_w<F, 4>(in, B, T, Cin, Cout, U, bias, out, epi, zero16, trash, order, s);
-  else if (wgs(WinoGeom<F, 2>::TRW) >= ncu)
-    launch_wino_w<F, 2>(in, B, T, Cin, Cout, U, bias, out, epi, zero16, trash, order, s);
+  auto wgs = [&](int trw, int nch) { return (int64_t)B * ((trows + trw - 1) / trw) * (Cout / nch); };
+  if (wgs(WinoGeom<F, 2, 2>::TRW, 64) >= ncu)
+    launch_wino_w<F, 2, 2>(in, B, T, Cin, Cout, U, bias, out, epi, zero16, trash, order, s);
+  else if (wgs(WinoGeom<F, 1, 2>::TRW, 64) >= ncu)
+    launch_wino_w<F, 1, 2>(in, B, T, Cin, Cout, U, bias, out, epi, zero16, trash, order, s);
   else
-    launch_wino_w<F, 1>(in, B, T, Cin, Cout, U, bias, out, epi, zero16, trash, order, s);
+    launch_wino_w<F, 1, 1>(in, B, T, Cin, Cout, U, bias, out, epi, zero16, trash, order, s);
 }
 
 void launch_conv3x3_wino(const float* in, int B, int T, int F, int Cin, int Cout, const float* U,
@@ -876,7 +887,7 @@ void launch_conv3x3_wino(const float* in, int B, int T, int F, int Cin, int Cout
                          int order) {
   // halo lanes outside the clip step through the zero block by the chunk's
   // channel offset: it must hold Cin + 4 floats
-  if (Cin % 8 != 0 || Cin < 32 || Cout % 32 != 0 || B <= 0 || T <= 0 || Cin + 4 > ZERO_BLOCK_FLOATS)
+  if (Cin % 8 != 0 || Cin < 32 || Cout % 64 != 0 || Cout > 512 || B <= 0 || T <= 0 || Cin + 4 > ZERO_BLOCK_FLOATS)
     return note_launch_error(hipErrorInvalidValue);
   // the kernel's DMA offsets are 32-bit: batches whose input passes 2^31
   // elements run as several launches over whole clips (same per-clip work,
@@ -926,9 +937,9 @@ void launch_block1_wino(const float* x0, int B, int T, const float* w1, const fl
   const int64_t bmax = (INT32_MAX - 1) / in_clip;
   for (int64_t b0 = 0; b0 < B; b0 += bmax) {
     const int bs = (int)std::min<int64_t>(bmax, B - b0);
-    // 2 tile groups x 2 channel groups (64 tiles x 64 channels, 8 waves)
-    // at every batch size (with 1 tile group the 4 waves would not cover
-    // the halo's conv1 pixel groups)
+    // 2 tile groups x 64 channels (64 tiles, 8 waves) at every batch size
+    // (with 1 tile group the 4 waves would not cover the halo's conv1 pixel
+    // groups)
     launch_block1_w<2>(x0 + b0 * in_clip, bs, T, U, bias, out + b0 * out_clip, w1, b1, zero16, trash, s);
   }
 }

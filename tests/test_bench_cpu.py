@@ -78,7 +78,7 @@ def test_roofline_winograd_block1(bench):
     try:
         bench.WINO_BLOCK1 = 1
         w = bench.roofline(stage, 32, 'winograd')
-        assert w['kernel'] == 'sedx::conv3x3_wino_kernel<64, 1, 4> (b1c2)'
+        assert w['kernel'] == 'sedx::conv3x3_wino_kernel<64, 1, 2, 2> (b1c2)'
         assert w['flops_per_launch'] == bench.conv_flops('b1c2', 32, 1001) * 16.0 / 36.0
         bench.WINO_BLOCK1 = 0
         d = bench.roofline(stage, 32, 'winograd')
