@@ -93,7 +93,7 @@ DTYPE = {'exact': 'f32',
 WINO_BLOCK1 = 2
 WINO_MUL = 16.0 / 36.0
 # SEDX_TUNE_GRU_KERNEL values (include/sedx.h)
-GRU_KERNELS = {'coop': 0, 'simple': 1, 'tag16': 2, 'tag8': 3, 'coop16': 4, 'auto': 5}
+GRU_KERNELS = {'coop': 0, 'simple': 1, 'tag16': 2, 'tag8': 3, 'coop16': 4, 'auto': 5, 'ksplit': 6}
 
 
 def wino_stages():

@@ -262,6 +262,11 @@ sedx_status sedx_set_precision(sedx_handle* h, int32_t mode);
  *                         (32-clip group, direction) — half the serial
  *                         product per step, twice the CUs held;
  *                         bit-identical to COOP.
+ *                         SEDX_GRU_KERNEL_KSPLIT (exact, more than 8 clips):
+ *                         16 workgroups per (32-clip group, direction), each
+ *                         K-eighth wave waiting only for the two slices it
+ *                         multiplies and loading their h straight into its
+ *                         MFMA operands (no LDS gather); bit-identical.
  *  SEDX_TUNE_GRU_HANDOFF  (COOP) SEDX_GRU_HANDOFF_AUTO (default): XCD-local hand-off
  *                         when all 8 slices share an XCD, else global;
  *                         SEDX_GRU_HANDOFF_GLOBAL: always the global protocol
@@ -284,8 +289,9 @@ sedx_status sedx_set_precision(sedx_handle* h, int32_t mode);
  *  SEDX_TUNE_GRU_SPIN     bound of every GRU hand-off spin, in polls (default
  *                         2^24 = 16777216).  A spin that runs out turns that
  *                         forward's outputs into NaN and is reported by
- *                         sedx_check_error (tests force it with 0: the first
- *                         poll that finds the data not yet there fails).
+ *                         sedx_check_error (tests force it with 0: every
+ *                         step that would wait fails, whether or not its data
+ *                         has arrived).
  *  SEDX_TUNE_WINO_ORDER   (winograd) 1 (default): the 512-channel layers run
  *                         each XCD's rounds of 32 concurrent items as 4 tile
  *                         blocks x 8 channel groups (8 weight slabs + 4 halos
@@ -315,7 +321,8 @@ enum {
   SEDX_GRU_KERNEL_TAG16 = 2,
   SEDX_GRU_KERNEL_TAG8 = 3,
   SEDX_GRU_KERNEL_COOP16 = 4,
-  SEDX_GRU_KERNEL_AUTO = 5
+  SEDX_GRU_KERNEL_AUTO = 5,
+  SEDX_GRU_KERNEL_KSPLIT = 6
 };
 enum { SEDX_GRU_HANDOFF_AUTO = 0, SEDX_GRU_HANDOFF_GLOBAL = 1 };
 sedx_status sedx_set_tuning(sedx_handle* h, int32_t knob, int32_t value);

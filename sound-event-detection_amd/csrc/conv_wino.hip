@@ -188,13 +188,6 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
                                           int order2d = 0) {
   using G = WinoGeom<F, TG, NT, C1>;
   constexpr int WAVES = G::WAVES;
-  // unit u = wv + WAVES k of this wave: a weight unit, a halo unit, or none.
-  // Folded at compile time where k alone decides (UW a multiple of WAVES:
-  // k < UW / WAVES weight, else halo; k < U / WAVES always present), so the
-  // per-chunk DMA issue has no branches but the last unit's presence check
-  static_assert(G::UW % WAVES == 0, "weight units a multiple of the waves");
-  auto is_w = [&](int k) { return (k + 1) * WAVES <= G::UW; };
-  auto present = [&](int k, int wv_) { return (k + 1) * WAVES <= G::U || wv_ + WAVES * k < G::U; };
   constexpr int CS = G::CS, KC = G::KC, FT = G::FT;
   extern __shared__ __attribute__((aligned(16))) float smem[];   // G::LDS_BYTES (dynamic: > 64 KiB)
 
@@ -202,6 +195,17 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
   const int lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   WS_DECL
+  // unit u = wv + WAVES k of this wave: a weight unit, a halo unit, or none.
+  // Folded at compile time where k alone decides (k < UW / WAVES weight,
+  // k >= ceil(UW / WAVES) halo; k < U / WAVES always present), so the
+  // per-chunk DMA issue has no branches but the last unit's presence check
+  // (and, when UW is not a multiple of WAVES, one wave-uniform test)
+  auto is_w = [&](int k) {
+    if ((k + 1) * WAVES <= G::UW) return true;
+    if (k * WAVES >= G::UW) return false;
+    return wv + WAVES * k < G::UW;
+  };
+  auto present = [&](int k, int wv_) { return (k + 1) * WAVES <= G::U || wv_ + WAVES * k < G::U; };
   // tile group of the wave: waves tg, tg + TG, tg + 2 TG, tg + 3 TG are its
   // V rows 0..3
   const int tg = wv % TG;
@@ -874,6 +878,16 @@ static void launch_wino_f(const float* in, int B, int T, int Cin, int Cout, cons
   const int64_t ncu = wino_device_cus();
   const int trows = epi == EPI_POOL2 ? T / 2 : (T + 1) / 2;
   auto wgs = [&](int trw, int nch) { return (int64_t)B * ((trows + trw - 1) / trw) * (Cout / nch); };
+#ifdef SEDX_WINO_TG3
+  if (wgs(WinoGeom<F, 3, 1>::TRW, 32) >= ncu)
+    launch_wino_w<F, 3, 1>(in, B, T, Cin, Cout, U, bias, out, epi, zero16, trash, order, s);
+  else
+#endif
+#ifdef SEDX_WINO_TG4
+  if (wgs(WinoGeom<F, 4, 1>::TRW, 32) >= ncu)
+    launch_wino_w<F, 4, 1>(in, B, T, Cin, Cout, U, bias, out, epi, zero16, trash, order, s);
+  else
+#endif
   if (wgs(WinoGeom<F, 2, 2>::TRW, 64) >= ncu)
     launch_wino_w<F, 2, 2>(in, B, T, Cin, Cout, U, bias, out, epi, zero16, trash, order, s);
   else if (wgs(WinoGeom<F, 1, 2>::TRW, 64) >= ncu)

@@ -106,6 +106,16 @@ __device__ __forceinline__ void gru_fail(GruSync* sync, unsigned* host_err, unsi
   atomicOr(&sync->err, code);
   if (host_err) __hip_atomic_store(host_err, code | 0x80000000u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+// spin bound 0 (tests): every step that would wait fails at once, whether
+// or not its data has already arrived (a bound of 0 polls is otherwise a
+// race against the producers' timing)
+__device__ __forceinline__ void gru_forced_fail(unsigned spin_limit, int gs, GruSync* sync, unsigned* host_err,
+                                                int* s_err) {
+  if (spin_limit == 0 && gs > 0) {
+    gru_fail(sync, host_err, 8u);
+    *s_err = 1;
+  }
+}
 // the workgroup's timeout word (a __shared__ int): read as an LDS access
 // (a generic volatile pointer would become a flat load, which the compiler
 // orders with vmcnt(0) — a drain of every store in flight)
@@ -265,6 +275,7 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
       // after a timed-out spin (s_err) no later wait is attempted: the
       // workgroup runs its remaining steps on NaN instead of timing out again
       // at every step
+      if (tid == 0) gru_forced_fail(spin_limit, gs, sync, host_err, &s_err);
       if (!VALU && gs > 0) {
         if (fast) {
           if (tid < NS) {
@@ -654,6 +665,7 @@ __global__ __launch_bounds__(gru_tag_threads<NS>()) void gru_tag_kernel(
         float gnext[3] = {0.f, 0.f, 0.f};
         if (s + 1 < T) load_gi(s + 1, gnext);    // in flight across this step's sweep and product
         float hb[8];
+        if (tid == 0) gru_forced_fail(spin_limit, gs, sync, host_err, &s_err);
         if (gs > 0 && n16 < nc) {
           const unsigned long long* src = Xp + ((gs - 1) & 1) * 16 * 256 + n16 * 256 + 32 * e + q;
           unsigned long long w[8];
@@ -770,6 +782,194 @@ __global__ __launch_bounds__(gru_tag_threads<NS>()) void gru_tag_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// K-split hand-off (round 4, launch variant 4): per (32-clip group,
+// direction) 16 slices of 16 hidden units (48 gate rows); 8 waves, wave e =
+// K eighth e = the hidden units of slices 2e and 2e + 1.  A wave waits for
+// ITS two slices' flags only and loads their h(t-1) straight into its MFMA A
+// fragments (v_mfma_f32_16x16x4_f32: lane (clip m, k-quarter kk) needs
+// h[m][32 e + 4 st + kk], st = 0..7 — 8 consecutive floats in the K-permuted
+// exchange layout below, two 16-byte sc1 loads per clip tile), so a wave
+// whose slices published early starts its product while the others still
+// wait: no LDS image of h, no gather barrier (variant 3 waits for all 16
+// flags, gathers 32 KB into LDS, then multiplies).  Then the 8 eighth
+// partials -> LDS, one barrier, the gate phase on (clip, unit) threads, sc1
+// payload stores, vmcnt(0), barrier, the slice's flag (placement-independent:
+// agent-scope stores and polls).  Exchange layout per (pair, parity):
+// [clip 32][256] with unit u at 32 (u >> 5) + 8 (u & 3) + ((u >> 2) & 7).
+// Arithmetic: each eighth the in-order fma chain over its 32 k (16x16x4 =
+// the in-order chain over its 4 k), the 8 partials summed in K order, then
+// gru_cell — the contract of every exact kernel here: bit-identical.
+constexpr int GRU_KS_LD = 20;         // partial rows: 4 rows = 80 floats (16 mod 64 banks)
+__device__ __forceinline__ int gru_kperm(int u) { return 32 * (u >> 5) + 8 * (u & 3) + ((u >> 2) & 7); }
+
+__global__ __launch_bounds__(512) void gru_ksplit_kernel(const float* __restrict__ G, int B, int T,
+                                                         const float* __restrict__ whh,
+                                                         const float* __restrict__ bhh, float* __restrict__ H,
+                                                         float* X, GruSync* sync, int nslots, unsigned* host_err,
+                                                         unsigned spin_limit) {
+  __shared__ float part[8][3][32][GRU_KS_LD];  // [eighth][gate][clip][unit]
+  __shared__ int s_err;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int e = __builtin_amdgcn_readfirstlane(tid >> 6);   // K eighth of this wave
+  const int pair = blockIdx.x & 7;             // dispatch residue -> one XCD (speed only)
+  const int p = blockIdx.x >> 3;               // slice 0..15
+  const int slot = pair >> 1, dir = pair & 1;
+  if (slot >= nslots) return;                  // whole workgroup exits (uniform)
+  if (tid == 0) s_err = 0;
+  __syncthreads();
+  const int ngroups = (B + 31) / 32;
+  const int n16 = lane & 15, kk = lane >> 4;
+  // W_hh B fragments: B[k][n] = W_hh[gate g row 16 p + n][32 e + 4 st + kk]
+  float Wf[3][8];
+#pragma unroll
+  for (int g = 0; g < 3; ++g)
+#pragma unroll
+    for (int st = 0; st < 8; ++st)
+      Wf[g][st] = whh[((int64_t)dir * 768 + g * 256 + 16 * p + n16) * 256 + 32 * e + 4 * st + kk];
+  // gate-phase thread: (clip gc, unit gu of the slice)
+  const int gc = tid >> 4, gu = tid & 15;
+  const int uo = 16 * p + gu;
+  const float br = bhh[dir * 768 + uo], bz = bhh[dir * 768 + 256 + uo], bn = bhh[dir * 768 + 512 + uo];
+  const int upos = gru_kperm(uo);
+  float* const Xs = X + (int64_t)pair * 2 * 32 * 256;
+  unsigned* const Fl = &sync->flag[pair][0][0];
+#ifdef SEDX_GRU_STAMPS
+  unsigned long long st_acc[4] = {0, 0, 0, 0};
+  unsigned long long st_last = __builtin_amdgcn_s_memtime();
+#define GRU_KSTAMP(i)                                                                   \
+  if (tid == 0 && pair == 0 && p == 0) {                                                \
+    const unsigned long long now_ = __builtin_amdgcn_s_memtime();                       \
+    st_acc[i] += now_ - st_last;                                                        \
+    st_last = now_;                                                                     \
+  }
+#else
+#define GRU_KSTAMP(i)
+#endif
+  int j = 0;
+  for (int grp = slot; grp < ngroups; grp += nslots, ++j) {
+    const int c0 = grp * 32;
+    const int nc = min(32, B - c0);
+    auto load_gi = [&](int s_, float (&v)[3]) {
+      const int t_ = dir ? T - 1 - s_ : s_;
+      if (gc < nc) {
+        const float* gp = G + ((int64_t)(c0 + gc) * T + t_) * 1536 + dir * 768 + uo;
+        v[0] = gp[0];
+        v[1] = gp[256];
+        v[2] = gp[512];
+      } else {
+        v[0] = v[1] = v[2] = 0.f;
+      }
+    };
+    float gcur[3];
+    load_gi(0, gcur);
+    float hreg = 0.f;                          // this thread's h(t-1): same (clip, unit) every step
+    for (int s = 0; s < T; ++s) {
+      const int gs = j * T + s;                // step of this pair; flags / parities are gs-based
+      const int t = dir ? T - 1 - s : s;
+      float gnext[3] = {0.f, 0.f, 0.f};
+      if (s + 1 < T) load_gi(s + 1, gnext);    // in flight across the wait and the product
+      // ---- product wave e: wait for slices 2e, 2e + 1 (step gs - 1).  At a
+      // group boundary the wait still runs (values discarded): a slice
+      // publishes step gs only after every slice finished reading gs - 2 ----
+      if (tid == 0) gru_forced_fail(spin_limit, gs, sync, host_err, &s_err);
+      if (gs > 0 && lane < 2) {
+        unsigned spins = 0;
+        while (!gru_dead(&s_err) && g_ld(Fl + (2 * e + lane) * 16) < (unsigned)gs) {
+          if (++spins > spin_limit) {
+            gru_fail(sync, host_err, 2u);
+            s_err = 1;
+            break;
+          }
+        }
+      }
+      GRU_KSTAMP(0);
+      float a[2][8];
+      if (s > 0) {
+        const float* src = Xs + ((gs - 1) & 1) * 32 * 256 + 32 * e + 8 * kk;
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+          const int c = 16 * mt + n16;
+          if (c < nc) {
+            const unsigned long long* q = reinterpret_cast<const unsigned long long*>(src + c * 256);
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+              const unsigned long long v = __hip_atomic_load(q + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              a[mt][2 * w] = __uint_as_float((uint32_t)v);
+              a[mt][2 * w + 1] = __uint_as_float((uint32_t)(v >> 32));
+            }
+          } else {
+#pragma unroll
+            for (int st = 0; st < 8; ++st) a[mt][st] = 0.f;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+          for (int st = 0; st < 8; ++st) a[mt][st] = 0.f;
+      }
+      GRU_KSTAMP(1);
+      f32x4_g acc[3][2];
+#pragma unroll
+      for (int g = 0; g < 3; ++g)
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) acc[g][mt] = f32x4_g{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int st = 0; st < 8; ++st)
+#pragma unroll
+        for (int g = 0; g < 3; ++g)
+#pragma unroll
+          for (int mt = 0; mt < 2; ++mt)
+            acc[g][mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[mt][st], Wf[g][st], acc[g][mt], 0, 0, 0);
+      // D[clip][unit]: lane (unit n16, kk) register i = clip 16 mt + 4 kk + i
+#pragma unroll
+      for (int g = 0; g < 3; ++g)
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) part[e][g][16 * mt + 4 * kk + i][n16] = acc[g][mt][i];
+      __syncthreads();
+      GRU_KSTAMP(2);
+      // ---- gate phase: thread (gc, gu) ----
+      float hv = 0.f;
+      if (gc < nc) {
+        float ghr = part[0][0][gc][gu], ghz = part[0][1][gc][gu], ghn = part[0][2][gc][gu];
+#pragma unroll
+        for (int q = 1; q < 8; ++q) {          // partials in K order
+          ghr += part[q][0][gc][gu];
+          ghz += part[q][1][gc][gu];
+          ghn += part[q][2][gc][gu];
+        }
+        ghr += br;
+        ghz += bz;
+        ghn += bn;
+        const float hn = gru_cell(gcur[0], gcur[1], gcur[2], ghr, ghz, ghn, hreg);
+        hv = gru_dead(&s_err) ? __builtin_nanf("") : hn;   // NaN propagates to every slice
+        __hip_atomic_store(reinterpret_cast<unsigned*>(Xs + (gs & 1) * 32 * 256 + gc * 256 + upos),
+                           __float_as_uint(hv), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      hreg = hv;
+      // every storing wave drains its payload stores, then one flag per slice;
+      // the barrier also orders this step's partial reads before the next
+      // step's partial writes
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) __hip_atomic_store(Fl + p * 16, (unsigned)(gs + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      GRU_KSTAMP(3);
+      // the H output is not part of the hand-off: stored after the flag
+      if (gc < nc) H[((int64_t)(c0 + gc) * T + t) * 512 + dir * 256 + uo] = hv;
+#pragma unroll
+      for (int g = 0; g < 3; ++g) gcur[g] = gnext[g];
+    }
+  }
+#ifdef SEDX_GRU_STAMPS
+  if (tid == 0 && pair == 0 && p == 0)
+    for (int i = 0; i < 4; ++i) sync->stamps[i] = st_acc[i];
+#endif
+#undef GRU_KSTAMP
+}
+
 size_t gru_coop_workspace_bytes(int B) {
   (void)B;
   // sync block, then the exchange space: 32-clip kernel 8 pairs x 2 parities
@@ -801,6 +1001,13 @@ void launch_gru_coop(const float* G, int B, int T, const float* whh, const float
   const size_t sync_bytes = (sizeof(GruSync) + 255) & ~size_t(255);
   float* X = reinterpret_cast<float*>(static_cast<char*>(ws) + sync_bytes);
   const bool valu = exact && B <= GRU_VALU_CLIPS;
+  if (exact && !valu && variant == 4) {   // K-split hand-off, 16 slices
+    const int ngroups = (B + 31) / 32;
+    const int nslots = ngroups < GRU_MAX_SLOTS ? ngroups : GRU_MAX_SLOTS;
+    (void)hipMemsetAsync(sync, 0, sync_bytes, s);
+    launch_kernel(gru_ksplit_kernel, dim3(128), 512, s, G, B, T, whh, bhh, H, X, sync, nslots, host_err, spin);
+    return;
+  }
   if (exact && !valu && variant != 2 && variant != 3) {
     auto* Xg = reinterpret_cast<unsigned long long*>(X);
     if (variant == 1)

@@ -271,7 +271,8 @@ size_t gru_coop_workspace_bytes(int B);
 // host_err (nullable): host-mapped word OR-ed with the failure code when a
 // bounded hand-off spin times out (outputs of that launch are then NaN).
 // variant (exact, B > 8): 2 the 32-clip flag hand-off kernel (default; x3
-// always), 0 the 16-clip data-tagged kernel with 16 slices, 1 with 8 slices.
+// always), 0 the 16-clip data-tagged kernel with 16 slices, 1 with 8 slices,
+// 3 the flag kernel on 16 slices, 4 the K-split hand-off on 16 slices.
 // spin: bound of every hand-off spin in polls (the handle's SEDX_TUNE_GRU_SPIN, 2^24 by default).
 void launch_gru_coop(const float* G, int B, int T, const float* whh, const float* bhh, float* H,
                      void* ws, bool exact, bool allow_fast, int variant, unsigned* host_err, unsigned spin,

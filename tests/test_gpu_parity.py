@@ -200,8 +200,9 @@ def test_gru_handoff_modes_bit_identical(prec):
 def test_gru_tag_kernels_bit_identical(n_clips):
     """The data-tagged recurrences (SEDX_GRU_KERNEL_TAG16 / TAG8: 16-clip
     groups, granules straight into v_mfma_f32_16x16x4_f32 operands) and the
-    16-slice cooperative kernel (COOP16: 16 units per workgroup on 16x16x4
-    MFMAs) keep the exact kernels' arithmetic contract (eight in-order K
+    16-slice cooperative kernels (COOP16: 16 units per workgroup on 16x16x4
+    MFMAs; KSPLIT: each K-eighth wave waits for and loads only its two
+    slices) keep the exact kernels' arithmetic contract (eight in-order K
     partials, summed in order): bit-identical to the 8-slice 32-clip kernel,
     ragged last group and more groups than resident slots (80 clips) included;
     AUTO (the default: COOP16 on an unpipelined handle) too."""
@@ -209,19 +210,19 @@ def test_gru_tag_kernels_bit_identical(n_clips):
     m = build(GRU).set_precision('exact')
     wave = synth.make_waveforms(n_clips, seconds=2.0, sample_rate=16000, seed=n_clips + 3)
     outs = {}
-    for knob in (0, 2, 3, 4, 5):     # COOP, TAG16, TAG8, COOP16, AUTO
+    for knob in (0, 2, 3, 4, 5, 6):     # COOP, TAG16, TAG8, COOP16, AUTO, KSPLIT
         _tune(m, _lib.TUNE_GRU_KERNEL, knob)
         outs[knob] = run(m, wave)['framewise_output']
     _tune(m, _lib.TUNE_GRU_KERNEL, 5)
     assert np.isfinite(outs[0]).all()
-    for knob in (2, 3, 4, 5):
+    for knob in (2, 3, 4, 5, 6):
         assert np.array_equal(outs[knob], outs[0]), knob
 
 
-@pytest.mark.parametrize('kernel,n_clips', [(0, 32), (4, 32), (0, 4), (2, 40)])
+@pytest.mark.parametrize('kernel,n_clips', [(0, 32), (4, 32), (0, 4), (2, 40), (6, 40)])
 def test_gru_spin_timeout_surfaces(kernel, n_clips):
     """A GRU hand-off spin that runs out (forced with SEDX_TUNE_GRU_SPIN = 0
-    polls: any wait that is not satisfied at once) turns that forward's outputs into NaN and is reported by
+    polls: every step that would wait fails, deterministically) turns that forward's outputs into NaN and is reported by
     sedx_check_error / model.check_error() once the batch is complete — for
     the 8- and 16-slice cooperative kernels, the small-batch VALU kernel and
     the data-tagged one; with the default bound the same handle is clean and
@@ -251,7 +252,7 @@ def test_gru_spin_timeout_surfaces(kernel, n_clips):
         finally:
             _tune(m, _lib.TUNE_GRU_SPIN, 1 << 24)
             _tune(m, _lib.TUNE_GRU_KERNEL, 5)
-        assert failed >= 1
+        assert failed == 4
         _tune(m, _lib.TUNE_GRU_KERNEL, kernel)
         out = m(wave)['framewise_output']
         torch.cuda.synchronize()
