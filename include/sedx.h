@@ -292,13 +292,12 @@ sedx_status sedx_set_precision(sedx_handle* h, int32_t mode);
  *                         sedx_check_error (tests force it with 0: every
  *                         step that would wait fails, whether or not its data
  *                         has arrived).
- *  SEDX_TUNE_WINO_ORDER   (winograd) 1 (default): the 512-channel layers run
- *                         each XCD's rounds of 32 concurrent items as 4 tile
- *                         blocks x 8 channel groups (8 weight slabs + 4 halos
- *                         per round through the XCD's L2 instead of 16 + 2:
- *                         b4c2 576 -> 383 MB of L2 fills per B = 32 launch,
- *                         b4c1 288 -> 192 MB, 1 % faster); 0: tile block
- *                         major.  Bit-identical outputs.
+ *  SEDX_TUNE_WINO_ORDER   (winograd) 1 (default): layers whose channel groups'
+ *                         weight slabs exceed ~8 MB together (the 512-channel
+ *                         layers) run each XCD's rounds of 32 concurrent items
+ *                         as 8 tile blocks x 4 channel groups of 64 (4 slabs
+ *                         per round through the XCD's L2 instead of 8);
+ *                         0: tile block major.  Bit-identical outputs.
  *
  * Co-residency: the cooperative GRU kernels need all workgroups of a
  * (32-clip group, direction) resident at once — 8 CUs (COOP) or 16 (COOP16)

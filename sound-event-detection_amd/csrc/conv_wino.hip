@@ -214,21 +214,22 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
   // item decode: item -> XCD id & 7; on one XCD, tile blocks in order, each
   // with its channel groups consecutive.  Padding items (tile blocks rounded
   // up to a multiple of 8) come last on their XCD.
-  // order2d (launcher: 16+ channel groups, whole rounds of 32 items per XCD,
-  // no padding tile blocks): each round of 32 consecutive items on an XCD —
-  // the ones its 32 resident workgroups run together — is 4 tile blocks x 8
-  // channel groups instead of 2 x 16, so per round the XCD's L2 streams 8
-  // weight slabs and 4 halos instead of 16 and 2 (fewer L2 misses on the
-  // 512-channel layers; a workgroup's successive items keep their slot in
-  // the round)
+  // order2d = G > 0 (launcher: more than G channel groups, whole rounds of
+  // 32 items per XCD, no padding tile blocks): each round of 32 consecutive
+  // items on an XCD — the ones its 32 resident workgroups run together — is
+  // 32 / G tile blocks x G channel groups instead of 32 / ngroups x ngroups,
+  // so per round the XCD's L2 streams G weight slabs (at most ~8 MB) instead
+  // of all of them (fewer L2 misses on the 512-input-channel layers; a
+  // workgroup's successive items keep their slot in the round)
   auto decode = [&](int item, int& b_, int& t0_, int& n0_) -> bool {
     const int xcd = item & 7, j = item >> 3;
     int jb, cgi;
     if (order2d) {
-      const int idx = j & 31, r = j >> 5, ncg = ngroups >> 3;
+      const int tbr = 32 / order2d;                // tile blocks per round
+      const int idx = j & 31, r = j >> 5, ncg = ngroups / order2d;
       const int tbg = r / ncg;
-      jb = 4 * tbg + (idx & 3);
-      cgi = 8 * (r - tbg * ncg) + (idx >> 2);
+      jb = tbr * tbg + idx % tbr;
+      cgi = order2d * (r - tbg * ncg) + idx / tbr;
     } else {
       jb = j / ngroups;
       cgi = j - jb * ngroups;
@@ -844,11 +845,24 @@ static void launch_wino_w(const float* in, int B, int T, int Cin, int Cout, cons
   const int64_t per = (nitems + WINO_ITEMS - 1) / WINO_ITEMS;
   const int64_t nwg = std::min<int64_t>(nitems, std::max<int64_t>(std::max<int64_t>(8, resident), (per + 7) / 8 * 8));
   dim3 grid((unsigned)nwg);
-  // 4 x 8 rounds: 16+ channel groups in whole groups of 8, whole groups of 4
-  // tile blocks per XCD with no padding, and a grid of whole 32-item rounds
-  // per XCD (a workgroup keeps its slot in the round from item to item)
-  const int order2d = order && ngroups >= 16 && ngroups % 8 == 0 && tblocks % 32 == 0 && nwg % 256 == 0 &&
-                      (nitems / 8) % 32 == 0;
+  // rounds of 32 / G tile blocks x G channel groups: the G (< ngroups,
+  // dividing it) whose round streams the fewest bytes through the XCD's L2 —
+  // G weight slabs (16 Cin NCH floats each) + 32 / G halos (PL Cin floats) —
+  // with whole rounds of tile blocks per XCD, no padding, and a grid of whole
+  // 32-item rounds per XCD (a workgroup keeps its slot in the round from item
+  // to item).  (b4c2: 4 slabs of 2 MB + 8 halos of 0.7 MB instead of 8 + 4.)
+  int order2d = 0;
+  if (order && nwg % 256 == 0 && (nitems / 8) % 32 == 0) {
+    const int64_t slab = (int64_t)16 * Cin * G::NCH * 4, halo = (int64_t)G::PL * Cin * 4;
+    int64_t best = (int64_t)ngroups * slab + (32 / std::min(ngroups, 32)) * halo;   // the default order
+    for (int gr = 1; gr <= 8 && gr < ngroups; gr *= 2) {
+      const int64_t bytes = gr * slab + (32 / gr) * halo;
+      if (ngroups % gr == 0 && tblocks % (8 * (32 / gr)) == 0 && bytes < best) {
+        best = bytes;
+        order2d = gr;
+      }
+    }
+  }
 #define SEDX_WG_LAUNCH(E)                                                                              \
   {                                                                                                    \
     auto* k_ = conv3x3_wino_kernel<F, E, TG, NT>;                                                      \

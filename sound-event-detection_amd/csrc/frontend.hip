@@ -857,20 +857,43 @@ __global__ __launch_bounds__(GAMMA_SPEC_THREADS) void gamma_spec_kernel(GammaPar
       load(fr + gridDim.x, v);
       continue;
     }
+    const double2* Z;
+    if constexpr (PER == 4 && zradix<N2, 1>() == 4 && N2 / 4 == P) {
+      // (nfft 2048) the first radix-4 stage's butterfly of thread tid reads
+      // exactly the samples it owns (m = tid + 256 i): computed from its
+      // registers, so the windowed frame never goes through LDS (one LDS
+      // write + read pass and one barrier fewer per frame)
+      double2 u[4];
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int m = tid + P * i;
-      X[m] = make_double2(wv[i].x * (double)v[i].x, wv[i].y * (double)v[i].y);
+      for (int i = 0; i < 4; ++i) u[i] = make_double2(wv[i].x * (double)v[i].x, wv[i].y * (double)v[i].y);
+      load(fr + gridDim.x, v);  // next frame's samples, in flight during this FFT
+      const double2 a0 = zadd(u[0], u[2]), a1 = zsub(u[0], u[2]);
+      const double2 b0 = zadd(u[1], u[3]), b1 = zsub(u[1], u[3]);
+      const double2 mib1 = make_double2(b1.y, -b1.x);
+      Y[4 * tid] = zadd(a0, b0);
+      Y[4 * tid + 1] = zadd(a1, mib1);
+      Y[4 * tid + 2] = zsub(a0, b0);
+      Y[4 * tid + 3] = zsub(a1, mib1);
+      __syncthreads();
+      Z = zstockham<N2, 4, P, 0>(Y, X, tw, tid);
+    } else {
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        const int m = tid + P * i;
+        X[m] = make_double2(wv[i].x * (double)v[i].x, wv[i].y * (double)v[i].y);
+      }
+      load(fr + gridDim.x, v);  // next frame's samples, in flight during this FFT
+      __syncthreads();
+      Z = zstockham<N2, 1, P, 0>(X, Y, tw, tid);
     }
-    load(fr + gridDim.x, v);    // next frame's samples, in flight during this FFT
-    __syncthreads();
-    const double2* Z = zstockham<N2, 1, P, 0>(X, Y, tw, tid);
 #pragma unroll
     for (int i = 0; i < UB; ++i) {
       const int k = tid + P * i;
       if (k < NB) {
         const double2 Xk = zreal_bin<N2>(Z, twu[i], k);
-        row[k] = hypot(Xk.x, Xk.y);   // numpy abs(complex)
+        // numpy abs(complex) is hypot; sqrt(x^2 + y^2) with one fma is within an
+        // ulp of it (the int16 codes are ~3e-5 relative apart: identical)
+        row[k] = sqrt(fma(Xk.x, Xk.x, Xk.y * Xk.y));
       }
     }
     for (int k = NB + tid; k < p.kp; k += P) row[k] = 0.0;   // row padding
