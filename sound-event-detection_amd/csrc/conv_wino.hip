@@ -49,6 +49,7 @@
 namespace sedx {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4w __attribute__((ext_vector_type(4)));
 
 // TG tile groups (32 tiles each) x 32 NT channels per workgroup, 4 TG waves.
 // C1 (block 1, F = 64): the input is the bn0 output X0 [B][T][64] and conv1
@@ -94,7 +95,10 @@ struct WinoGeom {
   // from LDS, the epilogue's bias needs no vmcnt wait (which would also wait
   // for the next item's DMAs in flight)
   static constexpr int BIAS_OFF = XA_OFF + 2 * X0_SZ, BIAS_MAX = 512;
-  static constexpr int LDS_BYTES = 4 * (BIAS_OFF + BIAS_MAX);   // ring, epilogue exchange, X0 tiles, biases
+  // C1 with conv1 on the matrix pipe: conv1's weights [64 ch][9] (3 DMA
+  // units, zero-padded) and biases (1 unit), LDS-DMA'd in the prologue
+  static constexpr int W1_OFF = BIAS_OFF + BIAS_MAX, W1_SZ = C1 ? 1024 : 0;
+  static constexpr int LDS_BYTES = 4 * (W1_OFF + W1_SZ);   // ring, epilogue exchange, X0 tiles, biases, conv1 weights
   static constexpr int WG_PER_CU = WAVES == 8 || LDS_BYTES > 80 * 1024 ? 1 : 2;
   static_assert(NT == 1 || NT == 2, "channel tiles per wave");
   static_assert(P % FT == 0, "whole tile rows per workgroup");
@@ -116,6 +120,11 @@ struct WinoGeom {
 // LDS reads, 16 the DMAs of the chunk operands.
 #ifndef SEDX_WINO_ABL
 #define SEDX_WINO_ABL 0
+#endif
+// block 1's conv1 on the matrix pipe (v_mfma_f32_4x4x1f32, 16 blocks) instead
+// of VALU fma chains: the same fma chain per (pixel, channel)
+#ifndef SEDX_WINO_C1MFMA
+#define SEDX_WINO_C1MFMA 0
 #endif
 // VALU instructions per MFMA in the second half of a chunk step (tuning builds)
 #ifndef SEDX_WINO_VG
@@ -404,10 +413,31 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
     }
     *reinterpret_cast<float4*>(smem + cb * G::BUF + 4 * pslot) = make_float4(y[0], y[1], y[2], y[3]);
   };
+  // on the matrix pipe: v_mfma_f32_4x4x1f32 (16 blocks of 4 x 4, K = 1;
+  // tools/mfma4x4_probe.cpp): lane l = 4 b + t supplies A[t][0] of block b
+  // (the weight of channel 4 cc + t for tap k, from LDS) and B[0][t] (tap k
+  // of its own pixel) and receives D[0..3][t] of block b — channels 4 cc ..
+  // 4 cc + 3 of its pixel, i.e. the chunk's [pixel][4 ch] halo slot.  Nine
+  // MFMAs from zero are the VALU form's fma chain over the taps in order
+  [[maybe_unused]] auto conv1m = [&](int cc, int cb) {
+    const float* wl = smem + G::W1_OFF + 9 * (4 * cc + (lane & 3));
+    f32x4w d = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int k = 0; k < 9; ++k) d = __builtin_amdgcn_mfma_f32_4x4x1f32(wl[k], xw[k], d, 0, 0, 0);
+    const float4 bq = *reinterpret_cast<const float4*>(smem + G::W1_OFF + 768 + 4 * cc);
+    const float y0 = fmaxf(d[0] + bq.x, 0.0f), y1 = fmaxf(d[1] + bq.y, 0.0f);
+    const float y2 = fmaxf(d[2] + bq.z, 0.0f), y3 = fmaxf(d[3] + bq.w, 0.0f);
+    *reinterpret_cast<float4*>(smem + cb * G::BUF + 4 * pslot) =
+        c1_ov ? make_float4(y0, y1, y2, y3) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  };
   [[maybe_unused]] auto conv1 = [&](int cc, int cb) {
-    float wq[40];
-    c1_weights(cc, wq);
-    conv1w(wq, cb);
+    if constexpr (SEDX_WINO_C1MFMA) {
+      conv1m(cc, cb);
+    } else {
+      float wq[40];
+      c1_weights(cc, wq);
+      conv1w(wq, cb);
+    }
   };
 
   f32x16 acc[4][NT];
@@ -533,6 +563,18 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
         (uint32_t)(size_t)(__attribute__((address_space(3))) float*)(smem + G::BIAS_OFF + 256 * wv);
     sedx_glds16(i < Cout ? bias + i : zero16, __builtin_amdgcn_readfirstlane(m0_));
     asm volatile("" ::: "memory");
+  }
+  if constexpr (C1 && SEDX_WINO_C1MFMA) {
+    // conv1's weights (units 0-2: waves 2-4) and biases (wave 5), before the
+    // ring: covered by the prologue's first wait like the biases
+    if (wv >= 2 && wv < 6) {   // wave-uniform
+      const int i = 256 * (wv - 2) + 4 * lane;
+      const float* src = wv < 5 ? (i < 576 ? w1 + i : zero16) : (4 * lane < 64 ? b1 + 4 * lane : zero16);
+      const uint32_t m0_ =
+          (uint32_t)(size_t)(__attribute__((address_space(3))) float*)(smem + G::W1_OFF + 256 * (wv - 2));
+      sedx_glds16(src, __builtin_amdgcn_readfirstlane(m0_));
+      asm volatile("" ::: "memory");
+    }
   }
   if constexpr (C1) x0_dma(b, t0, 0);
 #pragma unroll
