@@ -554,6 +554,15 @@ def clip_leg(model, wave, args, world, rank, dev, precision, isolated=False):
     return value, elapsed, stage_ms, p50, p99, iso
 
 
+def gamma_profile(B):
+    """(HBM bytes, rocprofv3 ms) per batch of the gammatone frontend's launches
+    from the config-4 PMC passes (B = 32 only; else (None, None))."""
+    prof = [profiled(k, GAMMA_PROFILE_SUMMARY) for k in GAMMA_KERNELS] if B == 32 else []
+    traffic = sum(p[0] for p in prof) if prof and all(p[0] is not None for p in prof) else None
+    rocprof_ms = sum(p[1] for p in prof) if prof and all(p[1] is not None for p in prof) else None
+    return traffic, rocprof_ms
+
+
 def gamma_leg(args, dev, precision):
     """BASELINE config 4: Cnn_9layers_Gru_FrameAtt gammatone 32k, B=32.  A
     step = float64 gammatone features of 32 x 10 s @ 32 kHz clips (the
@@ -587,10 +596,7 @@ def gamma_leg(args, dev, precision):
     T = 994
     flops = B * (T * (5.0 * 1024 * 10 + 8.0 * 1025) + 2.0 * 64 * 1025 * T)   # FFT + unpack/|X| + ERB product
     bytes_ = B * (320000 * 4 + 64 * T * 4)
-    # HBM bytes per batch of the frontend's launches (PMC passes of --mode gamma)
-    prof = [profiled(k, GAMMA_PROFILE_SUMMARY) for k in GAMMA_KERNELS] if B == 32 else []
-    traffic = sum(p[0] for p in prof) if prof and all(p[0] is not None for p in prof) else None
-    rocprof_fe = sum(p[1] for p in prof) if prof and all(p[1] is not None for p in prof) else None
+    traffic, rocprof_fe = gamma_profile(B)
     return {'workload': 'Cnn_9layers_Gru_FrameAtt gammatone 32k, %d x 10 s @ 32 kHz clips per step '
                         '(float64 gammatone features + forward)' % B,
             'value': round(value, 2), 'unit': 'clips/s', 'dtype': DTYPE[precision] + '; gammatone frontend f64',

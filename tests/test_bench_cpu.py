@@ -152,3 +152,18 @@ def test_bench_launcher_fails_when_a_rank_fails():
                        capture_output=True, text=True, timeout=300, cwd=REPO, env=_bench_env())
     assert r.returncode != 0
     assert not [ln for ln in r.stdout.splitlines() if ln.startswith('{')]
+
+
+def test_config4_profile_fields(bench):
+    """Config 4 (gammatone 32k, T = 994 frames) reads its own committed
+    profile: the conv roofline's HBM traffic and the gamma frontend's bytes
+    and rocprof time per batch are filled (round 3 left them null because
+    only the (32, 1001) shapes were looked up)."""
+    stage = {s: 0.2 for s in bench.CONV_STAGES}
+    stage['b1c2'] = 1.0
+    r = bench.roofline(stage, 32, 'winograd', T=994, summary=bench.GAMMA_PROFILE_SUMMARY)
+    assert r['traffic'] is not None and r['traffic'] > 0
+    assert r['traffic_source'].endswith('config4_kernel_summary.json')
+    traffic, ms = bench.gamma_profile(32)
+    assert traffic is not None and traffic > 49e6 and ms is not None and 0.0 < ms < 1.0
+    assert bench.gamma_profile(8) == (None, None)
