@@ -570,6 +570,8 @@ def gamma_leg(args, dev, precision):
     361-370) + the gamma-branch forward (models.py:636-688)."""
     name = MODEL_NAMES['gru']
     m = build_model(name, dev, (32000, 1024, 320, 64, 50, 14000), 'gamma').set_precision(precision)
+    if getattr(args, 'gamma_spec', None) is not None:
+        m.set_tuning(_lib.TUNE_GAMMA_SPEC, args.gamma_spec)
     B = args.batch
     audio = torch.from_numpy(synth.make_waveforms(B, 10.0, 32000, seed=4321)).to(dev)
 
@@ -773,6 +775,8 @@ def main():
                          '(the 8-slice kernel on a pipelined handle, 16 slices one batch at a time)')
     ap.add_argument('--wino-order', type=int, choices=[0, 1], default=None,
                     help='SEDX_TUNE_WINO_ORDER (A/B runs): Winograd item order on the 512-channel layers')
+    ap.add_argument('--gamma-spec', type=int, choices=[0, 1], default=None,
+                    help='SEDX_TUNE_GAMMA_SPEC (A/B runs): gammatone spectrum kernel (config 4)')
     ap.add_argument('--ab-package', default=None,
                     help='A/B runs: load sedx from this package directory instead of the in-tree build '
                          '(recorded in the JSON line as "library")')

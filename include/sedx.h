@@ -292,6 +292,11 @@ sedx_status sedx_set_precision(sedx_handle* h, int32_t mode);
  *                         sedx_check_error (tests force it with 0: every
  *                         step that would wait fails, whether or not its data
  *                         has arrived).
+ *  SEDX_TUNE_GAMMA_SPEC   (gammatone, nfft 2048) 0 (default): the spectrum
+ *                         as a 256-thread Stockham FFT per frame; 1: one
+ *                         wave per frame (16 x 16 x 4 four-step in registers,
+ *                         wave-local transposes).  Same int16 codes in every
+ *                         test (f64 sums in another order).
  *  SEDX_TUNE_WINO_ORDER   (winograd) 1 (default): layers whose channel groups'
  *                         weight slabs exceed ~8 MB together (the 512-channel
  *                         layers) run each XCD's rounds of 32 concurrent items
@@ -312,7 +317,8 @@ typedef enum {
   SEDX_TUNE_WINO_BLOCK1 = 2,
   SEDX_TUNE_MEL_MFMA = 3,
   SEDX_TUNE_GRU_SPIN = 4,
-  SEDX_TUNE_WINO_ORDER = 5
+  SEDX_TUNE_WINO_ORDER = 5,
+  SEDX_TUNE_GAMMA_SPEC = 6
 } sedx_tuning_knob;
 enum {
   SEDX_GRU_KERNEL_COOP = 0,

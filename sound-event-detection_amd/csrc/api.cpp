@@ -94,6 +94,7 @@ struct sedx_handle {
   int mel_mfma = 0;                        // SEDX_TUNE_MEL_MFMA (measured slower: opt-in)
   unsigned gru_spin = 1u << 24;            // SEDX_TUNE_GRU_SPIN: bound of every GRU hand-off spin (polls)
   int wino_order = 1;                      // SEDX_TUNE_WINO_ORDER (4 x 8 rounds on the 512-channel layers)
+  int gamma_spec = 0;                      // SEDX_TUNE_GAMMA_SPEC
   // sedx_set_capture: copy one stage's output of every later forward
   int cap_stage = -1;
   float* cap_buf = nullptr;
@@ -643,6 +644,10 @@ sedx_status sedx_set_tuning(sedx_handle* h, int32_t knob, int32_t value) {
     case SEDX_TUNE_WINO_ORDER:
       if (value != 0 && value != 1) break;
       h->wino_order = value;
+      return SEDX_OK;
+    case SEDX_TUNE_GAMMA_SPEC:
+      if (value != 0 && value != 1) break;
+      h->gamma_spec = value;
       return SEDX_OK;
     default:
       return fail(h, SEDX_EINVAL, "unknown tuning knob %d", (int)knob);
@@ -1290,7 +1295,7 @@ sedx_status sedx_gamma_features(sedx_handle* h, const float* d_audio, int64_t B,
   base += al((size_t)B * 64 * T * sizeof(double));
   p.mm = reinterpret_cast<unsigned long long*>(base);
   p.out = d_feat;
-  launch_gamma(p, s);
+  launch_gamma(p, s, h->gamma_spec);
   return launch_status(h);
 }
 

@@ -901,6 +901,168 @@ __global__ __launch_bounds__(GAMMA_SPEC_THREADS) void gamma_spec_kernel(GammaPar
   }
 }
 
+// ---------------------------------------------------------------------------
+// nfft 2048, one WAVE per frame (round 4, SEDX_TUNE_GAMMA_SPEC 1): the
+// 1024-point complex FFT of the packed frame as a 16 x 16 x 4 four-step in
+// registers (each lane 16 complex values), with wave-local LDS transposes
+// between the passes — no workgroup barrier, 16 values of independent work
+// per lane.  m = l + 64 j (lane l holds j = 0..15), k = p + 16 q:
+//   pass 1 (lane l):       Y[l][p]  = DFT16_j z[l + 64 j]  x  W1024^(l p)
+//   pass 2 (lane 4 p + s): R[p][s][u] = DFT16_r Y[s + 4 r][p]  x  W64^(s u)
+//   pass 3 (lane 4 p + w): Z[p + 16 u + 256 v] = DFT4_s R[p][s][u], u = 4 w + c
+// then the real-spectrum unpack of bins l + 64 i (+ 1024) from Z[k] and
+// Z[1024 - k] (a third transpose) and sqrt(fma) magnitudes, coalesced row
+// stores.  The window and every twiddle a lane uses stay in its registers
+// for the whole launch (one wave per SIMD).
+__device__ __forceinline__ void zdft4(double2& x0, double2& x1, double2& x2, double2& x3) {
+  const double2 a0 = zadd(x0, x2), a1 = zsub(x0, x2);
+  const double2 b0 = zadd(x1, x3), b1 = zsub(x1, x3);
+  const double2 mib1 = make_double2(b1.y, -b1.x);   // -i (x1 - x3)
+  x0 = zadd(a0, b0);
+  x1 = zadd(a1, mib1);
+  x2 = zsub(a0, b0);
+  x3 = zsub(a1, mib1);
+}
+// v[j] -> V[p] = sum_j v[j] W16^(j p), in place (natural order out);
+// w16[k] = W16^k for k = 0..9 (only 1, 2, 3, 4, 6, 9 used)
+__device__ __forceinline__ void zdft16(double2 (&v)[16], const double2 (&w16)[10]) {
+  // j = j1 + 4 j2: DFT4 over j2 for each j1 -> a[j1][p2] (stored back in v[j1 + 4 p2])
+#pragma unroll
+  for (int j1 = 0; j1 < 4; ++j1) zdft4(v[j1], v[j1 + 4], v[j1 + 8], v[j1 + 12]);
+  // twiddle a[j1][p2] by W16^(j1 p2)
+#pragma unroll
+  for (int j1 = 1; j1 < 4; ++j1)
+#pragma unroll
+    for (int p2 = 1; p2 < 4; ++p2) v[j1 + 4 * p2] = zmul(v[j1 + 4 * p2], w16[j1 * p2]);
+  // DFT4 over j1 for each p2: V[p2 + 4 p1]
+  double2 o[16];
+#pragma unroll
+  for (int p2 = 0; p2 < 4; ++p2) {
+    double2 x0 = v[4 * p2], x1 = v[4 * p2 + 1], x2 = v[4 * p2 + 2], x3 = v[4 * p2 + 3];
+    zdft4(x0, x1, x2, x3);
+    o[p2] = x0;
+    o[p2 + 4] = x1;
+    o[p2 + 8] = x2;
+    o[p2 + 12] = x3;
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) v[i] = o[i];
+}
+
+constexpr int GSW_WAVES = 4;                 // waves (frames in flight) per workgroup
+constexpr int GSW_LD = 1024 + 64 + 16;       // complex per wave buffer (padded layouts below)
+__global__ __launch_bounds__(64 * GSW_WAVES, 1) void gamma_spec_wave_kernel(GammaParams p) {
+  extern __shared__ double2 s_gsw[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  double2* buf = s_gsw + wave * GSW_LD;
+  const int pp = lane >> 2, qs = lane & 3;   // pass 2 / 3 roles: (p, s) and (p, w)
+  // registers for the whole launch: window of the lane's samples, twiddles
+  double2 win[16], tw1[16], tw2[16], tw3[16], w16[10];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int m = lane + 64 * j;
+    win[j] = make_double2(p.window[2 * m], p.window[2 * m + 1]);
+    tw1[j] = p.twiddle[2 * ((lane * j) & 1023)];          // W1024^(l p), p = j
+    tw2[j] = p.twiddle[32 * qs * j];                       // W64^(s u), u = j
+    tw3[j] = p.twiddle[lane + 64 * j];                     // W2048^k, k = l + 64 i
+  }
+#pragma unroll
+  for (int k = 0; k < 10; ++k) w16[k] = p.twiddle[128 * k];
+  const double2 twn = p.twiddle[1024 & (p.nfft - 1)];     // bin 1024 (W2048^1024 = -1)
+  const int64_t total = (int64_t)p.B * p.T;
+  const int64_t step = (int64_t)gridDim.x * GSW_WAVES;
+  auto load = [&](int64_t fr, float2 (&v)[16]) {
+    const int64_t b = fr / p.T;
+    const int t = (int)(fr - b * p.T);
+    if (fr >= total || t >= p.T_fill) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) v[j] = make_float2(0.f, 0.f);
+      return;
+    }
+    const float2* src = reinterpret_cast<const float2*>(p.audio + b * p.L + (int64_t)t * p.hop);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = src[lane + 64 * j];
+  };
+  float2 xs[16];
+  int64_t fr = (int64_t)blockIdx.x * GSW_WAVES + wave;
+  load(fr, xs);
+  for (; fr < total; fr += step) {
+    const int64_t b = fr / p.T;
+    const int t = (int)(fr - b * p.T);
+    double* row = p.mag + fr * p.kp;
+    if (t >= p.T_fill) {        // column never written by specgram's loop: zeros
+      for (int k = lane; k < p.kp; k += 64) row[k] = 0.0;
+      load(fr + step, xs);
+      continue;
+    }
+    double2 v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = make_double2(win[j].x * (double)xs[j].x, win[j].y * (double)xs[j].y);
+    load(fr + step, xs);        // next frame's samples, in flight during this FFT
+    // ---- pass 1: DFT16 over j, twiddle, transpose: buf[p * 65 + l] ----
+    zdft16(v, w16);
+#pragma unroll
+    for (int q = 1; q < 16; ++q) v[q] = zmul(v[q], tw1[q]);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) buf[q * 65 + lane] = v[q];
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // ---- pass 2: lane (p, s) reads Y[s + 4 r][p] = buf[p * 65 + s + 4 r] ----
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = buf[pp * 65 + qs + 4 * r];
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    zdft16(v, w16);
+#pragma unroll
+    for (int u = 1; u < 16; ++u) v[u] = zmul(v[u], tw2[u]);
+    // R[p][s][u = 4 w + c] -> buf[(4 p + w) * 17 + 4 s + c]
+#pragma unroll
+    for (int u = 0; u < 16; ++u) buf[(4 * pp + (u >> 2)) * 17 + 4 * qs + (u & 3)] = v[u];
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // ---- pass 3: lane (p, w) reads R[p][s][4 w + c] for s, c ----
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = buf[lane * 17 + i];   // v[4 s + c]
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // DFT4 over s for each c: Z[p + 16 (4 w + c) + 256 v] -> buf[k + (k >> 4)]
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      double2 x0 = v[c], x1 = v[4 + c], x2 = v[8 + c], x3 = v[12 + c];
+      zdft4(x0, x1, x2, x3);
+      const int k0 = pp + 16 * (4 * qs + c);
+      buf[k0 + (k0 >> 4)] = x0;
+      buf[k0 + 256 + ((k0 + 256) >> 4)] = x1;
+      buf[k0 + 512 + ((k0 + 512) >> 4)] = x2;
+      buf[k0 + 768 + ((k0 + 768) >> 4)] = x3;
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // ---- unpack bins l + 64 i (and 1024 on lane 0), magnitudes ----
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int k = lane + 64 * i;
+      const int kn = (1024 - k) & 1023;
+      const double2 A = buf[k + (k >> 4)];
+      const double2 Bz = buf[kn + (kn >> 4)];
+      const double2 E = make_double2(0.5 * (A.x + Bz.x), 0.5 * (A.y - Bz.y));
+      const double2 O = make_double2(0.5 * (A.y + Bz.y), -0.5 * (A.x - Bz.x));
+      const double2 Xk = zadd(E, zmul(tw3[i], O));
+      row[k] = sqrt(fma(Xk.x, Xk.x, Xk.y * Xk.y));
+    }
+    if (lane == 0) {            // bin 1024: A = Bz = Z[0]
+      const double2 A = buf[0];
+      const double2 E = make_double2(A.x, 0.0);
+      const double2 O = make_double2(A.y, 0.0);
+      const double2 Xk = zadd(E, zmul(twn, O));
+      row[1024] = sqrt(fma(Xk.x, Xk.x, Xk.y * Xk.y));
+    }
+    for (int k = 1025 + lane; k < p.kp; k += 64) row[k] = 0.0;   // row padding
+    __builtin_amdgcn_wave_barrier();   // this frame's reads before the next frame's writes
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+}
+
 __device__ __forceinline__ unsigned long long d2ord(double d) {
   const unsigned long long u = (unsigned long long)__double_as_longlong(d);
   return (u & 0x8000000000000000ull) ? ~u : (u | 0x8000000000000000ull);
@@ -1067,9 +1229,18 @@ static void launch_gamma_spec(const GammaParams& p, hipStream_t s) {
   hipLaunchKernelGGL(gamma_spec_kernel<NFFT>, dim3((unsigned)blocks), dim3(GAMMA_SPEC_THREADS), li.dyn, s, p);
 }
 
-void launch_gamma(const GammaParams& p, hipStream_t s) {
+void launch_gamma(const GammaParams& p, hipStream_t s, int spec_variant) {
   hipLaunchKernelGGL(gamma_init_kernel, dim3((p.B + 255) / 256), dim3(256), 0, s, p.mm, p.B);
-  if (p.nfft == 2048)
+  if (p.nfft == 2048 && spec_variant == 1 && p.L % 2 == 0 && p.hop % 2 == 0) {   // float2 sample loads
+    const void* k = reinterpret_cast<const void*>(gamma_spec_wave_kernel);
+    const size_t lds = (size_t)GSW_WAVES * GSW_LD * sizeof(double2);
+    const LaunchInfo li = launch_info(k, 64 * GSW_WAVES, lds);
+    if (!li.ok) return;
+    const int64_t frames = (int64_t)p.B * p.T;
+    int64_t blocks = std::min<int64_t>((frames + GSW_WAVES - 1) / GSW_WAVES, (int64_t)li.ncu * li.per_cu);
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(gamma_spec_wave_kernel, dim3((unsigned)blocks), dim3(64 * GSW_WAVES), li.dyn, s, p);
+  } else if (p.nfft == 2048)
     launch_gamma_spec<2048>(p, s);
   else if (p.nfft == 1024)
     launch_gamma_spec<1024>(p, s);

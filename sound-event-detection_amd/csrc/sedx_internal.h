@@ -86,7 +86,8 @@ int gamma_kp(int nfft);
 void gamma_tables(double fs, int nfft, int nwin, int nfilts, double fmin, std::vector<double>& weightsT,
                   int kp, std::vector<double>& twiddle, std::vector<double>& window);
 size_t gamma_workspace_bytes(int64_t B, int64_t T, int nfft);
-void launch_gamma(const GammaParams& p, hipStream_t s);
+// spec_variant (nfft 2048): 0 the workgroup Stockham spectrum, 1 one wave per frame
+void launch_gamma(const GammaParams& p, hipStream_t s, int spec_variant = 0);
 
 // ---- conv stack -----------------------------------------------------------
 // bn0 output X0 [B][T][64] -> zero-bordered [B][T+2][66] (block1_pad_floats)

@@ -25,6 +25,7 @@ EXPORTS = ['sedx_create', 'sedx_destroy', 'sedx_last_error', 'sedx_version', 'se
            'sedx_resample_workspace_size', 'sedx_resample', 'sedx_gamma_workspace_size',
            'sedx_set_tuning', 'sedx_set_capture', 'sedx_window_starts', 'sedx_merge_host', 'sedx_check_error']
 TUNE_GRU_KERNEL, TUNE_GRU_HANDOFF, TUNE_WINO_BLOCK1, TUNE_MEL_MFMA, TUNE_GRU_SPIN, TUNE_WINO_ORDER = 0, 1, 2, 3, 4, 5
+TUNE_GAMMA_SPEC = 6
 PRECISION = {'exact': 0, 'x3': 1, 'winograd': 2}
 STAGES = ['frontend', 'b1c1', 'b1c2', 'b2c1', 'b2c2', 'b3c1', 'b3c2', 'b4c1', 'b4c2', 'seq', 'head']
 

@@ -464,13 +464,17 @@ def test_gamma(golden_dir):
         assert e <= TOL
 
 
+@pytest.mark.parametrize('spec', [0, 1])
 @pytest.mark.parametrize('seconds,seed', [(10.0, 5), (10.0, 6), (3.3, 7)])
-def test_gamma_codes_vs_oracle(seconds, seed):
+def test_gamma_codes_vs_oracle(seconds, seed, spec):
     """Bit-exact int16 codes against the oracle's numpy float64 restatement on
     other clips, incl. a clip whose last specgram column stays unfilled
-    (the frame count divides exactly: range(0, s - n, h) stops one short)."""
-    from sedx import inference
+    (the frame count divides exactly: range(0, s - n, h) stops one short) —
+    with either spectrum kernel (SEDX_TUNE_GAMMA_SPEC 0: workgroup Stockham,
+    1: one wave per frame)."""
+    from sedx import inference, _lib
     m = build(GRU, P32, 'gamma')
+    m.set_tuning(_lib.TUNE_GAMMA_SPEC, spec)
     audio = synth.make_waveforms(3, seconds=seconds, sample_rate=32000, seed=seed)
     if seconds != 10.0:
         L = 2048 + 320 * 300                      # (L - nfft) % hop == 0
