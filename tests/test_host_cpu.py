@@ -267,3 +267,19 @@ def test_dataparallel_replicas_reuse_the_source_handle(monkeypatch):
     assert c._weights_source() is c
     buf = io.BytesIO()
     torch.save(m, buf)
+
+
+def test_python_tuning_constants_match_the_header():
+    """The ctypes mirror's knob numbers (sedx/_lib.py) and bench.py's GRU
+    kernel table are the values include/sedx.h declares (a drifted number
+    would silently A/B the wrong implementation)."""
+    import re
+    from sedx import _lib
+    import bench
+    hdr = open(os.path.join(REPO, 'include', 'sedx.h')).read()
+    enum = {m.group(1): int(m.group(2)) for m in re.finditer(r'\b(SEDX_[A-Z0-9_]+)\s*=\s*(\d+)', hdr)}
+    for name in ('GRU_KERNEL', 'GRU_HANDOFF', 'WINO_BLOCK1', 'MEL_MFMA', 'GRU_SPIN', 'WINO_ORDER', 'GAMMA_SPEC'):
+        assert getattr(_lib, 'TUNE_' + name) == enum['SEDX_TUNE_' + name], name
+    for key, name in (('coop', 'COOP'), ('simple', 'SIMPLE'), ('tag16', 'TAG16'), ('tag8', 'TAG8'),
+                      ('coop16', 'COOP16'), ('auto', 'AUTO'), ('ksplit', 'KSPLIT')):
+        assert bench.GRU_KERNELS[key] == enum['SEDX_GRU_KERNEL_' + name], key
