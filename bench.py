@@ -83,8 +83,8 @@ PEAK_TF = {'exact': 157.3, 'winograd': 157.3, 'x3': 2500.0 / 3}
 PEAK_HBM_GBPS = 8000.0
 PEAK_FP64_TF = 78.6        # MI355X datasheet FP64 vector (not in MI355X_MICROARCH.md)
 DTYPE = {'exact': 'f32',
-         'winograd': 'f32 (conv2 of block 1 and blocks 2-4 as Winograd F(2x2,3x3): f32 transforms, f32 MFMA, '
-                     'f32 accumulate)',
+         'winograd': 'f32 (conv2 of block 1 as Winograd F(2x2,3x3), blocks 2-4 as Winograd F(4x4,3x3): f32 '
+                     'transforms, f32 MFMA, f32 accumulate)',
          'x3': 'bf16x3-split (3 bf16 MFMAs per f32 MAC: hi*hi + hi*lo + lo*hi, f32 accumulate)'}
 # Winograd F(2x2,3x3): 16 matrix-pipe multiplies per 2x2 output tile where the
 # direct conv does 36 ('winograd' mode: blocks 2-4, and block 1's conv2 unless
@@ -92,12 +92,23 @@ DTYPE = {'exact': 'f32',
 # separate conv1 launch, 2 computes conv1 inside the Winograd launch)
 WINO_BLOCK1 = 2
 WINO_MUL = 16.0 / 36.0
+# blocks 2-4 as Winograd F(4x4,3x3) (SEDX_TUNE_WINO_F43, the library default):
+# 36 multiplies per 4x4 output tile where the direct conv does 144
+WINO_F43 = 1
+WINO43_MUL = 36.0 / 144.0
 # SEDX_TUNE_GRU_KERNEL values (include/sedx.h)
 GRU_KERNELS = {'coop': 0, 'simple': 1, 'tag16': 2, 'tag8': 3, 'coop16': 4, 'auto': 5, 'ksplit': 6}
 
 
 def wino_stages():
     return (('b1c2',) if WINO_BLOCK1 else ()) + ('b2c1', 'b2c2', 'b3c1', 'b3c2', 'b4c1', 'b4c2')
+
+
+def wino_mul(stage):
+    """Matrix-pipe multiplies of a winograd-mode stage per direct-conv multiply."""
+    if stage not in wino_stages():
+        return 1.0
+    return WINO43_MUL if (WINO_F43 and stage != 'b1c2') else WINO_MUL
 # conv stages of sedx_stage_times: (F, Cin, Cout, number of 2x poolings before it)
 CONV_STAGES = {'b1c2': (64, 64, 64, 0), 'b2c1': (32, 64, 128, 1), 'b2c2': (32, 128, 128, 1),
                'b3c1': (16, 128, 256, 2), 'b3c2': (16, 256, 256, 2), 'b4c1': (8, 256, 512, 3),
@@ -108,6 +119,23 @@ FRONTEND_BYTES_PER_CLIP = 160000 * 4 + 1001 * 64 * 4   # waveform
 # 16 kHz), dB + bn0 (~4 per band)
 FRONTEND_FLOPS_PER_FRAME = 5 * 256 * 8 + 10 * 257 + 512 + 3 * 257 + 2 * 514 + 4 * 64
 PEAK_VALU_F32_TF = 78.6    # non-packed f32 VALU (packed FP32 is excluded beside MFMA)
+
+
+# --backend gloo (a rehearsal of the N-rank path on one GPU: every rank on
+# device 0, the gathers through host copies); nccl (= RCCL, the default at
+# N > 1) gathers device tensors over xGMI
+GATHER_CPU = False
+
+
+def gather_outputs(out, world, rank):
+    """The step's only collective: framewise + clipwise of every
+    rank's shard to rank 0.  Returns (framewise, clipwise) on rank 0."""
+    fw, cw = out['framewise_output'], out['clipwise_output']
+    if world == 1:
+        return fw, cw
+    if GATHER_CPU:
+        fw, cw = fw.cpu(), cw.cpu()
+    return distributed.gather_to_rank0(fw, world, rank), distributed.gather_to_rank0(cw, world, rank)
 
 
 def conv_flops(stage, B, T):
@@ -124,6 +152,7 @@ def build_model(name, device, preset=(16000, 512, 160, 64, 25, 7000), feature='l
         sd[k] = torch.from_numpy(v)
     m.load_state_dict(sd)
     m.set_tuning(_lib.TUNE_WINO_BLOCK1, int(WINO_BLOCK1))
+    m.set_tuning(_lib.TUNE_WINO_F43, int(WINO_F43))
     return m.to(device).eval()
 
 
@@ -316,7 +345,7 @@ def measure(step, args, world, dev, model=None, B=32):
     if model is not None:
         model.set_pipelined(False)
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device='cpu' if GATHER_CPU else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     return world * B * args.steps / elapsed, elapsed, stage_ms
@@ -353,9 +382,7 @@ def host_to_host_step(model, host_wave, host_out, dev, world, rank):
         torch.cuda.current_stream(dev).wait_stream(copy)
         d.record_stream(torch.cuda.current_stream(dev))
         with torch.no_grad():
-            fw = model(d)['framewise_output']
-        if world > 1:
-            fw = distributed.gather_to_rank0(fw, world, rank)
+            fw, _ = gather_outputs(model(d), world, rank)
         if rank == 0:
             host_out.copy_(fw, non_blocking=True)
     return step
@@ -417,6 +444,9 @@ PROFILE_SUMMARY = os.path.join(REPO, 'profiles', 'r04n_kernel_summary.json')
 # the same passes over the config-4 leg (bench.py --mode gamma: B = 32 x 10 s
 # @ 32 kHz, T = 994 frames)
 GAMMA_PROFILE_SUMMARY = os.path.join(REPO, 'profiles', 'r04n_config4_kernel_summary.json')
+# the same passes over the window-mode leg (bench.py --mode window: B' = 192
+# windows x 501 frames per call)
+WINDOW_PROFILE_SUMMARY = os.path.join(REPO, 'profiles', 'r05_window_kernel_summary.json')
 GAMMA_KERNELS = ('sedx::gamma_init_kernel', 'sedx::gamma_spec_kernel<2048>', 'sedx::gamma_erb_kernel',
                  'sedx::gamma_quant_kernel')
 
@@ -438,6 +468,8 @@ def conv_kernel_name(stage, precision):
         return 'sedx::conv3x3_x3_kernel<%d, %d, %d, %s>' % (F, bn, epi, 'true' if stage == 'b1c2' else 'false')
     if precision == 'winograd' and stage == 'b1c2' and WINO_BLOCK1 == 2:
         return 'sedx::wino_block1_kernel<2>'
+    if precision == 'winograd' and stage in wino_stages() and WINO_F43 and stage != 'b1c2':
+        return 'sedx::conv3x3_wino43_kernel<%d, %d>' % (F, epi)
     if precision == 'winograd' and stage in wino_stages():
         # 2 tile groups x 64 channels (8 row waves) at the bench shapes
         return 'sedx::conv3x3_wino_kernel<%d, %d, 2, 2>' % (F, epi)
@@ -464,7 +496,8 @@ def roofline(stage_ms, B, precision, T=1001, iso_ms=None, summary=None):
 
     achieved = FLOPs the launch executes on the matrix pipe (direct conv:
     2 B T F Cout 9 Cin, + the fused block-1 conv1 2 B T 64 64 9 for b1c2;
-    Winograd layers: 16/36 of the direct conv's) / its launch time, with the
+    Winograd layers: 16/36 (F(2x2,3x3)) or 36/144 (F(4x4,3x3)) of the direct
+    conv's, without the tile padding of a ragged last tile row) / its launch time, with the
     launch time from HIP events on the launch stream measured live in this
     run ONE BATCH AT A TIME (``iso_ms``: sedx_set_profiling mode 1; the
     rocprofv3 summary of the same single-stream work is committed under
@@ -479,7 +512,7 @@ def roofline(stage_ms, B, precision, T=1001, iso_ms=None, summary=None):
     conv = {s_: stage_ms[s_] for s_ in CONV_STAGES}
     dom = max(conv, key=conv.get)
     wino = precision == 'winograd'
-    mul = {st: (WINO_MUL if wino and st in wino_stages() else 1.0) for st in CONV_STAGES}
+    mul = {st: (wino_mul(st) if wino else 1.0) for st in CONV_STAGES}
     flops = conv_flops(dom, B, T) * mul[dom]
     if dom == 'b1c2' and fused_block1(precision):
         flops += 2.0 * B * T * 64 * 64 * 9      # conv1 (Cin 1 -> 64) computed inside the launch
@@ -498,8 +531,11 @@ def roofline(stage_ms, B, precision, T=1001, iso_ms=None, summary=None):
     direct = flops / mul[dom]
     out = {'bound': 'mfma', 'kernel': '%s (%s)' % (kname, dom),
            'arith': {'exact': 'fp32 MFMA v_mfma_f32_32x32x2_f32 (f32 in, f32 acc)',
-                     'winograd': 'fp32 MFMA v_mfma_f32_32x32x2_f32 (f32 in, f32 acc); Winograd F(2x2,3x3) '
-                                 'layers (%s) counted as executed FLOPs (16/36 of direct)' % ', '.join(wino_stages()),
+                     'winograd': ('fp32 MFMA (f32 in, f32 acc); Winograd layers counted as executed FLOPs: '
+                                  '%s' % ', '.join('%s %s' % (st, 'F(4x4,3x3) 36/144 of direct, v_mfma_f32_16x16x4_f32'
+                                                             if wino_mul(st) == WINO43_MUL else
+                                                             'F(2x2,3x3) 16/36 of direct, v_mfma_f32_32x32x2_f32')
+                                                   for st in wino_stages())),
                      'x3': '3xbf16-split MFMA 32x32x16, f32 acc (peak = bf16 dense 2.5 PF / 3)'}[precision],
            'achieved': round(achieved, 2), 'peak': round(peak, 1), 'unit': 'TFLOP/s',
            'frac': round(achieved / peak, 4),
@@ -544,9 +580,7 @@ def clip_leg(model, wave, args, world, rank, dev, precision, isolated=False):
 
     def step():
         with torch.no_grad():
-            fw = model(wave)['framewise_output']
-            if world > 1:
-                distributed.gather_to_rank0(fw, world, rank)
+            gather_outputs(model(wave), world, rank)
 
     value, elapsed, stage_ms = measure(step, args, world, dev, model, B)
     p50, p99 = latency(step, B, max(5, min(args.steps, 20)), dev)
@@ -627,11 +661,60 @@ def window_leg(model, wave, args, dev, precision):
             inference.predict_windows(model, wave, 5, 1)
 
     value, elapsed, _ = measure(step, args, 1, dev, None, B)
+    p50, p99 = latency(step, B, max(5, min(args.steps, 20)), dev)
+    # the dominant launch of one windowed call: B' = 6 B windows of T = 501
+    # frames (5 s at hop 160) through the model as one batch
+    iso = window_stage_times(model, wave, dev, max(3, min(args.steps, 10)))
+    nwin, Tw = 6 * B, 80000 // 160 + 1
+    summary = WINDOW_PROFILE_SUMMARY if (B == 32 and os.path.exists(WINDOW_PROFILE_SUMMARY)) else None
+    roof = roofline(iso, nwin, precision, T=Tw, iso_ms=iso, summary=summary)
+    roof['workload_per_launch'] = '%d windows x %d frames (5 s windows of %d clips)' % (nwin, Tw, B)
     return {'value': round(value, 2), 'unit': 'clips/s', 'windows_per_clip': 6,
             'windows_per_s': round(6 * value, 1), 'ms_per_step': round(elapsed / args.steps * 1e3, 4),
+            'ms_per_clip_p50': round(p50, 4), 'ms_per_clip_p99': round(p99, 4),
+            'ms_per_clip_p50_note': 'device input, one batch of %d clips (its %d windows) at a time, per clip'
+                                    % (B, nwin),
+            'roofline': roof, 'stage_ms_isolated': iso,
             'dtype': DTYPE[precision],
             'note': '5 s windows, 1 s stride, all windows of the batch in one launch, merged + avg_merge '
                     'on the GPU (predict.py:297-349)'}
+
+
+def config5_leg(model, wave, args, world, rank, dev, precision, isolated=True):
+    """BASELINE config 5 (Cnn_9layers_Transformer_FrameAtt, B per GPU, N GPUs):
+    the N > 1 run's second leg — the same clip-sharded step (every rank its
+    own clips, framewise + clipwise gathered to rank 0 each step) on the
+    Transformer model.  Whole-job clips/s from the max-over-ranks time."""
+    B = wave.shape[0]
+    v, e, st, p50, _, iso = clip_leg(model, wave, args, world, rank, dev, precision, isolated=isolated)
+    out = {'workload': '%s logmel 16k, %d x 10 s clips per GPU per step (clip mode)' % (MODEL_NAMES['transformer'], B),
+           'metric': METRICS['transformer'], 'value': round(v, 2), 'unit': 'clips/s', 'n_gpus': world,
+           'global_batch': B * world, 'batch_per_gpu': B,
+           'backend': dist.get_backend() if world > 1 else None,
+           'ms_per_step': round(e / args.steps * 1e3, 4), 'ms_per_clip_p50_device': round(p50, 4),
+           'scaling': 'weak', 'dtype': DTYPE.get(precision, precision),
+           'gathered': 'framewise_output + clipwise_output to rank 0 every step'}
+    if st is not None:
+        out['roofline'] = roofline(st, B, precision, iso_ms=iso)
+        out['stage_ms'] = st
+    return out
+
+
+def window_stage_times(model, wave, dev, reps):
+    """Per-stage device time of one windowed call (all windows of the batch as
+    one forward, sedx_set_profiling mode 1), averaged over reps."""
+    nat, L = model.native(dev), _lib.lib()
+    _lib.check(L.sedx_set_profiling(nat.h, 1), nat.h, 'set_profiling')
+    acc = np.zeros(len(_lib.STAGES))
+    for _ in range(reps):
+        with torch.no_grad():
+            inference.predict_windows(model, wave, 5, 1)
+        ms = (ctypes.c_float * len(_lib.STAGES))()
+        n = ctypes.c_int32()
+        _lib.check(L.sedx_stage_times(nat.h, ms, len(_lib.STAGES), ctypes.byref(n)), nat.h, 'stage_times')
+        acc += np.array(ms[:])
+    _lib.check(L.sedx_set_profiling(nat.h, 0), nat.h, 'set_profiling')
+    return {s: round(float(v), 4) for s, v in zip(_lib.STAGES, acc / reps)}
 
 
 def events_side(model, wave):
@@ -721,7 +804,8 @@ class StubModel:
 
     def __call__(self, wave):
         x = wave[:, :1000].reshape(wave.shape[0], 1000, 1)
-        return {'framewise_output': torch.sigmoid(x * self.w)}
+        fw = torch.sigmoid(x * self.w)
+        return {'framewise_output': fw, 'clipwise_output': fw.max(dim=1).values}
 
 
 def stub_main(args, world, rank):
@@ -733,6 +817,8 @@ def stub_main(args, world, rank):
     B = args.batch
     wave = torch.from_numpy(synth.make_waveforms(B, 0.1, 16000, seed=1234 + rank))
     value, elapsed, _, p50, _, _ = clip_leg(StubModel(), wave, args, world, rank, dev, args.precision)
+    # the config-5 leg of the N > 1 run (a second model, the same measurement path)
+    c5 = config5_leg(StubModel(), wave, args, world, rank, dev, args.precision, isolated=False)
     env = {k: os.environ.get(k) for k in ('RANK', 'LOCAL_RANK', 'WORLD_SIZE', 'MASTER_ADDR')}
     envs = [None] * world if rank == 0 else None
     if world > 1:
@@ -743,7 +829,7 @@ def stub_main(args, world, rank):
         print(json.dumps({'metric': 'stub', 'value': round(value, 3), 'unit': 'clips/s', 'n_gpus': world,
                           'steps': args.steps, 'warmup': args.warmup,
                           'ms_per_step': round(elapsed / args.steps * 1e3, 4), 'stub': True,
-                          'rank_env': envs}))
+                          'rank_env': envs, 'configs': {'config5': c5}}))
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
@@ -784,6 +870,13 @@ def main():
                     help='CPU stand-in model (tests of the N-rank launcher and the N > 1 measurement path)')
     ap.add_argument('--stub-fail-rank', type=int, default=-1,
                     help='with --stub: this rank exits with status 3 after the process group is up (launcher test)')
+    ap.add_argument('--backend', choices=['nccl', 'gloo'], default=None,
+                    help='N > 1 process-group backend: nccl (= RCCL, the default with GPUs; rank r on GPU r) or '
+                         'gloo (every rank on GPU 0, gathers through host copies: a rehearsal of the N-rank path '
+                         'with the real model on a one-GPU box)')
+    ap.add_argument('--wino-f43', type=int, choices=[0, 1], default=None,
+                    help='SEDX_TUNE_WINO_F43 (A/B runs): blocks 2-4 as Winograd F(4x4,3x3) (1, the default) or '
+                         'F(2x2,3x3) (0)')
     ap.add_argument('--wino-block1', type=int, choices=[0, 1, 2], default=None,
                     help='winograd precision: block 1 as Winograd with conv1 inside the launch (2), fed by a '
                          'separate conv1 launch (1), or as the direct fused kernel (0); default: WINO_BLOCK1')
@@ -793,7 +886,10 @@ def main():
         # a plain `python bench.py --gpus N`: start the N ranks here, before
         # anything in this process touches the GPU
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
-    world, rank, local = distributed.init('gloo' if args.stub else None)
+    global GATHER_CPU
+    backend = 'gloo' if args.stub else args.backend
+    GATHER_CPU = backend == 'gloo'
+    world, rank, local = distributed.init(backend)
     if world != args.gpus:
         if rank == 0:
             print('bench: --gpus %d but WORLD_SIZE %d' % (args.gpus, world), file=sys.stderr)
@@ -801,12 +897,15 @@ def main():
     if args.stub:
         stub_main(args, world, rank)
         return
-    dev = torch.device('cuda', local)
+    # gloo rehearsal: every rank on GPU 0 (each with its own libsedx handle)
+    dev = torch.device('cuda', 0 if GATHER_CPU else local)
     torch.cuda.set_device(dev)
     name = MODEL_NAMES[args.model]
-    global WINO_BLOCK1
+    global WINO_BLOCK1, WINO_F43
     if args.wino_block1 is not None:
         WINO_BLOCK1 = args.wino_block1
+    if args.wino_f43 is not None:
+        WINO_F43 = args.wino_f43
     model = build_model(name, dev)
     model.set_tuning(_lib.TUNE_GRU_KERNEL, GRU_KERNELS[args.gru_kernel])
     if args.wino_order is not None:
@@ -824,8 +923,10 @@ def main():
             print(json.dumps(res))
         return
     if args.mode == 'clip':
+        # per-stage times one batch at a time (the roofline's launch time) on
+        # every rank at N > 1 too (no collective inside; rank 0's are reported)
         value, elapsed, stage_ms, p50_dev, p99_dev, iso_ms = clip_leg(model, wave, args, world, rank, dev,
-                                                                     args.precision, isolated=side)
+                                                                     args.precision, isolated=side or world > 1)
         roof = roofline(stage_ms, B, args.precision, iso_ms=iso_ms)
     else:
         model.set_precision(args.precision)
@@ -835,6 +936,15 @@ def main():
     # p50 from host-visible input (pinned) to the framewise output on the host
     host_wave = wave.cpu().pin_memory()
     host_out = torch.empty((B * world, 1000, 25), dtype=torch.float32).pin_memory() if rank == 0 else None
+    # BASELINE config 5 at N > 1: the Transformer model through the same
+    # sharded step (the driver's `bench.py --gpus N` measures both models)
+    c5 = None
+    if world > 1 and args.mode == 'clip' and args.model == 'gru' and not args.no_side:
+        if rank == 0:
+            progress('config5 (Transformer, %d ranks) leg' % world)
+        trf = build_model(MODEL_NAMES['transformer'], dev)
+        c5 = config5_leg(trf, wave, args, world, rank, dev, args.precision)
+        del trf
     h2h = host_to_host_step(model, host_wave, host_out, dev, world, rank)
     for _ in range(3):
         h2h()
@@ -872,7 +982,8 @@ def main():
         extra['latency_b1'] = latency_b1(model, dev)
         notes = {'x3': 'opt-in arithmetic (operands narrowed to 16 significant bits), same workload',
                  'exact': 'fp32, direct 3x3 conv everywhere (bit-reproducible reference arithmetic), same workload',
-                 'winograd': 'fp32, block 1 conv2 and blocks 2-4 as Winograd F(2x2,3x3), same workload'}
+                 'winograd': 'fp32, block 1 conv2 as Winograd F(2x2,3x3) and blocks 2-4 as F(4x4,3x3), same '
+                             'workload'}
         for other in [p for p in ('exact', 'winograd', 'x3') if p != args.precision]:
             progress('value_%s leg' % other)
             model.set_precision(other)
@@ -926,7 +1037,9 @@ def main():
                                    % (name, B, args.mode),
                        'batch_per_gpu': B, 'global_batch': B * world, 'clip_seconds': 10,
                        'sample_rate': 16000, 'mode': args.mode, 'precision': args.precision,
-                       'parallelism': 'dp%d clip-sharded, RCCL gather of framewise' % world,
+                       'parallelism': 'dp%d clip-sharded, %s gather of framewise + clipwise to rank 0'
+                                      % (world, 'gloo (host copies, all ranks on GPU 0)' if GATHER_CPU else 'RCCL'),
+                       'backend': dist.get_backend() if world > 1 else None,
                        'streams': args.streams,
                        'pipelined': args.streams > 1 and not args.no_pipeline,
                        'gru_kernel': args.gru_kernel if args.model == 'gru' else None},
@@ -941,6 +1054,8 @@ def main():
             'library': os.path.relpath(_lib.LIB_PATH, REPO), 'library_version': _lib.lib().sedx_version().decode(),
         }
         line.update(extra)
+        if c5 is not None:
+            line.setdefault('configs', {})['config5'] = c5
         if cpu:
             line['speedup_vs_cpu'] = round(value / cpu['value'], 1)
         print(json.dumps(line))

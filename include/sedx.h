@@ -74,7 +74,13 @@ typedef struct sedx_handle sedx_handle;
 sedx_status sedx_create(const sedx_config* cfg, int device, sedx_handle** out);
 void sedx_destroy(sedx_handle* h);
 const char* sedx_last_error(const sedx_handle* h);
+/* "sedx <major>.<minor> (abi N)".  SEDX_ABI_VERSION changes whenever an
+ * entry point's signature or a struct layout changes incompatibly; a caller
+ * built against this header checks sedx_abi_version() == SEDX_ABI_VERSION
+ * at load time ("ABI history"). */
+#define SEDX_ABI_VERSION 5
 const char* sedx_version(void);
+int32_t sedx_abi_version(void);
 
 /* One state_dict entry (host fp32; int64 scalars such as num_batches_tracked
  * are skipped by the caller).  Keys/shapes exactly as the reference
@@ -162,7 +168,12 @@ typedef struct {
   int32_t driver;           /* sedx_window_driver */
   int32_t overlap;          /* PREDICT: predict.py --overlap (stride 1 s, else sample_duration s); MAIN_STRONG: ignored */
   int32_t sample_duration;  /* seconds (an int in both drivers: predict.py:701, main_strong.py:746) */
-  int32_t reserved;         /* must be 0 */
+  int32_t vote;             /* 0: the averaged merge (sedx_forward_windows, avg_merge after merge);
+                               1: the vote merge (sedx_forward_windows_vote, merge only).  Picks the
+                               plan sedx_window_geometry / sedx_window_workspace_size size, so they
+                               reject exactly what the matching forward rejects (avg_merge raises on
+                               a zero step, the vote merge does not).  Was `reserved` (0) before
+                               ABI 5: old callers get the averaged path, as before. */
   double overlap_value;     /* merge step int(100 * overlap_value); MAIN_STRONG: also the stride */
   double audio_duration;    /* the loop bound in seconds; <= 0: L_clip / sample_rate */
 } sedx_window_spec;
@@ -223,14 +234,17 @@ sedx_status sedx_forward_windows_vote(sedx_handle* h, const float* d_audio, int6
  *                       arithmetic (pytorch/models.py:614-615, :663-670),
  *                       direct 3x3 convolution.
  *  SEDX_PRECISION_WINOGRAD (default)  fp32 throughout as EXACT, with block 1's conv2
- *                       (SEDX_TUNE_WINO_BLOCK1) and the six conv layers of
- *                       blocks 2-4 computed by Winograd F(2x2,3x3):
- *                       input / weight / output transforms and the 16
+ *                       (SEDX_TUNE_WINO_BLOCK1) computed by Winograd
+ *                       F(2x2,3x3) and the six conv layers of blocks 2-4 by
+ *                       F(4x4,3x3) (SEDX_TUNE_WINO_F43; 0: F(2x2,3x3)):
+ *                       input / weight / output transforms and the
  *                       element-wise GEMMs all in fp32 (weights transformed
- *                       in float64, rounded once), 2.25x fewer multiplies;
- *                       |error| vs a float64 conv equal to or below the
- *                       direct conv's (tools/wino_bench.cpp).  Different
- *                       rounding from EXACT, so not bit-identical to it.
+ *                       in float64, rounded once), 2.25x / 4x fewer
+ *                       multiplies than the direct conv; F(2x2,3x3)'s error
+ *                       vs a float64 conv is at or below the direct conv's,
+ *                       F(4x4,3x3)'s ~6x it (tools/wino_bench.cpp,
+ *                       tools/wino43_bench.cpp).  Different rounding from
+ *                       EXACT, so not bit-identical to it.
  *  SEDX_PRECISION_X3    opt-in: bf16 MFMA with a 3-term hi/lo operand split
  *                       (hi*hi + hi*lo + lo*hi, fp32 accumulate): operands
  *                       carry 16 significant bits, products err ~2^-16 rel.
@@ -303,6 +317,13 @@ sedx_status sedx_set_precision(sedx_handle* h, int32_t mode);
  *                         as 8 tile blocks x 4 channel groups of 64 (4 slabs
  *                         per round through the XCD's L2 instead of 8);
  *                         0: tile block major.  Bit-identical outputs.
+ *  SEDX_TUNE_WINO_F43     (winograd) 1 (default): the six conv layers of
+ *                         blocks 2-4 as fp32 Winograd F(4x4,3x3) (36
+ *                         multiplies per 4x4 tile, v_mfma_f32_16x16x4_f32,
+ *                         csrc/conv_wino43.hip); 0: F(2x2,3x3).  Different
+ *                         rounding (both fp32 throughout; F(4,3)'s error vs a
+ *                         float64 conv is ~6x the direct conv's, still ~1e-5
+ *                         of the 1e-3 bar), so not bit-identical to each other.
  *
  * Co-residency: the cooperative GRU kernels need all workgroups of a
  * (32-clip group, direction) resident at once — 8 CUs (COOP) or 16 (COOP16)
@@ -318,7 +339,8 @@ typedef enum {
   SEDX_TUNE_MEL_MFMA = 3,
   SEDX_TUNE_GRU_SPIN = 4,
   SEDX_TUNE_WINO_ORDER = 5,
-  SEDX_TUNE_GAMMA_SPEC = 6
+  SEDX_TUNE_GAMMA_SPEC = 6,
+  SEDX_TUNE_WINO_F43 = 7
 } sedx_tuning_knob;
 enum {
   SEDX_GRU_KERNEL_COOP = 0,
@@ -353,12 +375,15 @@ sedx_status sedx_set_pipelined(sedx_handle* h, int32_t on);
  * on its stream at the stage boundaries; sedx_stage_times waits for them and
  * returns milliseconds for: 0 frontend, 1 conv1 of block 1, 2..8 the seven
  * implicit-GEMM convs (b1c2, b2c1, b2c2, b3c1, b3c2, b4c1, b4c2), 9 GRU / MHA
- * incl. projections, 10 AttBlock head.  on = 1: the last forward's times;
+ * incl. projections, 10 AttBlock head, 11 pipeline wait: with
+ * sedx_set_pipelined on, the stream's wait for the previous forward's conv
+ * stack (between the frontend and block 1; ~0 otherwise), so stage 0 times
+ * the frontend's own work.  on = 1: the last forward's times;
  * on = 2 (accumulate): every forward records into its own event set (so
  * forwards in flight on several streams time independently) and
  * sedx_stage_times returns per-stage averages over all forwards since the
  * previous call (or since profiling was switched on), then resets them. */
-#define SEDX_N_STAGES 11
+#define SEDX_N_STAGES 12
 /* Stage capture (per-stage parity tests): every later forward copies the
  * output of stage `stage` (numbering as above) into d_buf (at most `bytes`),
  * on its stream, in the library's channels-last layout:

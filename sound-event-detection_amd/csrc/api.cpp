@@ -1,5 +1,6 @@
 // libsedx C ABI (include/sedx.h): handle, state_dict ingestion + packing,
 // forward orchestration, windowed driver.  Host C++; kernels live in *.hip.
+#include <new>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -48,6 +49,7 @@ struct DevWeights {
   float* cb[8] = {};    // folded biases
   void* wx3[8] = {};    // split bf16 hi/lo packs for conv3x3_x3 (same indices)
   float* wu[8] = {};    // Winograd U = G g G^T packs for conv3x3_wino (same indices)
+  float* wu43[8] = {};  // F(4x4,3x3) U packs for conv3x3_wino43 (blocks 2-4: indices 2..7)
   float* w_ih = nullptr;   // [1536][512]
   float* b_ih = nullptr;   // [1536]
   float* whhT = nullptr;   // [2][256][768]
@@ -94,6 +96,7 @@ struct sedx_handle {
   int mel_mfma = 0;                        // SEDX_TUNE_MEL_MFMA (measured slower: opt-in)
   unsigned gru_spin = 1u << 24;            // SEDX_TUNE_GRU_SPIN: bound of every GRU hand-off spin (polls)
   int wino_order = 1;                      // SEDX_TUNE_WINO_ORDER (4 x 8 rounds on the 512-channel layers)
+  int wino_f43 = 1;                        // SEDX_TUNE_WINO_F43 (blocks 2-4 as Winograd F(4x4,3x3))
   int gamma_spec = 0;                      // SEDX_TUNE_GAMMA_SPEC
   // sedx_set_capture: copy one stage's output of every later forward
   int cap_stage = -1;
@@ -112,6 +115,9 @@ struct sedx_handle {
   // forward / sedx_stage_times turns it into SEDX_EHIP
   unsigned* gru_err_host = nullptr;
   unsigned* gru_err_dev = nullptr;
+  // events 0..10 bound stages 0..10 (stage i = [i, i + 1]) except stage 0 =
+  // [0, 12] (frontend) and stage 11 = [12, 1] (pipeline wait): event 12 is
+  // recorded after the frontend, before the cross-stream wait
   hipEvent_t ev[SEDX_N_STAGES + 1] = {};
   bool ev_recorded[SEDX_N_STAGES + 1] = {};
   // profiling mode 2 (accumulate): every forward takes its own event set from
@@ -131,13 +137,19 @@ struct sedx_handle {
 
 namespace {
 // mode 2: sums the elapsed times of every used event set, frees the pool
+// the events bounding stage i (see sedx_handle::ev)
+inline int stage_begin(int i) { return i == 11 ? 12 : i; }
+inline int stage_end(int i) { return i == 0 ? 12 : i == 11 ? 1 : i + 1; }
+static_assert(SEDX_N_STAGES == 12, "stage event map");
+
 void fold_ev_pool(sedx_handle* h) {
   for (size_t k = 0; k < h->ev_used; ++k) {
     auto& e = h->ev_pool[k];
     for (int i = 0; i < SEDX_N_STAGES; ++i) {
-      if (!e.rec[i] || !e.rec[i + 1]) continue;
+      const int a = stage_begin(i), b = stage_end(i);
+      if (!e.rec[a] || !e.rec[b]) continue;
       float v = 0.f;
-      if (hipEventSynchronize(e.ev[i + 1]) == hipSuccess && hipEventElapsedTime(&v, e.ev[i], e.ev[i + 1]) == hipSuccess) {
+      if (hipEventSynchronize(e.ev[b]) == hipSuccess && hipEventElapsedTime(&v, e.ev[a], e.ev[b]) == hipSuccess) {
         h->acc_ms[i] += v;
         ++h->acc_n[i];
       }
@@ -198,6 +210,15 @@ void capture(sedx_handle* h, int stage, const float* src, size_t n, hipStream_t 
   const size_t bytes = std::min(n * sizeof(float), h->cap_bytes);
   if (hipMemcpyAsync(h->cap_buf, src, bytes, hipMemcpyDeviceToDevice, s) != hipSuccess)
     note_launch_error(hipErrorInvalidValue);
+}
+// a stage held in the chunk-of-4 layout [B][C/4][T][F][4] (the F(4x4,3x3)
+// layers): captured in the documented channels-last layout (a buffer short
+// of the whole stage gets the raw prefix)
+void capture_c4(sedx_handle* h, int stage, const float* src, int64_t B, int T, int F, int C, hipStream_t s) {
+  if (h->cap_stage != stage || !h->cap_buf) return;
+  const size_t n = (size_t)B * T * F * C;
+  if (h->cap_bytes < n * sizeof(float)) return capture(h, stage, src, n, s);
+  launch_c4_to_nhwc(src, (int)B, T, F, C, h->cap_buf, s);
 }
 
 // errors of the launches just issued: preparation failures noted by
@@ -362,6 +383,7 @@ sedx_status run_body(sedx_handle* h, int64_t B, const Geometry& g, float* ws, co
   const int iB = (int)B;
   // the cross-stream wait for the previous forward's conv stack comes before
   // the b1c1 stage event, so stage 1 times only this forward's work
+  mark(h, 12, s);   // the frontend's end: the wait below is stage 11, not the frontend's
   if (h->pipelined && h->conv_done_recorded) HIP_TRY(h, hipStreamWaitEvent(s, h->conv_done, 0));
   mark(h, 1, s);
   capture(h, 0, X0, (size_t)B * g.T * 64, s);
@@ -371,6 +393,9 @@ sedx_status run_body(sedx_handle* h, int64_t B, const Geometry& g, float* ws, co
   // staging (the b1c1 stage is just the zero-bordered copy of the bn0 output)
   if (x3) HIP_TRY(h, hipMemsetAsync(sched, 0, 7 * CONV_SCHED_INTS * sizeof(int), s));
   const bool wb1 = wino_block1_on(h);
+  // winograd with F(4x4,3x3): block 1 (one launch) and blocks 2-4 keep their
+  // activations in the chunk-of-4 layout [B][C/4][T][F][4] (dense halo DMA)
+  const bool c4 = h->precision == SEDX_PRECISION_WINOGRAD && h->wino_f43 && wb1 && h->wino_block1 == 2;
   // Winograd block 1: 1 = conv1's activation [B][T][64][64] into A by its
   // own launch; 2 = conv1 inside the Winograd launch (reads X0 itself)
   if (wb1 && h->wino_block1 == 1)
@@ -396,7 +421,7 @@ sedx_status run_body(sedx_handle* h, int64_t B, const Geometry& g, float* ws, co
       launch_block1_fused_x3(nullptr, iB, c.T, A, w.c1_wt, w.c1_b, w.wx3[c.idx], w.cb[c.idx], c.out,
                              sched, s);
     else if (i == 0 && wb1 && h->wino_block1 == 2)
-      launch_block1_wino(X0, iB, c.T, w.c1_w, w.c1_b, w.wu[c.idx], w.cb[c.idx], c.out, w.zero, w.trash, s);
+      launch_block1_wino(X0, iB, c.T, w.c1_w, w.c1_b, w.wu[c.idx], w.cb[c.idx], c.out, w.zero, w.trash, s, c4);
     else if (i == 0 && wb1)
       launch_conv3x3_wino(A, iB, c.T, 64, 64, 64, w.wu[c.idx], w.cb[c.idx], c.out, EPI_POOL2, w.zero, w.trash, s);
     else if (i == 0)
@@ -404,6 +429,9 @@ sedx_status run_body(sedx_handle* h, int64_t B, const Geometry& g, float* ws, co
     else if (x3)
       launch_conv3x3_x3(c.in, iB, c.T, c.F, c.cin, c.cout, w.wx3[c.idx], w.cb[c.idx], c.out, c.epi,
                         sched + i * CONV_SCHED_INTS, s);
+    else if (h->precision == SEDX_PRECISION_WINOGRAD && h->wino_f43)
+      launch_conv3x3_wino43(c.in, iB, c.T, c.F, c.cin, c.cout, w.wu43[c.idx], w.cb[c.idx], c.out, c.epi, w.trash, s,
+                            h->wino_order, c4);
     else if (h->precision == SEDX_PRECISION_WINOGRAD)
       launch_conv3x3_wino(c.in, iB, c.T, c.F, c.cin, c.cout, w.wu[c.idx], w.cb[c.idx], c.out, c.epi, w.zero, w.trash,
                           s, h->wino_order);
@@ -411,7 +439,12 @@ sedx_status run_body(sedx_handle* h, int64_t B, const Geometry& g, float* ws, co
       launch_conv3x3(c.in, iB, c.T, c.F, c.cin, c.cout, w.wp[c.idx], w.cb[c.idx], c.out, c.epi, w.zero, s);
     const size_t px = c.epi == EPI_STORE ? (size_t)c.T * c.F : c.epi == EPI_POOL2 ? (size_t)(c.T / 2) * (c.F / 2)
                                                                                    : (size_t)c.T;
-    capture(h, 2 + i, c.out, (size_t)B * px * c.cout, s);
+    if (c4 && c.epi != EPI_FMEAN) {
+      const int To = c.epi == EPI_POOL2 ? c.T / 2 : c.T, Fo = c.epi == EPI_POOL2 ? c.F / 2 : c.F;
+      capture_c4(h, 2 + i, c.out, B, To, Fo, c.cout, s);
+    } else {
+      capture(h, 2 + i, c.out, (size_t)B * px * c.cout, s);
+    }
   }
   mark(h, 9, s);
   if (h->pipelined) {
@@ -587,8 +620,11 @@ T* carve(char*& p, size_t n) {
 extern "C" {
 
 const char* sedx_version(void) {
-  return "sedx 0.3 (gfx950: fp32 MFMA exact direct conv | fp32 Winograd F(2x2,3x3) | 3xbf16-split MFMA)";
+  return "sedx 0.5 (abi 5; gfx950: fp32 MFMA exact direct conv | fp32 Winograd F(4x4,3x3) + F(2x2,3x3) | "
+         "3xbf16-split MFMA)";
 }
+
+int32_t sedx_abi_version(void) { return SEDX_ABI_VERSION; }
 
 sedx_status sedx_set_precision(sedx_handle* h, int32_t mode) {
   if (!h) return SEDX_EINVAL;
@@ -648,6 +684,10 @@ sedx_status sedx_set_tuning(sedx_handle* h, int32_t knob, int32_t value) {
     case SEDX_TUNE_GAMMA_SPEC:
       if (value != 0 && value != 1) break;
       h->gamma_spec = value;
+      return SEDX_OK;
+    case SEDX_TUNE_WINO_F43:
+      if (value != 0 && value != 1) break;
+      h->wino_f43 = value;
       return SEDX_OK;
     default:
       return fail(h, SEDX_EINVAL, "unknown tuning knob %d", (int)knob);
@@ -831,7 +871,7 @@ sedx_status sedx_finalize_weights(sedx_handle* h) {
   const int ch[5] = {1, 64, 128, 256, 512};
   std::vector<float> packed[8], cbias[8], c1w(64 * 9), c1b(64);
   std::vector<uint16_t> packed_x3[8];
-  std::vector<float> packed_wu[8];
+  std::vector<float> packed_wu[8], packed_wu43[8];
   for (int k = 1; k <= 4; ++k)
     for (int j = 1; j <= 2; ++j) {
       const std::string p = "conv_block" + std::to_string(k);
@@ -866,6 +906,10 @@ sedx_status sedx_finalize_weights(sedx_handle* h) {
           for (size_t k = 0; k < (size_t)cin * 9; ++k) wf[(size_t)o * cin * 9 + k] = wt[(size_t)o * cin * 9 + k] * sc[o];
         packed_wu[idx].assign((size_t)cin * cout * 16, 0.f);
         pack_conv_wino(wf.data(), cin, cout, packed_wu[idx].data());
+        if (k >= 2) {   // blocks 2-4: F(4x4,3x3) pack as well
+          packed_wu43[idx].assign((size_t)cin * cout * 36, 0.f);
+          pack_conv_wino43(wf.data(), cin, cout, packed_wu43[idx].data());
+        }
       }
       // 3xbf16 split pack: [Cout/BN][Cin/16][9][BN][4 slots x 8 bf16], slot c at c ^ ((n>>2)&3)
       {
@@ -1028,6 +1072,7 @@ sedx_status sedx_finalize_weights(sedx_handle* h) {
     add((void**)&W.cb[i], cbias[i].data(), cbias[i].size() * 4);
     add((void**)&W.wx3[i], packed_x3[i].data(), packed_x3[i].size() * 2);
     add((void**)&W.wu[i], packed_wu[i].data(), packed_wu[i].size() * 4);
+    if (!packed_wu43[i].empty()) add((void**)&W.wu43[i], packed_wu43[i].data(), packed_wu43[i].size() * 4);
   }
   if (is_gru(h)) {
     add((void**)&W.w_ih, w_ih.data(), w_ih.size() * 4);
@@ -1139,9 +1184,10 @@ sedx_status sedx_stage_times(sedx_handle* h, float* ms, int32_t capacity, int32_
   }
   for (int i = 0; i < SEDX_N_STAGES && i < capacity; ++i) {
     float v = 0.f;
-    if (h->ev_recorded[i] && h->ev_recorded[i + 1]) {
-      HIP_TRY(h, hipEventSynchronize(h->ev[i + 1]));
-      HIP_TRY(h, hipEventElapsedTime(&v, h->ev[i], h->ev[i + 1]));
+    const int a = stage_begin(i), b = stage_end(i);
+    if (h->ev_recorded[a] && h->ev_recorded[b]) {
+      HIP_TRY(h, hipEventSynchronize(h->ev[b]));
+      HIP_TRY(h, hipEventElapsedTime(&v, h->ev[a], h->ev[b]));
     }
     ms[i] = v;
   }
@@ -1311,16 +1357,30 @@ sedx_status sedx_gamma_workspace_size(const sedx_handle* h, int64_t B, int64_t L
   return SEDX_OK;
 }
 
+// host-side failures of the window entry points (plan vectors) become
+// status codes instead of exceptions crossing the C ABI
+#define SEDX_HOST_TRY(h, body)                                                              \
+  try {                                                                                     \
+    body                                                                                    \
+  } catch (const std::bad_alloc&) {                                                         \
+    return fail(const_cast<sedx_handle*>(h), SEDX_ENOMEM, "host allocation failed (merge plan)"); \
+  } catch (...) {                                                                           \
+    return fail(const_cast<sedx_handle*>(h), SEDX_EINVAL, "host-side failure building the window plan"); \
+  }
+
 sedx_status sedx_window_geometry(const sedx_handle* h, int64_t L_clip, const sedx_window_spec* spec,
                                  int64_t* n_windows, int64_t* window_samples, int64_t* merged_frames) {
   if (!h) return SEDX_EINVAL;
-  WinGeom wg;
-  sedx_status st = window_geometry(h, L_clip, spec, false, &wg);
-  if (st != SEDX_OK) return st;
-  if (n_windows) *n_windows = wg.n_win;
-  if (window_samples) *window_samples = wg.full_len;
-  if (merged_frames) *merged_frames = wg.plan.N;
-  return SEDX_OK;
+  SEDX_HOST_TRY(h, {
+    WinGeom wg;
+    // the plan of the forward the spec names: avg_merge rejects a zero step
+    sedx_status st = window_geometry(h, L_clip, spec, spec && spec->vote == 0, &wg);
+    if (st != SEDX_OK) return st;
+    if (n_windows) *n_windows = wg.n_win;
+    if (window_samples) *window_samples = wg.full_len;
+    if (merged_frames) *merged_frames = wg.plan.N;
+    return SEDX_OK;
+  })
 }
 
 // every window of every clip through the model (one batch per window group),
@@ -1334,6 +1394,8 @@ static sedx_status forward_windows_impl(sedx_handle* h, const float* d_audio, in
   if (h->cfg.feature_type != SEDX_FEATURE_LOGMEL)
     return fail(h, SEDX_EINVAL, "windowed inference needs a logmel model");
   if (!d_audio || !d_merged || n_clips <= 0) return fail(h, SEDX_EINVAL, "null pointer or empty batch");
+  if (spec && spec->vote != 0 && h_vote_thres == nullptr)
+    return fail(h, SEDX_EINVAL, "spec.vote = 1: call sedx_forward_windows_vote");
   WinGeom wg;
   sedx_status st = window_geometry(h, L_clip, spec, h_vote_thres == nullptr, &wg);
   if (st != SEDX_OK) return st;
@@ -1429,27 +1491,36 @@ static sedx_status forward_windows_impl(sedx_handle* h, const float* d_audio, in
 sedx_status sedx_window_workspace_size(const sedx_handle* h, int64_t n_clips, int64_t L_clip,
                                        const sedx_window_spec* spec, size_t* bytes) {
   if (!h || !bytes || n_clips <= 0) return SEDX_EINVAL;
-  WinGeom wg;
-  sedx_status st = window_geometry(h, L_clip, spec, false, &wg);
-  if (st != SEDX_OK) return st;
-  *bytes = win_layout(h, n_clips, wg).total_bytes;
-  return SEDX_OK;
+  SEDX_HOST_TRY(h, {
+    WinGeom wg;
+    sedx_status st = window_geometry(h, L_clip, spec, spec && spec->vote == 0, &wg);
+    if (st != SEDX_OK) return st;
+    *bytes = win_layout(h, n_clips, wg).total_bytes;
+    return SEDX_OK;
+  })
 }
 
 sedx_status sedx_forward_windows(sedx_handle* h, const float* d_audio, int64_t n_clips, int64_t L_clip,
                                  const sedx_window_spec* spec, float* d_merged, void* d_workspace,
                                  size_t workspace_bytes, void* stream) {
-  return forward_windows_impl(h, d_audio, n_clips, L_clip, spec, nullptr, d_merged, d_workspace, workspace_bytes,
-                              stream);
+  if (!h) return SEDX_EINVAL;
+  SEDX_HOST_TRY(h, {
+    return forward_windows_impl(h, d_audio, n_clips, L_clip, spec, nullptr, d_merged, d_workspace, workspace_bytes,
+                                stream);
+  })
 }
 
 sedx_status sedx_forward_windows_vote(sedx_handle* h, const float* d_audio, int64_t n_clips, int64_t L_clip,
                                       const sedx_window_spec* spec, const double* bin_thres, float* d_votes,
                                       void* d_workspace, size_t workspace_bytes, void* stream) {
+  if (!h) return SEDX_EINVAL;
   if (!bin_thres) return fail(h, SEDX_EINVAL, "vote mode needs the per-class binarisation thresholds");
-  return forward_windows_impl(h, d_audio, n_clips, L_clip, spec, bin_thres, d_votes, d_workspace, workspace_bytes,
-                              stream);
+  SEDX_HOST_TRY(h, {
+    return forward_windows_impl(h, d_audio, n_clips, L_clip, spec, bin_thres, d_votes, d_workspace, workspace_bytes,
+                                stream);
+  })
 }
+#undef SEDX_HOST_TRY
 
 sedx_status sedx_events_workspace_size(int64_t n_clips, int64_t T, int64_t C, size_t* bytes) {
   if (!bytes || n_clips < 0 || T < 0 || C <= 0) return SEDX_EINVAL;

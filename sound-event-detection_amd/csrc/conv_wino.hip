@@ -188,7 +188,9 @@ __device__ __forceinline__ void wino_bt4(float* x) {
 
 // the kernel body for V row ROW (wave-uniform; a template parameter so the
 // transform, the U rows and the patch offsets are static per wave)
-template <int F, int EPI, int TG, int NT, int ROW, bool C1>
+// C4O (block 1 only): the pooled output in the chunk-of-4 layout
+// [B][Cout/4][T/2][F/2][4] that the F(4x4,3x3) layers read (conv_wino43.hip)
+template <int F, int EPI, int TG, int NT, int ROW, bool C1, bool C4O = false>
 __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, int T, int Cin, int Cout,
                                           const float* __restrict__ U, const float* __restrict__ bias,
                                           float* __restrict__ out, const float* __restrict__ zero16,
@@ -784,7 +786,12 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
             const int To = T / 2;
             const int to = tr0 + trl;
             const float pv = (((y[0][0] + y[0][1]) + y[1][0]) + y[1][1]) * 0.25f;
-            float* dst = to < To ? ob + (trl * (F / 2) + tf) * Cout + n : tr_lane;
+            float* dst;
+            if constexpr (C4O)
+              dst = to < To ? out + ((((int64_t)b * (Cout / 4) + (n >> 2)) * To + to) * (F / 2) + tf) * 4 + (n & 3)
+                            : tr_lane;
+            else
+              dst = to < To ? ob + (trl * (F / 2) + tf) * Cout + n : tr_lane;
             *dst = pv;
           } else {
 #pragma unroll
@@ -819,11 +826,13 @@ __device__ __forceinline__ void wino_body(const float* __restrict__ in, int B, i
 
 // the V row of a wave (wave-uniform): one body instantiation per row
 #define SEDX_WINO_ROWS(F_, EPI_, TG_, NT_, C1_, ...)                                    \
+  SEDX_WINO_ROWS4(F_, EPI_, TG_, NT_, C1_, false, __VA_ARGS__)
+#define SEDX_WINO_ROWS4(F_, EPI_, TG_, NT_, C1_, C4O_, ...)                             \
   switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) / TG_) {                    \
-    case 0: wino_body<F_, EPI_, TG_, NT_, 0, C1_>(__VA_ARGS__); break;                 \
-    case 1: wino_body<F_, EPI_, TG_, NT_, 1, C1_>(__VA_ARGS__); break;                 \
-    case 2: wino_body<F_, EPI_, TG_, NT_, 2, C1_>(__VA_ARGS__); break;                 \
-    default: wino_body<F_, EPI_, TG_, NT_, 3, C1_>(__VA_ARGS__); break;                \
+    case 0: wino_body<F_, EPI_, TG_, NT_, 0, C1_, C4O_>(__VA_ARGS__); break;           \
+    case 1: wino_body<F_, EPI_, TG_, NT_, 1, C1_, C4O_>(__VA_ARGS__); break;           \
+    case 2: wino_body<F_, EPI_, TG_, NT_, 2, C1_, C4O_>(__VA_ARGS__); break;           \
+    default: wino_body<F_, EPI_, TG_, NT_, 3, C1_, C4O_>(__VA_ARGS__); break;          \
   }
 
 template <int F, int EPI, int TG, int NT>
@@ -838,14 +847,16 @@ __global__ __launch_bounds__(256 * TG, (WinoGeom<F, TG, NT>::WG_PER_CU)) void co
 // Block 1 in one launch: conv1 (computed into the halo images) + Winograd
 // conv2 + 2x2 pool, TG tile groups x 64 channels per workgroup (the conv1
 // halo serves all 64 output channels)
-template <int TG>
+template <int TG, bool C4O = false>
 __global__ __launch_bounds__(256 * TG, (WinoGeom<64, TG, 2, true>::WG_PER_CU)) void wino_block1_kernel(
     const float* __restrict__ x0, int B, int T, const float* __restrict__ U, const float* __restrict__ bias,
     float* __restrict__ out, const float* __restrict__ zero16, float* __restrict__ trash, int tb_per_clip,
     const float* __restrict__ w1, const float* __restrict__ b1) {
-  SEDX_WINO_ROWS(64, EPI_POOL2, TG, 2, true, x0, B, T, 64, 64, U, bias, out, zero16, trash, tb_per_clip, 1, w1, b1, 0)
+  SEDX_WINO_ROWS4(64, EPI_POOL2, TG, 2, true, C4O, x0, B, T, 64, 64, U, bias, out, zero16, trash, tb_per_clip, 1, w1,
+                  b1, 0)
 }
 #undef SEDX_WINO_ROWS
+#undef SEDX_WINO_ROWS4
 
 static int wino_device_cus() {
   int dev = 0, ncu = 256;
@@ -983,7 +994,8 @@ void launch_conv3x3_wino(const float* in, int B, int T, int F, int Cin, int Cout
 
 template <int TG>
 static void launch_block1_w(const float* x0, int B, int T, const float* U, const float* bias, float* out,
-                            const float* w1, const float* b1, const float* zero16, float* trash, hipStream_t s) {
+                            const float* w1, const float* b1, const float* zero16, float* trash, bool c4,
+                            hipStream_t s) {
   using G = WinoGeom<64, TG, 2, true>;
   const int tb_per_clip = (T / 2 + G::TRW - 1) / G::TRW;   // pooled: an odd last t-row is dropped
   const int64_t tblocks = (int64_t)B * tb_per_clip;
@@ -992,14 +1004,14 @@ static void launch_block1_w(const float* x0, int B, int T, const float* U, const
   const int64_t resident = (int64_t)wino_device_cus() * G::WG_PER_CU / 8 * 8;
   const int64_t per = (nitems + WINO_ITEMS_B1 - 1) / WINO_ITEMS_B1;
   const int64_t nwg = std::min<int64_t>(nitems, std::max<int64_t>(std::max<int64_t>(8, resident), (per + 7) / 8 * 8));
-  auto* k_ = wino_block1_kernel<TG>;
+  auto* k_ = c4 ? wino_block1_kernel<TG, true> : wino_block1_kernel<TG, false>;
   if (!launch_info(reinterpret_cast<const void*>(k_), G::THREADS, G::LDS_BYTES).ok) return;
   hipLaunchKernelGGL(k_, dim3((unsigned)nwg), dim3(G::THREADS), G::LDS_BYTES, s, x0, B, T, U, bias, out, zero16, trash,
                      tb_per_clip, w1, b1);
 }
 
 void launch_block1_wino(const float* x0, int B, int T, const float* w1, const float* b1, const float* U,
-                        const float* bias, float* out, const float* zero16, float* trash, hipStream_t s) {
+                        const float* bias, float* out, const float* zero16, float* trash, hipStream_t s, bool c4) {
   if (B <= 0 || T < 2) return note_launch_error(hipErrorInvalidValue);
   // 32-bit X0 offsets: batches past 2^31 floats run as several launches over
   // whole clips (same per-clip work)
@@ -1010,7 +1022,7 @@ void launch_block1_wino(const float* x0, int B, int T, const float* w1, const fl
     // 2 tile groups x 64 channels (64 tiles, 8 waves) at every batch size
     // (with 1 tile group the 4 waves would not cover the halo's conv1 pixel
     // groups)
-    launch_block1_w<2>(x0 + b0 * in_clip, bs, T, U, bias, out + b0 * out_clip, w1, b1, zero16, trash, s);
+    launch_block1_w<2>(x0 + b0 * in_clip, bs, T, U, bias, out + b0 * out_clip, w1, b1, zero16, trash, c4, s);
   }
 }
 

@@ -1,0 +1,807 @@
+// 3x3 conv of the 9-layer CNN (ConvBlock, pytorch/models.py:98-141; blocks
+// 2-4, models.py:663-666) as fp32 Winograd F(4x4, 3x3) on
+// v_mfma_f32_16x16x4_f32: every operand, product and sum is fp32, 36
+// multiplies per 4x4 output tile instead of F(2x2,3x3)'s 64 (conv_wino.hip)
+// and the direct conv's 144 (conv.hip).
+//
+// Per output tile (4 t x 4 f) and input channel c the 6x6 input patch d (rows
+// t-1..t+4, cols f-1..f+4, zero outside the clip) becomes V = B^T d B, the
+// BN-folded 3x3 weights g become U = G g G^T (host, float64, rounded once to
+// fp32), the 36 positions p = 6 i + j are 36 independent GEMMs
+// M_p[n][tile] = sum_c U_p[n][c] V_p[c][tile], and the output is
+// Y = A^T M A, then + bias, ReLU and the block's epilogue (store / 2x2 avg pool
+// / freq mean).  Interpolation points 0, 1, -1, 2, -2 (Lavin & Gray 2016):
+//   B^T = [4 0 -5 0 1 0; 0 -4 -4 1 1 0; 0 4 -4 -1 1 0; 0 -2 -1 2 1 0;
+//          0 2 -1 -2 1 0; 0 4 0 -5 0 1]
+//   G   = [1/4 0 0; -1/6 -1/6 -1/6; -1/6 1/6 -1/6; 1/24 1/12 1/6;
+//          1/24 -1/12 1/6; 0 0 1]
+//   A^T = [1 1 1 1 1 0; 0 1 -1 2 -2 0; 0 1 1 4 4 0; 0 1 -1 8 -8 1]
+// (fp32 error study: tools/wino_f43/err.py -> profiles/r04_wino_f43_error.txt.)
+//
+// Work: an item = 32 tiles (two tile groups of 16) x 64 output channels.
+// The workgroup is 12 waves (3 per SIMD): wave w = 2 ROW + tg owns V row ROW
+// (positions 6 ROW .. 6 ROW + 5) of tile group tg for all 64 channels — 6
+// positions x 4 channel tiles of v_mfma_f32_16x16x4_f32 (M = 16 output
+// channels, N = 16 tiles, K = the 4 input channels of a chunk), 96
+// accumulator registers.  Lane l supplies B[k = l >> 4][n = l & 15]: the
+// transformed value of tile n, input channel k — computed in-lane from the
+// patch rows its V row needs (3 or 4 rows of 6 pixels, 3 ds_read_b64 per
+// row), so one V value feeds the 4 channel tiles' MFMAs; U fragments
+// (A[m][k] = U_p[16 nt + m][k], one ds_read_b128 gives a lane its 4 channel
+// tiles) are read from LDS just before their MFMAs.
+//
+// Staging (per 4-channel chunk): the U slab (36 x 4 x 64 floats, 36 KiB,
+// [p][k][m][nt] so a lane's fragment read is 16 B at 16 l) by 36
+// buffer_load_dwordx4 ... lds, and the halo of the 32 tiles as four channel
+// planes ([k][row][RS]: one patch row of a lane is 6 consecutive floats) by
+// buffer_load_dword ... lds — the DMA's lane -> pixel gather does the NHWC ->
+// planar transpose, and the buffer range check writes the zeros of pixels
+// outside the clip (the lane's offset is set out of range).  The row stride RS
+// makes a lane's ds_read_b64 of its patch conflict-free: the 16 tiles of a
+// tile group hit 16 distinct even bank pairs and the odd plane stride puts
+// channels k and k + 1 on the odd ones.  Two rings of 3: the U slab of chunk c
+// is read during step c and the halo of chunk c + 1 (for V of the next chunk)
+// during step c, so at the top of step c the workgroup issues U(c + 2) and
+// halo(c + 3) into the slots freed by step c - 1 — two steps of DMA lead for
+// both — behind one counted-vmcnt barrier.
+//
+// Output transform: per register (channel, tile) a wave holds row ROW of M, so
+// z = (M A)_ROW is in-lane; Y = A^T M A sums the six rows' z across waves
+// through LDS (the U slot freed by the item's last step), two registers per
+// round; waves 0-3 finish (a 2x2 output block each, or one output row for the
+// freq mean) and store 16-byte groups of 4 channels.
+//
+// Persistent workgroups walk items g, g + grid, ... (grid a multiple of 8:
+// every item of a workgroup on its XCD, the XCD-aware decode of
+// conv_wino.hip); the last steps of an item DMA the next item's first chunks.
+// Every item performs the same operations in the same order for each (tile,
+// channel): outputs do not depend on the batch size or the grid.
+#include <type_traits>
+
+#include "sedx_internal.h"
+
+namespace sedx {
+
+typedef float w43_f32x4 __attribute__((ext_vector_type(4)));
+
+// Ablation builds (tools/wino43_bench.cpp only, results WRONG, timing only):
+// SEDX_W43_ABL bit 1 drops the halo DMAs, 2 the U DMAs, 4 the epilogue's
+// exchange and output transform (stores kept)
+#ifndef SEDX_W43_ABL
+#define SEDX_W43_ABL 0
+#endif
+
+template <int F>
+struct W43Geom {
+  static constexpr int WAVES = 12, THREADS = 64 * WAVES;
+  static constexpr int NT = 4, NCH = 64;             // channel tiles / output channels per item
+  static constexpr int TILES = 32;                   // two tile groups of 16
+  static constexpr int FT = F / 4;                   // tiles per tile row
+  static constexpr int TRW = TILES / FT;             // tile rows per item
+  // a tile group is TRG tile rows x TFG tile columns (lane n = tr TFG + tf)
+  static constexpr int TFG = F == 8 ? 2 : 4;
+  static constexpr int TRG = 16 / TFG;
+  static constexpr int RT = 4 * TRW + 2, CS = F + 2; // halo rows / columns
+  // halo row stride: (4 tr RS + 4 tf) / 2 over the 16 tiles of a group must
+  // take the 16 even values mod 32 (b64 bank pairs): 2 RS = 8 (mod 32) for
+  // 4 x 4 groups, 2 RS = 20 (mod 32) for 8 x 2
+  static constexpr int RS = F == 32 ? 36 : F == 16 ? 20 : 10;
+  static constexpr int HB = WAVES;                   // 64-dword DMA blocks per plane (one per wave)
+  static constexpr int PS = 64 * HB + 2;             // plane stride, = 2 mod 4 (odd bank pairs for odd k)
+  static constexpr int HALO = 4 * PS;                // dwords per halo slot
+  static constexpr int USZ = 36 * 4 * NCH;           // dwords per U slot ([p][k][m][nt])
+  static constexpr int NB = 3;                       // ring depth (U and halo)
+  static constexpr int U_OFF = 0, H_OFF = NB * USZ, BIAS_OFF = H_OFF + NB * HALO, BIAS_MAX = 512;
+  static constexpr int LDS_BYTES = 4 * (BIAS_OFF + BIAS_MAX);
+  static constexpr int VM = 7;                       // DMAs per wave per step (3 U units + 4 halo planes)
+  // epilogue exchange per round, in the free U slot: [tg][row 6][reg 2][b pair 2][lane 64][2]
+  static constexpr int XROUND = 2 * 6 * 2 * 2 * 128;
+  static_assert(F == 32 || F == 16 || F == 8, "F");
+  static_assert(RT * RS <= 64 * HB, "halo plane fits its DMA blocks");
+  static_assert(36 % WAVES == 0, "U units per wave");
+  static_assert(XROUND <= USZ, "exchange fits one U slot");
+  static_assert(LDS_BYTES <= 160 * 1024, "LDS per workgroup");
+  static_assert(FT * TRW == TILES && TFG * TRG == 16, "tile groups");
+};
+
+// raw workgroup barrier behind "this wave's DMAs and stores older than its N
+// youngest VMEM ops landed, its LDS operations done" (__syncthreads() would
+// drain every DMA in flight)
+template <int N>
+__device__ __forceinline__ void w43_bar() {
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ void w43_lds_bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// LDS-DMA through a buffer resource (M0 = LDS byte address of lane 0; out of
+// range offsets write zeros).  m0 and soff wave-uniform.
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ __forceinline__ void w43_dma16(uint32_t voff, __amdgpu_buffer_rsrc_t r, uint32_t soff, uint32_t m0) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, %3 offen lds" ::"v"(voff), "s"(r), "s"(m0),
+               "s"(soff)
+               : "memory", "m0");
+}
+// (no instruction offset: an LDS-DMA's inst_offset moves the LDS destination
+// as well as the source — measured, tools/oob_lds_probe.cpp — so the channel
+// step goes into soffset)
+__device__ __forceinline__ void w43_dma4(uint32_t voff, __amdgpu_buffer_rsrc_t r, uint32_t soff, uint32_t m0) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dword %0, %1, %3 offen lds" ::"v"(voff), "s"(r),
+               "s"(m0), "s"(soff)
+               : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
+__device__ __forceinline__ uint32_t w43_lds_addr(const float* p) {
+  return (uint32_t)(size_t)(const __attribute__((address_space(3))) float*)p;
+}
+
+// v = e B (the 6-point transform of one V row)
+__device__ __forceinline__ void w43_colt(const float (&e)[6], float (&v)[6]) {
+  v[0] = fmaf(4.0f, e[0], fmaf(-5.0f, e[2], e[4]));
+  const float a = fmaf(-4.0f, e[2], e[4]), b = fmaf(-4.0f, e[1], e[3]);
+  v[1] = a + b;
+  v[2] = a - b;
+  const float c = e[4] - e[2], t = e[3] - e[1];
+  v[3] = fmaf(2.0f, t, c);
+  v[4] = fmaf(-2.0f, t, c);
+  v[5] = fmaf(4.0f, e[1], fmaf(-5.0f, e[3], e[5]));
+}
+// z = m A (A^T applied to a row of six positions), and the same combination
+// of six rows' z for Y = A^T z
+__device__ __forceinline__ void w43_at(const float (&m)[6], float (&z)[4]) {
+  const float s12 = m[1] + m[2], d12 = m[1] - m[2], s34 = m[3] + m[4], d34 = m[3] - m[4];
+  z[0] = (m[0] + s12) + s34;
+  z[1] = fmaf(2.0f, d34, d12);
+  z[2] = fmaf(4.0f, s34, s12);
+  z[3] = fmaf(8.0f, d34, d12) + m[5];
+}
+
+// C4: activations in the chunk-of-4 layout [B][C/4][T][F][4] (input and
+// output; the freq-mean output is [B][T][C] either way), else NHWC
+// [B][T][F][C].  A chunk's halo plane is then a dense run of 16-byte pixels
+// (a halo DMA of 64 lanes touches ~9 cache lines instead of 64).
+template <int F, int EPI, int ROW, bool C4>
+__device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, int T, int Cin, int Cout,
+                                         const float* __restrict__ U, int u_bytes, const float* __restrict__ bias,
+                                         float* __restrict__ out, float* __restrict__ trash, int tb_per_clip,
+                                         int ngroups, int order2d) {
+  using G = W43Geom<F>;
+  constexpr int RS = G::RS, PS = G::PS;
+  extern __shared__ __attribute__((aligned(16))) float smem[];   // G::LDS_BYTES (dynamic)
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tg = wv & 1;
+  const int kk = lane >> 4, nn = lane & 15;
+
+  // XCD-aware item decode (conv_wino.hip): item -> XCD id & 7; on one XCD,
+  // tile blocks in order with their channel groups consecutive, or (order2d)
+  // rounds of 32 / order2d tile blocks x order2d channel groups
+  auto decode = [&](int item, int& b_, int& t0_, int& g_) -> bool {
+    const int xcd = item & 7, j = item >> 3;
+    int jb, cgi;
+    if (order2d) {
+      const int tbr = 32 / order2d;
+      const int idx = j & 31, r = j >> 5, ncg = ngroups / order2d;
+      const int tbg = r / ncg;
+      jb = tbr * tbg + idx % tbr;
+      cgi = order2d * (r - tbg * ncg) + idx / tbr;
+    } else {
+      jb = j / ngroups;
+      cgi = j - jb * ngroups;
+    }
+    const int tb = jb * 8 + xcd;
+    if (tb >= B * tb_per_clip) return false;
+    b_ = tb / tb_per_clip;
+    t0_ = 4 * G::TRW * (tb - b_ * tb_per_clip);   // first output row of the item
+    g_ = cgi;
+    return true;
+  };
+  int item = blockIdx.x;
+  int b = 0, t0 = 0, grp = 0;
+  if (!decode(item, b, t0, grp)) return;   // uniform
+
+  // this lane's tile within the item
+  const int tr = (F == 16 ? 4 * tg : F == 8 ? 8 * tg : 0) + nn / G::TFG;
+  const int tf = (F == 32 ? 4 * tg : 0) + nn % G::TFG;
+
+  // ---- DMA sources.  Buffer resources: the input (pixels outside the clip
+  // read out of range: zeros) and the U packs. ----
+  const __amdgpu_buffer_rsrc_t r_in =
+      __builtin_amdgcn_make_buffer_rsrc((void*)in, 0, (int)((int64_t)B * T * F * Cin * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t r_u = __builtin_amdgcn_make_buffer_rsrc((void*)U, 0, u_bytes, 0x00020000);
+  const int nchunks = Cin / 4;
+  // halo block wv of each plane: LDS positions q = 64 wv + lane of [row][RS]
+  auto halo_off = [&](int b_, int t0_) -> uint32_t {
+    const int q = 64 * wv + lane;
+    const int row = q / RS, col = q - (q / RS) * RS;
+    const int t = t0_ - 1 + row, f = col - 1;
+    const bool ok = row < G::RT && col < G::CS && t >= 0 && t < T && f >= 0 && f < F;
+    if constexpr (C4)   // chunk 0 of clip b_; a chunk adds T F 16 bytes (soffset)
+      return ok ? (uint32_t)((((b_ * (Cin / 4) * T + t) * F + f) * 16)) : 0x80000000u;
+    return ok ? (uint32_t)((((b_ * T + t) * F + f) * Cin) * 4) : 0x80000000u;
+  };
+  const uint32_t u_voff = 16 * lane + 1024 * wv;
+  const uint32_t bytes_per_chunk_u = 4 * G::USZ;
+  // DMA of chunk cc of an item (halo offsets hof, channel group g_) into the
+  // given slots; U units wv, wv + 12, wv + 24 and this wave's halo block
+  auto dma_u = [&](int g_, int cc, int uslot) {
+    if constexpr (SEDX_W43_ABL & 2) return;
+    const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)((g_ * nchunks + cc) * bytes_per_chunk_u));
+    const uint32_t m0 = __builtin_amdgcn_readfirstlane(w43_lds_addr(smem + G::U_OFF + uslot * G::USZ + 256 * wv));
+#pragma unroll
+    for (int q = 0; q < 3; ++q) w43_dma16(u_voff, r_u, so + q * 12288, m0 + q * 12288);
+  };
+  auto dma_h = [&](uint32_t hof, int cc, int hslot) {
+    if constexpr (SEDX_W43_ABL & 1) return;
+    const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)(16 * (C4 ? cc * T * F : cc)));
+    const uint32_t m0 = __builtin_amdgcn_readfirstlane(w43_lds_addr(smem + G::H_OFF + hslot * G::HALO + 64 * wv));
+    w43_dma4(hof, r_in, so, m0);
+    w43_dma4(hof, r_in, so + 4, m0 + 4 * PS);
+    w43_dma4(hof, r_in, so + 8, m0 + 8 * PS);
+    w43_dma4(hof, r_in, so + 12, m0 + 12 * PS);
+  };
+
+  // epilogue stores per wave per item (all issued: out-of-range ones go to
+  // this workgroup's trash); finisher waves 0-3 only
+  constexpr int S = ROW >= 4 ? 0 : EPI == EPI_STORE ? 16 : 4;
+  float* const tr_lane = trash + (blockIdx.x & 31) * 256 + 4 * lane;
+  // 4-channel group n .. n + 3 of output pixel (t, f) (rows To x cols Fo)
+  auto opix = [&](int t, int f, int n, int To, int Fo) -> float* {
+    if constexpr (C4) return out + ((((int64_t)b * (Cout / 4) + n / 4) * To + t) * Fo + f) * 4;
+    return out + (((int64_t)b * To + t) * Fo + f) * Cout + n;
+  };
+
+  // ---- prologue: biases (oldest; covered by the first wait), halo(0), then
+  // the groups of steps -2 and -1: {U(0), halo(1)}, {U(1), halo(2)} ----
+  if (wv < G::BIAS_MAX / 256) {   // wave-uniform
+    const int i = 256 * wv + 4 * lane;
+    const __amdgpu_buffer_rsrc_t r_b = __builtin_amdgcn_make_buffer_rsrc((void*)bias, 0, Cout * 4, 0x00020000);
+    w43_dma16(i < Cout ? 4 * i : 0x80000000u, r_b, 0,
+              __builtin_amdgcn_readfirstlane(w43_lds_addr(smem + G::BIAS_OFF + 256 * wv)));
+  }
+  uint32_t hof = halo_off(b, t0);
+  dma_h(hof, 0, 0);
+  dma_u(grp, 0, 0);
+  dma_h(hof, 1, 1);
+  dma_u(grp, 1, 1);
+  dma_h(hof, 2, 2);
+  if constexpr (S > 0) {
+    float* const vt = tr_lane;   // exactly S stores (never merged), as the epilogue's
+    const float zf = 0.0f;
+#pragma unroll
+    for (int i = 0; i < S; ++i) asm volatile("global_store_dword %0, %1, off" ::"v"(vt), "v"(zf) : "memory");
+  }
+
+  // the lane's patch in a halo slot: plane kk, tile (tr, tf)
+  const int p_base = kk * PS + 4 * tr * RS + 4 * tf;
+  // e = (B^T d)_ROW as a fold over the patch rows, in the order they are
+  // read: e = init(row PA[, row PB]), e = fma(CC, row PC, e), e = fma(CD, row PD, e)
+  //   ROW 0: d4;      -5 d2, 4 d0      ROW 1: d3 + d4; -4 d2, -4 d1
+  //   ROW 2: d4 - d3; -4 d2, 4 d1      ROW 3: d4 - d2;  2 d3, -2 d1
+  //   ROW 4: d4 - d2; -2 d3, 2 d1      ROW 5: d5;      -5 d3, 4 d1
+  constexpr int PA = ROW == 0 ? 4 : ROW == 5 ? 5 : ROW <= 2 ? 3 : 2;
+  constexpr int PB = (ROW == 0 || ROW == 5) ? -1 : 4;
+  constexpr int PC = ROW == 0 ? 2 : (ROW == 3 || ROW == 4 || ROW == 5) ? 3 : 2;
+  constexpr int PD = ROW == 0 ? 0 : 1;
+  constexpr float CC = ROW == 0 ? -5.0f : ROW == 1 ? -4.0f : ROW == 2 ? -4.0f : ROW == 3 ? 2.0f : ROW == 4 ? -2.0f : -5.0f;
+  constexpr float CD = ROW == 0 ? 4.0f : ROW == 1 ? -4.0f : ROW == 2 ? 4.0f : ROW == 3 ? -2.0f : ROW == 4 ? 2.0f : 4.0f;
+  // LDS reads of the main loop are inline asm with counted waits: the
+  // compiler would merge the patch reads into ds_read2_b64 (banked per 16
+  // lanes, where the 16 tiles' even bank pairs collide 2-way, and twice the
+  // LDS cycles of two ds_read_b64) — and with every LDS read hidden from it,
+  // the waits below are exact.  A wait names every register its consumers
+  // read, so no consumer is scheduled above it.
+  typedef float f2v __attribute__((ext_vector_type(2)));
+  // one patch row R (6 floats, 3 ds_read_b64) at LDS byte address a (the halo
+  // slot's patch base of the lane)
+  auto read_row = [](uint32_t a, auto r_tag, f2v (&x)[3]) {
+    constexpr int R = decltype(r_tag)::value;
+    asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(x[0]) : "v"(a), "n"(4 * (R * RS)));
+    asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(x[1]) : "v"(a), "n"(4 * (R * RS + 2)));
+    asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(x[2]) : "v"(a), "n"(4 * (R * RS + 4)));
+  };
+  // U fragment of position 6 ROW + J (byte address a of the lane in the U slot)
+  auto read_u = [](uint32_t a, auto j_tag, w43_f32x4& u) {
+    constexpr int J = decltype(j_tag)::value;
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(u) : "v"(a), "n"(4 * (6 * ROW + J) * 256));
+  };
+  auto wait_u = [](auto n_tag, w43_f32x4& u) {
+    asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(u) : "n"(decltype(n_tag)::value));
+  };
+  auto wait_r = [](auto n_tag, f2v (&x)[3], w43_f32x4& u) {
+    asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(u) : "n"(decltype(n_tag)::value));
+  };
+  auto wait_rr = [](auto n_tag, f2v (&x)[3], f2v (&y)[3], w43_f32x4& u) {
+    asm volatile("s_waitcnt lgkmcnt(%7)"
+                 : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(y[0]), "+v"(y[1]), "+v"(y[2]), "+v"(u)
+                 : "n"(decltype(n_tag)::value));
+  };
+  // a row's 6 floats as opaque scalars: the compiler would otherwise pair
+  // element-wise operations on two rows' halves into packed FP32
+  // (v_pk_add_f32), which this library bans (sedx_internal.h)
+  auto scal = [](const f2v (&x)[3], float (&d)[6]) {
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {
+      d[c] = x[c >> 1][c & 1];
+      asm volatile("" : "+v"(d[c]));
+    }
+  };
+  auto init_e = [&](const f2v (&xa)[3], const f2v (&xb)[3], float (&e)[6]) {
+    float a[6], b[6];
+    scal(xa, a);
+    if constexpr (PB >= 0) scal(xb, b);
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {
+      if constexpr (PB < 0) e[c] = a[c];
+      else if constexpr (ROW == 1) e[c] = a[c] + b[c];
+      else e[c] = b[c] - a[c];
+    }
+  };
+  auto fold_e = [&](float coef, const f2v (&x)[3], float (&e)[6]) {
+    float d[6];
+    scal(x, d);
+#pragma unroll
+    for (int c = 0; c < 6; ++c) e[c] = fmaf(coef, d[c], e[c]);
+  };
+  auto pin6 = [](float (&v)[6]) {
+#pragma unroll
+    for (int q = 0; q < 6; ++q) asm volatile("" : "+v"(v[q]));
+  };
+  using IPA = std::integral_constant<int, PA>;
+  using IPB = std::integral_constant<int, (PB < 0 ? 0 : PB)>;
+  using IPC = std::integral_constant<int, PC>;
+  using IPD = std::integral_constant<int, PD>;
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I3 = std::integral_constant<int, 3>;
+  using I4 = std::integral_constant<int, 4>;
+  using I5 = std::integral_constant<int, 5>;
+  const uint32_t h_lane = w43_lds_addr(smem + G::H_OFF + p_base);     // + slot * 4 HALO
+  const uint32_t u_lane = w43_lds_addr(smem + G::U_OFF + 4 * lane);   // + slot * 4 USZ
+  // V of the lane's 6 positions for the chunk in halo slot hs_ (item top: no
+  // MFMAs to hide behind)
+  auto transform = [&](int hs_, float (&v)[6]) {
+    const uint32_t a = h_lane + hs_ * (4 * G::HALO);
+    f2v xa[3], xb[3], xc[3], xd[3];
+    w43_f32x4 dummy = {0.0f, 0.0f, 0.0f, 0.0f};
+    read_row(a, IPA{}, xa);
+    if constexpr (PB >= 0) read_row(a, IPB{}, xb);
+    read_row(a, IPC{}, xc);
+    read_row(a, IPD{}, xd);
+    wait_rr(I0{}, xa, xb, dummy);
+    wait_rr(I0{}, xc, xd, dummy);
+    float e[6];
+    init_e(xa, xb, e);
+    fold_e(CC, xc, e);
+    fold_e(CD, xd, e);
+    w43_colt(e, v);
+    pin6(v);
+  };
+
+  w43_f32x4 acc[6][4];
+  float va[6], vb[6];
+  int us = 0, hs = 0;   // slots of the current chunk's U and halo
+
+  auto fence = []() { __builtin_amdgcn_sched_barrier(0); };
+  auto mfma4 = [&](int j, const w43_f32x4& u, float v) {
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) acc[j][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(u[nt], v, acc[j][nt], 0, 0, 0);
+  };
+
+  for (;;) {
+    const int nitem = item + (int)gridDim.x;
+    int nb_ = 0, nt0 = 0, ng = 0;
+    const bool has_next = decode(nitem, nb_, nt0, ng);
+    const uint32_t nhof = has_next ? halo_off(nb_, nt0) : hof;
+    if (!has_next) {
+      nb_ = b;
+      nt0 = t0;
+      ng = grp;
+    }
+    // item top: halo(0) landed (younger: the groups of steps -2, -1 and the
+    // previous epilogue's S stores)
+    w43_bar<2 * G::VM + S>();
+    transform(hs, va);
+#pragma unroll
+    for (int j = 0; j < 6; ++j)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) acc[j][nt] = w43_f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+
+    // step c: MFMAs of chunk c with V (vc) and U(c) read just in time (at most
+    // two positions ahead); V of chunk c + 1 from halo(c + 1) into vn, its
+    // patch rows folded as they arrive (unless LASTSTEP).  LDS reads in issue
+    // order: U0 U1 | U2 PA PB | U3 PC | U4 PD | U5 — the counts below are the
+    // reads younger than the awaited one.
+    auto step = [&](const float (&vc)[6], float (&vn)[6], int c, auto first_tag, auto last_tag) {
+      constexpr bool FIRST = decltype(first_tag)::value, LASTSTEP = decltype(last_tag)::value;
+      constexpr int NP0 = LASTSTEP ? 0 : (PB >= 0 ? 6 : 3), NP = LASTSTEP ? 0 : 3;
+      // U(c) and halo(c + 1) landed: issued two steps ago; younger: the
+      // previous step's group (+ the epilogue stores over an item's first two steps)
+      w43_bar<G::VM + (FIRST ? S : 0)>();
+      const int us1 = us == 2 ? 0 : us + 1, us2 = us1 == 2 ? 0 : us1 + 1;
+      const int hs1 = hs == 2 ? 0 : hs + 1;
+      const uint32_t ua = u_lane + us * (4 * G::USZ);
+      const uint32_t ha = h_lane + hs1 * (4 * G::HALO);
+      w43_f32x4 u0, u1, u2, u3, u4, u5;
+      f2v xa[3], xb[3], xc[3], xd[3];
+      float e[6];
+      read_u(ua, I0{}, u0);
+      read_u(ua, I1{}, u1);
+      // group of step c: U(c + 2) -> the U slot of c - 1, halo(c + 3) -> the
+      // halo slot of c (read during step c - 1)
+      if (c + 2 < nchunks) dma_u(grp, c + 2, us2);
+      else dma_u(ng, c + 2 - nchunks, us2);
+      if (c + 3 < nchunks) dma_h(hof, c + 3, hs);
+      else dma_h(nhof, c + 3 - nchunks, hs);
+      fence();
+      // position 0
+      read_u(ua, I2{}, u2);
+      if constexpr (!LASTSTEP) {
+        read_row(ha, IPA{}, xa);
+        if constexpr (PB >= 0) read_row(ha, IPB{}, xb);
+      }
+      wait_u(std::integral_constant<int, 2 + NP0>{}, u0);
+      mfma4(0, u0, vc[0]);
+      fence();
+      // position 1; e from PA (, PB)
+      read_u(ua, I3{}, u3);
+      if constexpr (!LASTSTEP) read_row(ha, IPC{}, xc);
+      wait_u(std::integral_constant<int, 2 + NP0 + NP>{}, u1);
+      mfma4(1, u1, vc[1]);
+      fence();
+      if constexpr (!LASTSTEP) {
+        wait_rr(std::integral_constant<int, 1 + NP>{}, xa, xb, u2);
+        init_e(xa, xb, e);
+      } else {
+        wait_u(I1{}, u2);
+      }
+      // position 2; fold PC
+      read_u(ua, I4{}, u4);
+      if constexpr (!LASTSTEP) read_row(ha, IPD{}, xd);
+      mfma4(2, u2, vc[2]);
+      fence();
+      if constexpr (!LASTSTEP) {
+        wait_r(std::integral_constant<int, 1 + NP>{}, xc, u3);
+        fold_e(CC, xc, e);
+      } else {
+        wait_u(I1{}, u3);
+      }
+      // position 3; fold PD
+      read_u(ua, I5{}, u5);
+      mfma4(3, u3, vc[3]);
+      fence();
+      if constexpr (!LASTSTEP) {
+        wait_r(I1{}, xd, u4);
+        fold_e(CD, xd, e);
+      } else {
+        wait_u(I1{}, u4);
+      }
+      // positions 4, 5; the column transform
+      mfma4(4, u4, vc[4]);
+      fence();
+      if constexpr (!LASTSTEP) {
+        w43_colt(e, vn);
+        pin6(vn);
+      }
+      wait_u(I0{}, u5);
+      mfma4(5, u5, vc[5]);
+      us = us1;
+      hs = hs1;
+    };
+    // steps in pairs (ping-pong V); nchunks even (launcher: Cin % 8 == 0, >= 16)
+    step(va, vb, 0, std::true_type{}, std::false_type{});
+    step(vb, va, 1, std::true_type{}, std::false_type{});
+    for (int c = 2; c < nchunks - 2; c += 2) {
+      step(va, vb, c, std::false_type{}, std::false_type{});
+      step(vb, va, c + 1, std::false_type{}, std::false_type{});
+    }
+    step(va, vb, nchunks - 2, std::false_type{}, std::false_type{});
+    step(vb, va, nchunks - 1, std::false_type{}, std::true_type{});
+
+    // ---- epilogue.  Exchange area: the U slot of the last step (us + 2 now);
+    // every wave's reads of it are done at the first barrier below. ----
+    float* const xb = smem + G::U_OFF + (us == 0 ? 2 : us - 1) * G::USZ + tg * (G::XROUND / 2);
+    auto xs = [&](int row, int s, int bp) { return ((row * 2 + s) * 2 + bp) * 128 + 2 * lane; };
+    // output element base of the item: first output row t0 of clip b
+    int le = lane;
+    asm volatile("" : "+v"(le));   // opaque: offsets computed here, not hoisted as live registers
+    const int kc = le >> 4;
+    const int trg = t0 / 4 + tr;   // the lane's tile row in the clip
+    w43_f32x4 ost[4];              // POOL2 / FMEAN: one 4-channel group per channel tile
+    w43_f32x4 ost2[4];             // STORE: the 2 x 2 pixels of the current channel tile
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int nt = q >> 1;
+      if constexpr (SEDX_W43_ABL & 4) {   // timing build: no exchange / output transform
+        if constexpr (ROW < 4) {
+#pragma unroll
+          for (int s = 0; s < 2; ++s) {
+            const int r = 2 * (q & 1) + s;
+            const float v = (acc[0][nt][r] + acc[1][nt][r]) + (acc[4][nt][r] + acc[5][nt][r]);
+            ost[nt][r] = v;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) ost2[i][r] = v;
+          }
+          if constexpr (EPI == EPI_STORE) {
+            if (q & 1) {
+              const int n = grp * 64 + 16 * nt + 4 * kc;
+#pragma unroll
+              for (int a = 0; a < 2; ++a) {
+                const int t = 4 * trg + 2 * (ROW >> 1) + a;
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                  const int f = 4 * tf + 2 * (ROW & 1) + c;
+                  float* dst = t < T ? opix(t, f, n, T, F) : tr_lane;
+                  *reinterpret_cast<w43_f32x4*>(dst) = ost2[2 * a + c];
+                }
+              }
+            }
+          }
+        }
+        continue;
+      }
+      w43_lds_bar();   // previous round's reads done (and, at q = 0, the last step's U reads)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int r = 2 * (q & 1) + s;
+        float m[6], z[4];
+#pragma unroll
+        for (int j = 0; j < 6; ++j) m[j] = acc[j][nt][r];
+        w43_at(m, z);
+        *reinterpret_cast<float2*>(xb + xs(ROW, s, 0)) = make_float2(z[0], z[1]);
+        *reinterpret_cast<float2*>(xb + xs(ROW, s, 1)) = make_float2(z[2], z[3]);
+      }
+      w43_lds_bar();
+      if constexpr (ROW < 4) {
+        const int n = grp * 64 + 16 * nt + 4 * kc;   // first of the lane's 4 channels
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const int r = 2 * (q & 1) + s;
+          const float bv = smem[G::BIAS_OFF + n + r];
+          if constexpr (EPI == EPI_FMEAN) {
+            // output row a = ROW of the tile: Y[ROW][0..3], ReLU, sum over
+            // the 4 columns, + the other tile of the row (lane ^ 1)
+            float z[6][4];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+              const float2 lo = *reinterpret_cast<const float2*>(xb + xs(i, s, 0));
+              const float2 hi = *reinterpret_cast<const float2*>(xb + xs(i, s, 1));
+              z[i][0] = lo.x; z[i][1] = lo.y; z[i][2] = hi.x; z[i][3] = hi.y;
+            }
+            float sum = 0.0f;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+              float col[6], y[4];
+#pragma unroll
+              for (int i = 0; i < 6; ++i) col[i] = z[i][c];
+              w43_at(col, y);
+              sum += fmaxf(y[ROW] + bv, 0.0f);
+            }
+            const float other = __shfl_xor(sum, 1);
+            ost[nt][r] = ((tf & 1) ? other + sum : sum + other) * (1.0f / F);
+          } else {
+            // the 2 x 2 block (2A, 2A + 1) x (2B, 2B + 1) of the tile
+            constexpr int A = ROW >> 1, Bc = ROW & 1;
+            float z[6][2];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+              const float2 w = *reinterpret_cast<const float2*>(xb + xs(i, s, Bc));
+              z[i][0] = w.x;
+              z[i][1] = w.y;
+            }
+            float y[2][2];
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+              float col[6], yy[4];
+#pragma unroll
+              for (int i = 0; i < 6; ++i) col[i] = z[i][c];
+              w43_at(col, yy);
+              y[0][c] = fmaxf(yy[2 * A] + bv, 0.0f);
+              y[1][c] = fmaxf(yy[2 * A + 1] + bv, 0.0f);
+            }
+            if constexpr (EPI == EPI_POOL2) {
+              ost[nt][r] = (((y[0][0] + y[0][1]) + y[1][0]) + y[1][1]) * 0.25f;
+            } else {
+#pragma unroll
+              for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int c = 0; c < 2; ++c) ost2[2 * a + c][r] = y[a][c];
+            }
+          }
+        }
+        if constexpr (EPI == EPI_STORE) {
+          if (q & 1) {   // the channel tile's 4 registers done: 4 pixels x 4 channels
+#pragma unroll
+            for (int a = 0; a < 2; ++a) {
+              const int t = 4 * trg + 2 * (ROW >> 1) + a;
+#pragma unroll
+              for (int c = 0; c < 2; ++c) {
+                const int f = 4 * tf + 2 * (ROW & 1) + c;
+                float* dst = t < T ? opix(t, f, n, T, F) : tr_lane;
+                *reinterpret_cast<w43_f32x4*>(dst) = ost2[2 * a + c];
+              }
+            }
+          }
+        }
+      }
+    }
+    if constexpr (ROW < 4 && EPI != EPI_STORE) {
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const int n = grp * 64 + 16 * nt + 4 * kc;
+        float* dst;
+        if constexpr (EPI == EPI_POOL2) {
+          const int to = 2 * trg + (ROW >> 1), fo = 2 * tf + (ROW & 1);
+          dst = to < T / 2 ? opix(to, fo, n, T / 2, F / 2) : tr_lane;
+        } else {
+          const int t = 4 * trg + ROW;
+          dst = (t < T && !(tf & 1)) ? out + (int64_t)(b * T + t) * Cout + n : tr_lane;
+        }
+        *reinterpret_cast<w43_f32x4*>(dst) = ost[nt];
+      }
+    }
+    if (!has_next) break;
+    item = nitem;
+    b = nb_;
+    t0 = nt0;
+    grp = ng;
+    hof = nhof;
+  }
+}
+
+#define SEDX_W43_ROWS(F_, EPI_, C4_, ...)                              \
+  switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >> 1) {    \
+    case 0: w43_body<F_, EPI_, 0, C4_>(__VA_ARGS__); break;           \
+    case 1: w43_body<F_, EPI_, 1, C4_>(__VA_ARGS__); break;           \
+    case 2: w43_body<F_, EPI_, 2, C4_>(__VA_ARGS__); break;           \
+    case 3: w43_body<F_, EPI_, 3, C4_>(__VA_ARGS__); break;           \
+    case 4: w43_body<F_, EPI_, 4, C4_>(__VA_ARGS__); break;           \
+    default: w43_body<F_, EPI_, 5, C4_>(__VA_ARGS__); break;          \
+  }
+
+template <int F, int EPI, bool C4>
+__global__ __launch_bounds__(768, 1) void conv3x3_wino43_kernel(const float* __restrict__ in, int B, int T, int Cin,
+                                                                int Cout, const float* __restrict__ U, int u_bytes,
+                                                                const float* __restrict__ bias, float* __restrict__ out,
+                                                                float* __restrict__ trash, int tb_per_clip,
+                                                                int ngroups, int order2d) {
+  SEDX_W43_ROWS(F, EPI, C4, in, B, T, Cin, Cout, U, u_bytes, bias, out, trash, tb_per_clip, ngroups, order2d)
+}
+#undef SEDX_W43_ROWS
+
+#ifndef SEDX_W43_ITEMS
+#define SEDX_W43_ITEMS 2
+#endif
+
+template <int F>
+static void launch_w43_f(const float* in, int B, int T, int Cin, int Cout, const float* U, const float* bias,
+                         float* out, int epi, float* trash, int order, bool c4, hipStream_t s) {
+  using G = W43Geom<F>;
+  // output rows the epilogue covers: POOL2 drops an odd last row
+  const int rows = epi == EPI_POOL2 ? 2 * (T / 2) : T;
+  const int trows = (rows + 3) / 4;
+  const int tb_per_clip = (trows + G::TRW - 1) / G::TRW;
+  const int ngroups = Cout / G::NCH;
+  const int64_t tblocks = (int64_t)B * tb_per_clip;
+  const int64_t nitems = (tblocks + 7) / 8 * 8 * ngroups;
+  const int64_t u_bytes = (int64_t)Cin * Cout * 36 * 4;
+  if (nitems > INT32_MAX || tblocks <= 0 || (int64_t)B * T * F * Cin * 4 >= INT32_MAX || u_bytes >= INT32_MAX)
+    return note_launch_error(hipErrorInvalidValue);
+  int ncu = 256, dev = 0;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  const int64_t resident = (int64_t)ncu / 8 * 8;
+  const int64_t per = (nitems + SEDX_W43_ITEMS - 1) / SEDX_W43_ITEMS;
+  const int64_t nwg = std::min<int64_t>(nitems, std::max<int64_t>(std::max<int64_t>(8, resident), (per + 7) / 8 * 8));
+  // rounds of 32 / G tile blocks x G channel groups (conv_wino.hip): the G
+  // whose round streams the fewest bytes through an XCD's L2
+  int order2d = 0;
+  if (order && nwg % 256 == 0 && (nitems / 8) % 32 == 0) {
+    const int64_t slab = (int64_t)36 * Cin * G::NCH * 4, halo = (int64_t)G::RT * G::CS * Cin * 4;
+    int64_t best = (int64_t)ngroups * slab + (32 / std::min(ngroups, 32)) * halo;
+    for (int gr = 1; gr <= 8 && gr < ngroups; gr *= 2) {
+      const int64_t bytes = gr * slab + (32 / gr) * halo;
+      if (ngroups % gr == 0 && tblocks % (8 * (32 / gr)) == 0 && bytes < best) {
+        best = bytes;
+        order2d = gr;
+      }
+    }
+  }
+#define SEDX_W43_LAUNCH(E)                                                                                 \
+  {                                                                                                        \
+    auto* k_ = c4 ? conv3x3_wino43_kernel<F, E, true> : conv3x3_wino43_kernel<F, E, false>;                \
+    if (!launch_info(reinterpret_cast<const void*>(k_), G::THREADS, G::LDS_BYTES).ok) return;              \
+    hipLaunchKernelGGL(k_, dim3((unsigned)nwg), dim3(G::THREADS), G::LDS_BYTES, s, in, B, T, Cin, Cout, U, \
+                       (int)u_bytes, bias, out, trash, tb_per_clip, ngroups, order2d);                     \
+    return;                                                                                                \
+  }
+  if constexpr (F == 8) {
+    if (epi == EPI_STORE) SEDX_W43_LAUNCH(EPI_STORE);
+    if (epi == EPI_FMEAN) SEDX_W43_LAUNCH(EPI_FMEAN);
+  } else {
+    if (epi == EPI_STORE) SEDX_W43_LAUNCH(EPI_STORE);
+    if (epi == EPI_POOL2) SEDX_W43_LAUNCH(EPI_POOL2);
+  }
+#undef SEDX_W43_LAUNCH
+  note_launch_error(hipErrorInvalidValue);
+}
+
+void launch_conv3x3_wino43(const float* in, int B, int T, int F, int Cin, int Cout, const float* U43,
+                           const float* bias, float* out, int epi, float* trash, hipStream_t s, int order, bool c4) {
+  if (Cin % 8 != 0 || Cin < 16 || Cout % 64 != 0 || Cout > 512 || B <= 0 || T <= 0)
+    return note_launch_error(hipErrorInvalidValue);
+  // byte offsets are 32-bit (buffer DMA): batches whose input passes 2^31
+  // bytes run as several launches over whole clips (same per-clip work)
+  const int64_t in_clip = (int64_t)T * F * Cin;
+  const int64_t out_clip = epi == EPI_STORE ? (int64_t)T * F * Cout
+                           : epi == EPI_POOL2 ? (int64_t)(T / 2) * (F / 2) * Cout : (int64_t)T * Cout;
+  const int64_t bmax = (INT32_MAX / 4 - 1) / in_clip;
+  if (bmax < 1) return note_launch_error(hipErrorInvalidValue);
+  for (int64_t b0 = 0; b0 < B; b0 += bmax) {
+    const int bs = (int)std::min<int64_t>(bmax, B - b0);
+    const float* in_s = in + b0 * in_clip;
+    float* out_s = out + b0 * out_clip;
+    switch (F) {
+      case 32: launch_w43_f<32>(in_s, bs, T, Cin, Cout, U43, bias, out_s, epi, trash, order, c4, s); break;
+      case 16: launch_w43_f<16>(in_s, bs, T, Cin, Cout, U43, bias, out_s, epi, trash, order, c4, s); break;
+      case 8: launch_w43_f<8>(in_s, bs, T, Cin, Cout, U43, bias, out_s, epi, trash, order, c4, s); break;
+      default: return note_launch_error(hipErrorInvalidValue);
+    }
+  }
+}
+
+// [B][C/4][T][F][4] -> [B][T][F][C]: one thread per 16-byte group
+__global__ __launch_bounds__(256) void c4_to_nhwc_kernel(const float4* __restrict__ src, int T, int F, int C4,
+                                                         int64_t n, float4* __restrict__ dst) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;   // source group: ((b C4 + c) T + t) F + f
+  if (i >= n) return;
+  int64_t r = i;
+  const int f = (int)(r % F);
+  r /= F;
+  const int t = (int)(r % T);
+  r /= T;
+  const int c = (int)(r % C4);
+  const int64_t b = r / C4;
+  dst[((b * T + t) * F + f) * C4 + c] = src[i];
+}
+
+void launch_c4_to_nhwc(const float* src, int B, int T, int F, int C, float* dst, hipStream_t s) {
+  const int64_t n = (int64_t)B * T * F * (C / 4);
+  if (n <= 0 || C % 4 != 0) return note_launch_error(hipErrorInvalidValue);
+  hipLaunchKernelGGL(c4_to_nhwc_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                     reinterpret_cast<const float4*>(src), T, F, C / 4, n, reinterpret_cast<float4*>(dst));
+}
+
+// U = G g G^T per (input channel, output channel) in float64 from the
+// BN-folded weights wf [Cout][Cin][9], rounded once to fp32, packed
+// [Cout/64][Cin/4][36 p][4 k][16 m][4 nt] with output channel 64 group +
+// 16 nt + m and input channel 4 chunk + k (a chunk's slab is the LDS image;
+// lane l = 16 k + m reads its 4 channel tiles as one 16-byte word).
+void pack_conv_wino43(const double* wf, int Cin, int Cout, float* Up) {
+  static const double Gm[6][3] = {{1.0 / 4, 0, 0},
+                                  {-1.0 / 6, -1.0 / 6, -1.0 / 6},
+                                  {-1.0 / 6, 1.0 / 6, -1.0 / 6},
+                                  {1.0 / 24, 1.0 / 12, 1.0 / 6},
+                                  {1.0 / 24, -1.0 / 12, 1.0 / 6},
+                                  {0, 0, 1}};
+  const int nch = Cin / 4;
+  for (int o = 0; o < Cout; ++o)
+    for (int i = 0; i < Cin; ++i) {
+      const double* g = wf + ((size_t)o * Cin + i) * 9;
+      double tmp[6][3];
+      for (int a = 0; a < 6; ++a)
+        for (int y = 0; y < 3; ++y) tmp[a][y] = Gm[a][0] * g[0 * 3 + y] + Gm[a][1] * g[1 * 3 + y] + Gm[a][2] * g[2 * 3 + y];
+      const int grp = o / 64, nt = (o % 64) / 16, m = o % 16, chunk = i / 4, k = i % 4;
+      for (int a = 0; a < 6; ++a)
+        for (int c = 0; c < 6; ++c) {
+          const double u = tmp[a][0] * Gm[c][0] + tmp[a][1] * Gm[c][1] + tmp[a][2] * Gm[c][2];
+          const int p = 6 * a + c;
+          Up[(((((size_t)grp * nch + chunk) * 36 + p) * 4 + k) * 16 + m) * 4 + nt] = (float)u;
+        }
+    }
+}
+
+}  // namespace sedx

@@ -126,12 +126,29 @@ void launch_conv3x3_wino(const float* in, int B, int T, int F, int Cin, int Cout
                          const float* U, const float* bias, float* out, int epi,
                          const float* zero16, float* trash, hipStream_t s, int order = 0);
 void pack_conv_wino(const double* wf, int Cin, int Cout, float* U);   // U: Cin * Cout * 16 floats
+// Same contract as fp32 Winograd F(4x4,3x3) (conv_wino43.hip), blocks 2-4:
+// F in {32, 16, 8}, Cin % 8 == 0 and >= 16, Cout % 64 == 0 and <= 512; U43
+// from pack_conv_wino43 (Cin * Cout * 36 floats); pixels outside the clip are
+// zero-filled by the buffer DMA's range check (no zero block); trash >= 64 x
+// 128 floats of device scratch for the out-of-range epilogue stores.
+// c4: input and output in the chunk-of-4 layout [B][C/4][T][F][4] (the
+// freq-mean output stays [B][T][C]); else NHWC.  Batches are split over whole
+// clips, so B-major offsets hold in both layouts.
+void launch_conv3x3_wino43(const float* in, int B, int T, int F, int Cin, int Cout, const float* U43,
+                           const float* bias, float* out, int epi, float* trash, hipStream_t s, int order = 0,
+                           bool c4 = false);
+// [B][C/4][T][F][4] -> [B][T][F][C] (stage captures of the C4 layers)
+void launch_c4_to_nhwc(const float* src, int B, int T, int F, int C, float* dst, hipStream_t s);
+void pack_conv_wino43(const double* wf, int Cin, int Cout, float* U);   // U: Cin * Cout * 36 floats
 // block 1 as one Winograd launch: conv1 (w1 [64][9] folded, b1 [64], ReLU)
 // computed into conv2's halo images in LDS, conv2 (U of block 1's conv2) +
 // bias + ReLU + 2x2 pool: X0 [B][T][64] -> [B][T/2][32][64]; bit-identical to
 // launch_conv1_nhwc followed by launch_conv3x3_wino
+// c4: the pooled output in the chunk-of-4 layout [B][16][T/2][32][4] (the
+// F(4x4,3x3) layers' input), else NHWC
 void launch_block1_wino(const float* x0, int B, int T, const float* w1, const float* b1, const float* U,
-                        const float* bias, float* out, const float* zero16, float* trash, hipStream_t s);
+                        const float* bias, float* out, const float* zero16, float* trash, hipStream_t s,
+                        bool c4 = false);
 // block 1's conv1 + BN + ReLU: X0 [B][T][64] -> [B][T][64][64] (w1 [64][9] folded, b1 [64])
 void launch_conv1_nhwc(const float* x0, int B, int T, const float* w1, const float* b1, float* out,
                        hipStream_t s);

@@ -18,6 +18,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <new>
 #include <vector>
 
 #include "../../include/sedx.h"
@@ -29,7 +30,7 @@ const char* window_loop(int sample_rate, int64_t L_clip, const sedx_window_spec&
   out->start.clear();
   out->len.clear();
   if (sample_rate <= 0 || L_clip <= 0) return "empty clip or bad sample rate";
-  if (sp.reserved != 0) return "sedx_window_spec.reserved must be 0";
+  if (sp.vote != 0 && sp.vote != 1) return "sedx_window_spec.vote must be 0 (averaged merge) or 1 (vote merge)";
   if (sp.driver != SEDX_DRIVER_PREDICT && sp.driver != SEDX_DRIVER_MAIN_STRONG) return "unknown window driver";
   if (sp.sample_duration <= 0) return "sample_duration must be a positive number of seconds";
   const double sd = sp.sample_duration;
@@ -74,7 +75,9 @@ const char* build_merge_plan(const std::vector<int64_t>& frames, int64_t step, i
     if (frames[w] < 0 || (int64_t)wbase[w] + frames[w] > INT32_MAX) return "merge plan too large";
     wbase[w + 1] = wbase[w] + (int32_t)frames[w];
   }
-  m.reserve((size_t)frames[0] + (n - 1) * (size_t)std::max<int64_t>(step, 1));
+  // the merged length never exceeds the frames of all windows (a window adds
+  // at most its own frames), however large the step
+  m.reserve((size_t)std::min<int64_t>(wbase[n], frames[0] + (int64_t)(n - 1) * std::max<int64_t>(step, 1)));
   for (int64_t t = 0; t < frames[0]; ++t) m.push_back({wbase[0] + (int32_t)t});     // merged = curr_preds
   for (size_t w = 1; w < n; ++w) {
     // merge(prev, curr, sample_duration, num_segment = w + 1, overlap_value)
@@ -134,23 +137,36 @@ using namespace sedx;
 
 extern "C" {
 
+// (host vectors: a failed allocation returns SEDX_ENOMEM, never throws
+// across the C ABI)
 sedx_status sedx_window_starts(int32_t sample_rate, int64_t L_clip, const sedx_window_spec* spec,
                                int64_t* h_start, int64_t* h_len, int64_t capacity, int64_t* n_windows) {
   if (!spec || !n_windows || capacity < 0) return SEDX_EINVAL;
-  WindowLoop wl;
-  if (window_loop(sample_rate, L_clip, *spec, &wl)) return SEDX_EINVAL;
-  *n_windows = (int64_t)wl.start.size();
-  const int64_t k = std::min<int64_t>(capacity, *n_windows);
-  if (h_start) std::copy(wl.start.begin(), wl.start.begin() + k, h_start);
-  if (h_len) std::copy(wl.len.begin(), wl.len.begin() + k, h_len);
-  return SEDX_OK;
+  try {
+    WindowLoop wl;
+    if (window_loop(sample_rate, L_clip, *spec, &wl)) return SEDX_EINVAL;
+    *n_windows = (int64_t)wl.start.size();
+    const int64_t k = std::min<int64_t>(capacity, *n_windows);
+    if (h_start) std::copy(wl.start.begin(), wl.start.begin() + k, h_start);
+    if (h_len) std::copy(wl.len.begin(), wl.len.begin() + k, h_len);
+    return SEDX_OK;
+  } catch (const std::bad_alloc&) {
+    return SEDX_ENOMEM;
+  } catch (...) {
+    return SEDX_EINVAL;
+  }
 }
 
 sedx_status sedx_merge_host(const float* h_win, const int64_t* frames, int64_t n_win, int64_t C,
                             int32_t sample_duration, double overlap_value, int32_t avg, float* h_out,
                             int64_t capacity_frames, int64_t* merged_frames) {
   if (!frames || n_win <= 0 || C <= 0 || !merged_frames || (h_out && !h_win)) return SEDX_EINVAL;
-  const int64_t step = (int64_t)(100.0 * overlap_value);    // int(100 * overlap_value), float64
+  // int(100 * overlap_value) in float64; the same range as the handle API
+  // (a NaN / inf / huge value would be undefined in the cast)
+  const double stepd = 100.0 * overlap_value;
+  if (!std::isfinite(stepd) || !(std::fabs(stepd) < 1e9)) return SEDX_EINVAL;
+  const int64_t step = (int64_t)stepd;
+  try {
   MergePlan plan;
   if (build_merge_plan(std::vector<int64_t>(frames, frames + n_win), step, sample_duration, avg != 0, &plan))
     return SEDX_EINVAL;
@@ -168,6 +184,11 @@ sedx_status sedx_merge_host(const float* h_win, const int64_t* frames, int64_t n
       h_out[f * C + k] = d > 1 ? s / (float)d : s;      // float32 /= int (utilities.py:435)
     }
   return SEDX_OK;
+  } catch (const std::bad_alloc&) {
+    return SEDX_ENOMEM;
+  } catch (...) {
+    return SEDX_EINVAL;
+  }
 }
 
 }  // extern "C"

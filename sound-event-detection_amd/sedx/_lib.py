@@ -23,11 +23,13 @@ EXPORTS = ['sedx_create', 'sedx_destroy', 'sedx_last_error', 'sedx_version', 'se
            'sedx_forward_windows_vote', 'sedx_events_workspace_size', 'sedx_events_device',
            'sedx_forward_i16', 'sedx_wav_parse', 'sedx_wav_decode_mono', 'sedx_resample_size',
            'sedx_resample_workspace_size', 'sedx_resample', 'sedx_gamma_workspace_size',
-           'sedx_set_tuning', 'sedx_set_capture', 'sedx_window_starts', 'sedx_merge_host', 'sedx_check_error']
+           'sedx_set_tuning', 'sedx_set_capture', 'sedx_window_starts', 'sedx_merge_host', 'sedx_check_error',
+           'sedx_abi_version']
 TUNE_GRU_KERNEL, TUNE_GRU_HANDOFF, TUNE_WINO_BLOCK1, TUNE_MEL_MFMA, TUNE_GRU_SPIN, TUNE_WINO_ORDER = 0, 1, 2, 3, 4, 5
 TUNE_GAMMA_SPEC = 6
+TUNE_WINO_F43 = 7
 PRECISION = {'exact': 0, 'x3': 1, 'winograd': 2}
-STAGES = ['frontend', 'b1c1', 'b1c2', 'b2c1', 'b2c2', 'b3c1', 'b3c2', 'b4c1', 'b4c2', 'seq', 'head']
+STAGES = ['frontend', 'b1c1', 'b1c2', 'b2c1', 'b2c2', 'b3c1', 'b3c2', 'b4c1', 'b4c2', 'seq', 'head', 'pipeline_wait']
 
 
 class SedxWavInfo(ctypes.Structure):
@@ -41,20 +43,25 @@ RESAMPLE = {'kaiser_best': 0, 'kaiser_fast': 1}
 
 DRIVER = {'predict': 0, 'main_strong': 1}
 
+ABI_VERSION = 5   # include/sedx.h SEDX_ABI_VERSION
+
 
 class SedxWindowSpec(ctypes.Structure):
     _fields_ = [('driver', ctypes.c_int32), ('overlap', ctypes.c_int32),
-                ('sample_duration', ctypes.c_int32), ('reserved', ctypes.c_int32),
+                ('sample_duration', ctypes.c_int32), ('vote', ctypes.c_int32),
                 ('overlap_value', ctypes.c_double), ('audio_duration', ctypes.c_double)]
 
 
-def window_spec(sample_duration, overlap_value, driver='predict', overlap=True, audio_duration=None):
-    """sedx_window_spec of one windowed-driver call (include/sedx.h)."""
+def window_spec(sample_duration, overlap_value, driver='predict', overlap=True, audio_duration=None, vote=False):
+    """sedx_window_spec of one windowed-driver call (include/sedx.h); vote=True
+    for sedx_forward_windows_vote (its geometry / workspace queries then size
+    the vote merge, which accepts a zero merge step)."""
     if driver not in DRIVER:
         raise ValueError('driver must be one of %s' % sorted(DRIVER))
     if int(sample_duration) != sample_duration:
         raise ValueError('sample_duration is an int number of seconds in the reference (predict.py:701)')
-    return SedxWindowSpec(DRIVER[driver], int(bool(overlap)), int(sample_duration), 0, float(overlap_value),
+    return SedxWindowSpec(DRIVER[driver], int(bool(overlap)), int(sample_duration), int(bool(vote)),
+                          float(overlap_value),
                           float(audio_duration) if audio_duration is not None else 0.0)
 
 
@@ -93,6 +100,7 @@ def lib():
         'sedx_destroy': ([P], None),
         'sedx_last_error': ([P], ctypes.c_char_p),
         'sedx_version': ([], ctypes.c_char_p),
+        'sedx_abi_version': ([], I32),
         'sedx_load_param': ([P, ctypes.c_char_p, P, PI64, I32], I32),
         'sedx_finalize_weights': ([P], I32),
         'sedx_output_geometry': ([P, I64, PI64, PI64], I32),
@@ -129,6 +137,9 @@ def lib():
         fn = getattr(L, name)
         fn.argtypes = args
         fn.restype = res
+    if L.sedx_abi_version() != ABI_VERSION:
+        raise RuntimeError('libsedx.so ABI %d, this binding expects %d (include/sedx.h SEDX_ABI_VERSION): '
+                           'rebuild the library' % (L.sedx_abi_version(), ABI_VERSION))
     _lib = L
     return L
 

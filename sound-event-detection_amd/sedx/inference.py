@@ -51,11 +51,13 @@ def _ptr(t):
 
 
 def window_geometry(model, clip_samples, sample_duration=5, overlap_value=1.0, driver='predict', overlap=True,
-                    audio_duration=None):
+                    audio_duration=None, vote=False):
     """(windows per clip, samples per full window, merged frames) of one
-    windowed-driver call (sedx_window_geometry)."""
+    windowed-driver call (sedx_window_geometry); vote=True sizes the vote
+    merge (predict_windows_vote), which, unlike avg_merge, accepts a zero
+    merge step."""
     nat = model.native(torch.device('cuda', torch.cuda.current_device()))
-    spec = _lib.window_spec(sample_duration, overlap_value, driver, overlap, audio_duration)
+    spec = _lib.window_spec(sample_duration, overlap_value, driver, overlap, audio_duration, vote=vote)
     nw, ws, nf = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
     _lib.check(_lib.lib().sedx_window_geometry(nat.h, int(clip_samples), ctypes.byref(spec), ctypes.byref(nw),
                                                ctypes.byref(ws), ctypes.byref(nf)), nat.h, 'window_geometry')
@@ -129,6 +131,11 @@ def _windows(model, audio, spec, vote_thres):
         _lib.check(L.sedx_forward_windows_vote(nat.h, _ptr(x), n_clips, clip_len, ctypes.byref(spec),
                                                thr.ctypes.data_as(ctypes.c_void_p), _ptr(merged),
                                                _ptr(ws), wsz.value, stream), nat.h, 'forward_windows_vote')
+    # the merged / voted batch is complete once the stream is: a GRU hand-off
+    # that timed out inside this forward (NaN outputs) raises here, not at the
+    # next call on the handle (or never)
+    torch.cuda.current_stream(x.device).synchronize()
+    model.check_error()
     return merged
 
 
@@ -157,7 +164,7 @@ def predict_windows_vote(model, audio, sample_duration, overlap_value, bin_thres
     window binarised with ``bin_threshold`` (the reference passes
     sed_low_threshold, :1082) and overlap-added without averaging.  Returns
     the vote counts [n_clips, N, classes] (float32, exact integers)."""
-    spec = _lib.window_spec(sample_duration, overlap_value, 'main_strong', True, audio_duration)
+    spec = _lib.window_spec(sample_duration, overlap_value, 'main_strong', True, audio_duration, vote=True)
     return _windows(model, audio, spec, bin_threshold)
 
 

@@ -88,6 +88,29 @@ def test_roofline_winograd_block1(bench):
         bench.WINO_BLOCK1 = 2
 
 
+def test_roofline_winograd_f43(bench):
+    """Blocks 2-4 as Winograd F(4x4,3x3) (the default): their launches are
+    conv3x3_wino43_kernel<F, EPI> and execute 36/144 of the direct conv's
+    multiplies; with --wino-f43 0 they are the F(2x2,3x3) row-wave kernels
+    (16/36); block 1 stays F(2x2,3x3) either way."""
+    stage = {s: 0.1 for s in bench.CONV_STAGES}
+    stage['b4c2'] = 1.0
+    assert bench.WINO_F43 == 1
+    w = bench.roofline(stage, 32, 'winograd')
+    assert w['kernel'] == 'sedx::conv3x3_wino43_kernel<8, 2> (b4c2)'
+    assert w['flops_per_launch'] == bench.conv_flops('b4c2', 32, 1001) * 36.0 / 144.0
+    assert 'F(4x4,3x3)' in w['arith'] and 'b1c2 F(2x2,3x3)' in w['arith']
+    assert bench.conv_kernel_name('b2c2', 'winograd') == 'sedx::conv3x3_wino43_kernel<32, 1>'
+    assert bench.conv_kernel_name('b1c2', 'winograd') == 'sedx::wino_block1_kernel<2>'
+    try:
+        bench.WINO_F43 = 0
+        w = bench.roofline(stage, 32, 'winograd')
+        assert w['kernel'] == 'sedx::conv3x3_wino_kernel<8, 2, 2, 2> (b4c2)'
+        assert w['flops_per_launch'] == bench.conv_flops('b4c2', 32, 1001) * 16.0 / 36.0
+    finally:
+        bench.WINO_F43 = 1
+
+
 def test_roofline_fracs_are_fractions(bench):
     """The launch time behind ``frac`` is the isolated HIP-event time when the
     run measured it; every ``frac*`` field is executed FLOPs over the matrix
@@ -142,6 +165,13 @@ def test_bench_launches_n_ranks(n):
         assert e['WORLD_SIZE'] == str(n) and e['LOCAL_RANK'] == e['RANK'] and e['MASTER_ADDR'] == '127.0.0.1'
     # whole-job clips/s over all ranks from the max-over-ranks elapsed time
     assert abs(d['value'] - n * B * steps / (d['ms_per_step'] * steps / 1e3)) <= 0.01 * d['value'] + 1e-3
+    # the config-5 leg (BASELINE configs[5]: the Transformer model at N GPUs)
+    # runs through the same sharded step, framewise + clipwise gathered
+    c5 = d['configs']['config5']
+    assert c5['n_gpus'] == n and c5['global_batch'] == n * B and c5['batch_per_gpu'] == B
+    assert c5['backend'] == 'gloo' and 'clipwise' in c5['gathered']
+    assert 'Transformer' in c5['metric'] and c5['scaling'] == 'weak'
+    assert abs(c5['value'] - n * B * steps / (c5['ms_per_step'] * steps / 1e3)) <= 0.01 * c5['value'] + 1e-3
 
 
 def test_bench_launcher_fails_when_a_rank_fails():

@@ -261,6 +261,30 @@ def test_gru_spin_timeout_surfaces(kernel, n_clips):
     assert torch.equal(out, ref)
 
 
+@pytest.mark.parametrize('vote', [False, True])
+def test_windows_spin_timeout_raises(vote):
+    """A GRU hand-off spin that runs out inside a windowed forward
+    (SEDX_TUNE_GRU_SPIN = 0) raises from predict_windows / predict_windows_vote
+    themselves (sedx.inference syncs and calls model.check_error() before
+    returning), so sweep_overlap never extracts events from NaN merges; with
+    the default bound the same handle is clean again."""
+    from sedx import _lib, inference
+    m = build(GRU).set_precision('exact')
+    audio = torch.from_numpy(synth.make_waveforms(16, seconds=10.0, sample_rate=16000, seed=33)).cuda()
+    call = ((lambda: inference.predict_windows_vote(m, audio, 5, 1.0, 0.3)) if vote
+            else (lambda: inference.predict_windows(m, audio, 5, 1.0, driver='main_strong')))
+    with torch.no_grad():
+        ref = call().clone()
+        _tune(m, _lib.TUNE_GRU_SPIN, 0)
+        try:
+            with pytest.raises(RuntimeError, match='GRU'):
+                call()
+        finally:
+            _tune(m, _lib.TUNE_GRU_SPIN, 1 << 24)
+        again = call()
+    assert torch.equal(again, ref)
+
+
 def test_gru_exact_recurrence_is_fp32():
     """Exact mode runs the recurrence on fp32 MFMA operands: it agrees with
     the per-(clip, direction) fp32-FMA kernel and the oracle far inside the
@@ -553,16 +577,36 @@ def test_stage_times_accumulate():
     torch.cuda.synchronize()
     assert L.sedx_stage_times(nat.h, ms, len(_lib.STAGES), ctypes.byref(n)) == 0
     assert n.value == len(_lib.STAGES)
-    acc = list(ms[:])
-    assert all(v > 0 for v in acc), acc
+    acc = dict(zip(_lib.STAGES, ms[:]))
+    wait = acc.pop('pipeline_wait')
+    assert all(v > 0 for v in acc.values()), acc
+    assert 0 <= wait < acc['frontend'] + 0.05, wait     # not pipelined: nothing to wait for
     # reset after the read: nothing recorded since
     assert L.sedx_stage_times(nat.h, ms, len(_lib.STAGES), ctypes.byref(n)) == 0
     assert all(v == 0 for v in ms[:])
+    # pipelined over two streams: the wait for the previous forward's conv
+    # stack is its own stage, so the frontend stage times the frontend only
+    m.set_pipelined(True)
+    try:
+        with torch.no_grad():
+            for i in range(8):
+                with torch.cuda.stream(streams[i % 2]):
+                    outs.append(m(w)['framewise_output'])
+        torch.cuda.synchronize()
+        assert L.sedx_stage_times(nat.h, ms, len(_lib.STAGES), ctypes.byref(n)) == 0
+        pip = dict(zip(_lib.STAGES, ms[:]))
+    finally:
+        m.set_pipelined(False)
+    print('frontend', acc['frontend'], 'pipelined frontend', pip['frontend'], 'wait', pip['pipeline_wait'])
+    assert pip['pipeline_wait'] >= 0
+    assert pip['frontend'] <= 3 * acc['frontend'] + 0.1, (pip['frontend'], acc['frontend'])
     assert L.sedx_set_profiling(nat.h, 1) == 0
     with torch.no_grad():
         m(w)
     assert L.sedx_stage_times(nat.h, ms, len(_lib.STAGES), ctypes.byref(n)) == 0
-    assert all(v > 0 for v in ms[:])
+    one = dict(zip(_lib.STAGES, ms[:]))
+    assert one.pop('pipeline_wait') >= 0
+    assert all(v > 0 for v in one.values()), one
     assert L.sedx_set_profiling(nat.h, 0) == 0
     for o in outs[1:]:
         assert torch.equal(o, outs[0])

@@ -1,0 +1,204 @@
+// Winograd F(4x4,3x3) fp32 conv (conv_wino43.hip) against F(2x2,3x3)
+// (conv_wino.hip) and a float64 direct conv: the six block 2-4 layer shapes at
+// B clips x 10 s @ 16 kHz (sampled float64 checks, then both timed), plus
+// small edge shapes (odd T, a few frames, ragged last tile blocks) checked
+// against float64 at EVERY output.  Exit 0 = all within tolerance.
+#include <hip/hip_runtime.h>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <vector>
+#include "../sound-event-detection_amd/csrc/sedx_internal.h"
+
+namespace sedx {
+void launch_conv3x3_wino43(const float* in, int B, int T, int F, int Cin, int Cout, const float* U43,
+                           const float* bias, float* out, int epi, float* trash, hipStream_t s, int order, bool c4);
+void pack_conv_wino43(const double* wf, int Cin, int Cout, float* U);
+}
+
+struct Layer { const char* name; int B, T, F, cin, cout, epi; bool full; };
+
+int main(int argc, char** argv) {
+  const int B = argc > 1 ? atoi(argv[1]) : 32;
+  const int reps = argc > 2 ? atoi(argv[2]) : 20;
+  const char* only = argc > 3 ? argv[3] : nullptr;
+  const int order = getenv("W43_ORDER") ? atoi(getenv("W43_ORDER")) : 1;
+  std::vector<Layer> LM = {{"b2c1", B, 500, 32, 64, 128, sedx::EPI_STORE, false},
+                           {"b2c2", B, 500, 32, 128, 128, sedx::EPI_POOL2, false},
+                           {"b3c1", B, 250, 16, 128, 256, sedx::EPI_STORE, false},
+                           {"b3c2", B, 250, 16, 256, 256, sedx::EPI_POOL2, false},
+                           {"b4c1", B, 125, 8, 256, 512, sedx::EPI_STORE, false},
+                           {"b4c2", B, 125, 8, 512, 512, sedx::EPI_FMEAN, false},
+                           // edge shapes, every output checked
+                           {"e32s", 3, 37, 32, 64, 128, sedx::EPI_STORE, true},
+                           {"e32p", 2, 23, 32, 128, 64, sedx::EPI_POOL2, true},
+                           {"e16p", 3, 9, 16, 64, 128, sedx::EPI_POOL2, true},
+                           {"e16s", 1, 70, 16, 32, 64, sedx::EPI_STORE, true},
+                           {"e8m", 2, 67, 8, 64, 192, sedx::EPI_FMEAN, true},
+                           {"e8s", 5, 3, 8, 16, 64, sedx::EPI_STORE, true}};
+  float *d_in, *d_in4, *d_o1, *d_o2, *d_o3, *d_bias, *d_u, *d_u43, *d_zero, *d_trash;
+  size_t max_in = 0, max_out = 0, max_w = 0;
+  for (const Layer& l : LM) {
+    max_in = std::max(max_in, (size_t)l.B * l.T * l.F * l.cin);
+    max_out = std::max(max_out, (size_t)l.B * l.T * l.F * l.cout);
+    max_w = std::max(max_w, (size_t)l.cin * l.cout * 36);
+  }
+  hipMalloc(&d_in, max_in * 4); hipMalloc(&d_o1, max_out * 4); hipMalloc(&d_o2, max_out * 4);
+  hipMalloc(&d_in4, max_in * 4); hipMalloc(&d_o3, max_out * 4);
+  hipMalloc(&d_bias, 512 * 4); hipMalloc(&d_u, max_w * 4); hipMalloc(&d_u43, max_w * 4);
+  hipMalloc(&d_zero, 4096); hipMemset(d_zero, 0, 4096);
+  hipMalloc(&d_trash, 64 * 256 * 4);
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0); hipEventCreate(&e1);
+  std::mt19937 rng(7);
+  std::normal_distribution<float> nd(0.f, 1.f);
+  double tot_2 = 0, tot_4 = 0, tot_4c = 0;
+  bool ok = true;
+  for (const Layer& l : LM) {
+    if (only && strcmp(only, l.name) != 0) continue;
+    const size_t nin = (size_t)l.B * l.T * l.F * l.cin;
+    std::vector<float> in(nin), bias(l.cout);
+    for (auto& v : in) v = std::max(0.f, nd(rng));
+    std::vector<double> w((size_t)l.cout * l.cin * 9);
+    const float ws = std::sqrt(2.f / (9 * l.cin));
+    for (auto& v : w) v = (double)(float)(nd(rng) * ws);
+    for (auto& v : bias) v = 0.1f * nd(rng);
+    std::vector<float> U((size_t)l.cin * l.cout * 16), U43((size_t)l.cin * l.cout * 36);
+    sedx::pack_conv_wino(w.data(), l.cin, l.cout, U.data());
+    sedx::pack_conv_wino43(w.data(), l.cin, l.cout, U43.data());
+    hipMemcpy(d_in, in.data(), nin * 4, hipMemcpyHostToDevice);
+    // the same input in the chunk-of-4 layout [B][C/4][T][F][4]
+    {
+      std::vector<float> in4(nin);
+      for (int b = 0; b < l.B; ++b)
+        for (int t = 0; t < l.T; ++t)
+          for (int f = 0; f < l.F; ++f)
+            for (int c = 0; c < l.cin; ++c)
+              in4[((((size_t)b * (l.cin / 4) + c / 4) * l.T + t) * l.F + f) * 4 + c % 4] =
+                  in[(((size_t)b * l.T + t) * l.F + f) * l.cin + c];
+      hipMemcpy(d_in4, in4.data(), nin * 4, hipMemcpyHostToDevice);
+    }
+    hipMemcpy(d_bias, bias.data(), l.cout * 4, hipMemcpyHostToDevice);
+    hipMemcpy(d_u, U.data(), U.size() * 4, hipMemcpyHostToDevice);
+    hipMemcpy(d_u43, U43.data(), U43.size() * 4, hipMemcpyHostToDevice);
+    const int To = l.epi == sedx::EPI_POOL2 ? l.T / 2 : l.T;
+    const int Fo = l.epi == sedx::EPI_POOL2 ? l.F / 2 : (l.epi == sedx::EPI_FMEAN ? 1 : l.F);
+    const size_t nout = (size_t)l.B * To * Fo * l.cout;
+    hipMemset(d_o1, 0xff, nout * 4);
+    hipMemset(d_o2, 0xff, nout * 4);
+    hipMemset(d_o3, 0xff, nout * 4);
+    const bool with2 = !l.full || l.cin >= 32;   // F(2,3) launcher: Cin >= 32
+    auto w2 = [&]() {
+      sedx::launch_conv3x3_wino(d_in, l.B, l.T, l.F, l.cin, l.cout, d_u, d_bias, d_o1, l.epi, d_zero, d_trash, 0, order);
+    };
+    auto w4 = [&]() {
+      sedx::launch_conv3x3_wino43(d_in, l.B, l.T, l.F, l.cin, l.cout, d_u43, d_bias, d_o2, l.epi, d_trash, 0, order,
+                                  false);
+    };
+    auto w4c = [&]() {   // chunk-of-4 layout in and out (the library's F(4,3) chain)
+      sedx::launch_conv3x3_wino43(d_in4, l.B, l.T, l.F, l.cin, l.cout, d_u43, d_bias, d_o3, l.epi, d_trash, 0, order,
+                                  true);
+    };
+    if (with2) w2();
+    w4();
+    w4c();
+    const hipError_t ke = hipDeviceSynchronize();
+    std::vector<float> o1(nout), o2(nout), o3(nout), o3n(nout);
+    hipMemcpy(o1.data(), d_o1, nout * 4, hipMemcpyDeviceToHost);
+    hipMemcpy(o2.data(), d_o2, nout * 4, hipMemcpyDeviceToHost);
+    hipMemcpy(o3.data(), d_o3, nout * 4, hipMemcpyDeviceToHost);
+    // C4 output back to the NHWC order of o2 (freq mean: [B][T][C] in both)
+    if (l.epi == sedx::EPI_FMEAN) {
+      o3n = o3;
+    } else {
+      for (int b = 0; b < l.B; ++b)
+        for (int t = 0; t < To; ++t)
+          for (int f = 0; f < Fo; ++f)
+            for (int c = 0; c < l.cout; ++c)
+              o3n[(((size_t)b * To + t) * Fo + f) * l.cout + c] =
+                  o3[((((size_t)b * (l.cout / 4) + c / 4) * To + t) * Fo + f) * 4 + c % 4];
+    }
+    size_t c4diff = 0;
+    for (size_t i = 0; i < nout; ++i) c4diff += std::memcmp(&o2[i], &o3n[i], 4) != 0;
+    // float64 reference (conv + bias + ReLU, then the epilogue)
+    auto conv_px = [&](int b, int t, int f, int o) {
+      double s = 0;
+      for (int dt = 0; dt < 3; ++dt)
+        for (int df = 0; df < 3; ++df) {
+          const int tt = t + dt - 1, ff = f + df - 1;
+          if (tt < 0 || tt >= l.T || ff < 0 || ff >= l.F) continue;
+          const float* x = &in[(((size_t)b * l.T + tt) * l.F + ff) * l.cin];
+          for (int i = 0; i < l.cin; ++i) s += (double)x[i] * w[((size_t)o * l.cin + i) * 9 + dt * 3 + df];
+        }
+      return std::max(0.0, s + bias[o]);
+    };
+    auto ref_at = [&](size_t idx) {
+      const int o = idx % l.cout;
+      size_t r = idx / l.cout;
+      const int fo = r % Fo;
+      r /= Fo;
+      const int to = r % To, b = (int)(r / To);
+      if (l.epi == sedx::EPI_POOL2)
+        return (conv_px(b, 2 * to, 2 * fo, o) + conv_px(b, 2 * to, 2 * fo + 1, o) + conv_px(b, 2 * to + 1, 2 * fo, o) +
+                conv_px(b, 2 * to + 1, 2 * fo + 1, o)) * 0.25;
+      if (l.epi == sedx::EPI_FMEAN) {
+        double s = 0;
+        for (int f = 0; f < l.F; ++f) s += conv_px(b, to, f, o);
+        return s / l.F;
+      }
+      return conv_px(b, to, fo, o);
+    };
+    size_t nan = 0;
+    double omax = 0, e2max = 0, e4max = 0, e4sq = 0;
+    size_t nchk = 0;
+    std::uniform_int_distribution<size_t> pick(0, nout - 1);
+    const size_t nsamp = l.full ? nout : 400;
+    for (size_t k = 0; k < nsamp; ++k) {
+      const size_t idx = l.full ? k : (k < 8 ? (k % 2 ? nout - 1 - k : k) : pick(rng));
+      if (!std::isfinite(o2[idx])) { ++nan; continue; }
+      const double ref = ref_at(idx);
+      omax = std::max(omax, std::fabs(ref));
+      if (with2) e2max = std::max(e2max, std::fabs(o1[idx] - ref));
+      const double e = std::fabs(o2[idx] - ref);
+      e4max = std::max(e4max, e);
+      e4sq += e * e;
+      ++nchk;
+    }
+    const double tol = 2e-4 * std::max(1.0, omax);
+    const bool lok = ke == hipSuccess && nan == 0 && e4max < tol && c4diff == 0;
+    ok = ok && lok;
+    float m2 = 0, m4 = 0, m4c = 0;
+    if (!l.full) {
+      auto timeit = [&](auto fn) {
+        fn();
+        hipEventRecord(e0, 0);
+        for (int r = 0; r < reps; ++r) fn();
+        hipEventRecord(e1, 0);
+        hipEventSynchronize(e1);
+        float ms = 0;
+        hipEventElapsedTime(&ms, e0, e1);
+        return ms / reps;
+      };
+      m2 = timeit(w2);
+      m4 = timeit(w4);
+      m4c = timeit(w4c);
+      tot_2 += m2;
+      tot_4 += m4;
+      tot_4c += m4c;
+    }
+    const double fl = 2.0 * l.B * l.T * l.F * l.cin * l.cout * 9;   // direct-conv FLOPs
+    const double fl4 = fl * 36.0 / 144.0;                           // F(4,3) matrix-pipe FLOPs (no tile padding)
+    printf("%-5s B=%d T=%d  F(2,3) %.4f ms  F(4,3) nhwc %.4f  c4 %.4f ms (MFMA %.1f TF/s = %.3f of 157.3)  x%.2f  "
+           "|w2-ref| %.2e |w4-ref| max %.2e rms %.2e  max|ref| %.2f  checked %zu nonfinite %zu  c4!=nhwc %zu  %s\n",
+           l.name, l.B, l.T, m2, m4, m4c, m4c > 0 ? fl4 / m4c / 1e9 : 0.0, m4c > 0 ? fl4 / m4c / 1e9 / 157.3 : 0.0,
+           m4c > 0 ? m2 / m4c : 0.0, e2max, e4max, std::sqrt(e4sq / std::max<size_t>(1, nchk)), omax, nchk, nan,
+           c4diff, lok ? "OK" : "MISMATCH");
+    fflush(stdout);
+  }
+  printf("total F(2,3) %.4f ms  F(4,3) nhwc %.4f ms  c4 %.4f ms  (x%.2f)  %s  (err=%s, launch=%s)\n", tot_2, tot_4,
+         tot_4c, tot_4c > 0 ? tot_2 / tot_4c : 0.0, ok ? "ALL OK" : "MISMATCH", hipGetErrorString(hipGetLastError()),
+         hipGetErrorString(sedx::take_launch_error()));
+  return ok ? 0 : 1;
+}
