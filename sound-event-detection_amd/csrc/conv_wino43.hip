@@ -66,7 +66,7 @@ typedef float w43_f32x4 __attribute__((ext_vector_type(4)));
 
 // Ablation builds (tools/wino43_bench.cpp only, results WRONG, timing only):
 // SEDX_W43_ABL bit 1 drops the halo DMAs, 2 the U DMAs, 4 the epilogue's
-// exchange and output transform (stores kept)
+// exchange and output transform (stores kept), 8 the epilogue's barriers
 #ifndef SEDX_W43_ABL
 #define SEDX_W43_ABL 0
 #endif
@@ -86,20 +86,27 @@ struct W43Geom {
   // take the 16 even values mod 32 (b64 bank pairs): 2 RS = 8 (mod 32) for
   // 4 x 4 groups, 2 RS = 20 (mod 32) for 8 x 2
   static constexpr int RS = F == 32 ? 36 : F == 16 ? 20 : 10;
-  static constexpr int HB = WAVES;                   // 64-dword DMA blocks per plane (one per wave)
+  // a plane's halo in 64-dword DMA blocks, one per wave 0..HB-1 (RT RS <= 704
+  // for every F); wave 11 issues its four halo DMAs into an LDS trash block,
+  // so every wave has the same DMA count per step
+  static constexpr int HB = 11;
   static constexpr int PS = 64 * HB + 2;             // plane stride, = 2 mod 4 (odd bank pairs for odd k)
   static constexpr int HALO = 4 * PS;                // dwords per halo slot
   static constexpr int USZ = 36 * 4 * NCH;           // dwords per U slot ([p][k][m][nt])
   static constexpr int NB = 3;                       // ring depth (U and halo)
+  // epilogue exchange per round: [row 6][reg 2][b pair 2][lane 64][2] per tile
+  // group, in the U slot freed by the item's last step
+  static constexpr int XTG = 6 * 2 * 2 * 128;
   static constexpr int U_OFF = 0, H_OFF = NB * USZ, BIAS_OFF = H_OFF + NB * HALO, BIAS_MAX = 512;
-  static constexpr int LDS_BYTES = 4 * (BIAS_OFF + BIAS_MAX);
+  static constexpr int HTRASH_OFF = BIAS_OFF + BIAS_MAX;   // 64 dwords: wave 11's halo DMAs
+  static constexpr int LDS_BYTES = 4 * (HTRASH_OFF + 64);
   static constexpr int VM = 7;                       // DMAs per wave per step (3 U units + 4 halo planes)
-  // epilogue exchange per round, in the free U slot: [tg][row 6][reg 2][b pair 2][lane 64][2]
-  static constexpr int XROUND = 2 * 6 * 2 * 2 * 128;
+
   static_assert(F == 32 || F == 16 || F == 8, "F");
   static_assert(RT * RS <= 64 * HB, "halo plane fits its DMA blocks");
+  static_assert(HB == WAVES - 1, "wave 11: trash halo block");
   static_assert(36 % WAVES == 0, "U units per wave");
-  static_assert(XROUND <= USZ, "exchange fits one U slot");
+  static_assert(2 * XTG <= USZ, "both tile groups' exchange fits one U slot");
   static_assert(LDS_BYTES <= 160 * 1024, "LDS per workgroup");
   static_assert(FT * TRW == TILES && TFG * TRG == 16, "tile groups");
 };
@@ -237,11 +244,16 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
   auto dma_h = [&](uint32_t hof, int cc, int hslot) {
     if constexpr (SEDX_W43_ABL & 1) return;
     const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)(16 * (C4 ? cc * T * F : cc)));
-    const uint32_t m0 = __builtin_amdgcn_readfirstlane(w43_lds_addr(smem + G::H_OFF + hslot * G::HALO + 64 * wv));
+    // wave 11 (no block: its lanes' offsets are all out of range, halo_off)
+    // writes its four zero DMAs into the trash block — a select, not a branch
+    const bool tw = wv == G::HB;
+    const uint32_t m0 = __builtin_amdgcn_readfirstlane(
+        w43_lds_addr(tw ? smem + G::HTRASH_OFF : smem + G::H_OFF + hslot * G::HALO + 64 * wv));
+    const uint32_t pstep = tw ? 0u : 4u * PS;
     w43_dma4(hof, r_in, so, m0);
-    w43_dma4(hof, r_in, so + 4, m0 + 4 * PS);
-    w43_dma4(hof, r_in, so + 8, m0 + 8 * PS);
-    w43_dma4(hof, r_in, so + 12, m0 + 12 * PS);
+    w43_dma4(hof, r_in, so + 4, m0 + pstep);
+    w43_dma4(hof, r_in, so + 8, m0 + 2 * pstep);
+    w43_dma4(hof, r_in, so + 12, m0 + 3 * pstep);
   };
 
   // epilogue stores per wave per item (all issued: out-of-range ones go to
@@ -392,7 +404,14 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
     for (int nt = 0; nt < 4; ++nt) acc[j][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(u[nt], v, acc[j][nt], 0, 0, 0);
   };
 
+  // the first item's chunk 0: halo(0) landed (younger: the groups of steps
+  // -2, -1 and the S dummy stores)
+  w43_bar<2 * G::VM + S>();
   for (;;) {
+    // V of the item's chunk 0.  A later item's halo(0) was DMA'd with the
+    // previous item's step n - 3 and every wave waited for it before that
+    // item's last step's barrier: no wait here
+    transform(hs, va);
     const int nitem = item + (int)gridDim.x;
     int nb_ = 0, nt0 = 0, ng = 0;
     const bool has_next = decode(nitem, nb_, nt0, ng);
@@ -402,10 +421,6 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
       nt0 = t0;
       ng = grp;
     }
-    // item top: halo(0) landed (younger: the groups of steps -2, -1 and the
-    // previous epilogue's S stores)
-    w43_bar<2 * G::VM + S>();
-    transform(hs, va);
 #pragma unroll
     for (int j = 0; j < 6; ++j)
 #pragma unroll
@@ -413,9 +428,10 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
 
     // step c: MFMAs of chunk c with V (vc) and U(c) read just in time (at most
     // two positions ahead); V of chunk c + 1 from halo(c + 1) into vn, its
-    // patch rows folded as they arrive (unless LASTSTEP).  LDS reads in issue
-    // order: U0 U1 | U2 PA PB | U3 PC | U4 PD | U5 — the counts below are the
-    // reads younger than the awaited one.
+    // patch rows folded as they arrive (not in the last step: V of the next
+    // item's chunk 0 is computed after the epilogue, which keeps its registers
+    // free).  LDS reads in issue order: U0 U1 | U2 PA PB | U3 PC | U4 PD | U5
+    // — the counts below are the reads younger than the awaited one.
     auto step = [&](const float (&vc)[6], float (&vn)[6], int c, auto first_tag, auto last_tag) {
       constexpr bool FIRST = decltype(first_tag)::value, LASTSTEP = decltype(last_tag)::value;
       constexpr int NP0 = LASTSTEP ? 0 : (PB >= 0 ? 6 : 3), NP = LASTSTEP ? 0 : 3;
@@ -504,7 +520,8 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
 
     // ---- epilogue.  Exchange area: the U slot of the last step (us + 2 now);
     // every wave's reads of it are done at the first barrier below. ----
-    float* const xb = smem + G::U_OFF + (us == 0 ? 2 : us - 1) * G::USZ + tg * (G::XROUND / 2);
+    float* const xfree = smem + G::U_OFF + (us == 0 ? 2 : us - 1) * G::USZ;
+    float* const xbuf0 = xfree + tg * G::XTG;
     auto xs = [&](int row, int s, int bp) { return ((row * 2 + s) * 2 + bp) * 128 + 2 * lane; };
     // output element base of the item: first output row t0 of clip b
     int le = lane;
@@ -521,10 +538,15 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
 #pragma unroll
           for (int s = 0; s < 2; ++s) {
             const int r = 2 * (q & 1) + s;
-            const float v = (acc[0][nt][r] + acc[1][nt][r]) + (acc[4][nt][r] + acc[5][nt][r]);
+            // every position's accumulator feeds the stores (no MFMA is dead code)
+            const float v = ((acc[0][nt][r] + acc[1][nt][r]) + (acc[2][nt][r] + acc[3][nt][r])) +
+                            (acc[4][nt][r] + acc[5][nt][r]);
             ost[nt][r] = v;
 #pragma unroll
             for (int i = 0; i < 4; ++i) ost2[i][r] = v;
+          }
+          if constexpr (EPI != EPI_STORE) {
+            if (q & 1) *reinterpret_cast<w43_f32x4*>(tr_lane) = ost[nt];
           }
           if constexpr (EPI == EPI_STORE) {
             if (q & 1) {
@@ -544,7 +566,13 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
         }
         continue;
       }
-      w43_lds_bar();   // previous round's reads done (and, at q = 0, the last step's U reads)
+      // round q writes buffer q & 1: the reads of round q - 2 (same buffer)
+      // finished before round q - 1's barrier; at q = 0 the last step's U reads
+      // (double-buffering the rounds by parity, one barrier per round, cost
+      // 20-80 spilled VGPRs in the compiler's allocation: one buffer, two
+      // barriers per round)
+      if constexpr (!(SEDX_W43_ABL & 8)) w43_lds_bar();
+      float* const xb = xbuf0;
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const int r = 2 * (q & 1) + s;
@@ -555,7 +583,7 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
         *reinterpret_cast<float2*>(xb + xs(ROW, s, 0)) = make_float2(z[0], z[1]);
         *reinterpret_cast<float2*>(xb + xs(ROW, s, 1)) = make_float2(z[2], z[3]);
       }
-      w43_lds_bar();
+      if constexpr (!(SEDX_W43_ABL & 8)) w43_lds_bar();
       if constexpr (ROW < 4) {
         const int n = grp * 64 + 16 * nt + 4 * kc;   // first of the lane's 4 channels
 #pragma unroll
@@ -626,22 +654,19 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
               }
             }
           }
+        } else {   // POOL2 / FMEAN: the channel tile's 4 registers done: one 4-channel group
+          if (q & 1) {
+            float* dst;
+            if constexpr (EPI == EPI_POOL2) {
+              const int to = 2 * trg + (ROW >> 1), fo = 2 * tf + (ROW & 1);
+              dst = to < T / 2 ? opix(to, fo, n, T / 2, F / 2) : tr_lane;
+            } else {
+              const int t = 4 * trg + ROW;
+              dst = (t < T && !(tf & 1)) ? out + (int64_t)(b * T + t) * Cout + n : tr_lane;
+            }
+            *reinterpret_cast<w43_f32x4*>(dst) = ost[nt];
+          }
         }
-      }
-    }
-    if constexpr (ROW < 4 && EPI != EPI_STORE) {
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-        const int n = grp * 64 + 16 * nt + 4 * kc;
-        float* dst;
-        if constexpr (EPI == EPI_POOL2) {
-          const int to = 2 * trg + (ROW >> 1), fo = 2 * tf + (ROW & 1);
-          dst = to < T / 2 ? opix(to, fo, n, T / 2, F / 2) : tr_lane;
-        } else {
-          const int t = 4 * trg + ROW;
-          dst = (t < T && !(tf & 1)) ? out + (int64_t)(b * T + t) * Cout + n : tr_lane;
-        }
-        *reinterpret_cast<w43_f32x4*>(dst) = ost[nt];
       }
     }
     if (!has_next) break;

@@ -73,7 +73,7 @@ def test_roofline_winograd_block1(bench):
     stage['b1c1'] = 0.1
     assert bench.WINO_BLOCK1 == 2
     w = bench.roofline(stage, 32, 'winograd')
-    assert w['kernel'] == 'sedx::wino_block1_kernel<2> (b1c2)'
+    assert w['kernel'] == 'sedx::wino_block1_kernel<2, true> (b1c2)'
     assert w['flops_per_launch'] == bench.conv_flops('b1c2', 32, 1001) * 16.0 / 36.0
     try:
         bench.WINO_BLOCK1 = 1
@@ -97,11 +97,11 @@ def test_roofline_winograd_f43(bench):
     stage['b4c2'] = 1.0
     assert bench.WINO_F43 == 1
     w = bench.roofline(stage, 32, 'winograd')
-    assert w['kernel'] == 'sedx::conv3x3_wino43_kernel<8, 2> (b4c2)'
+    assert w['kernel'] == 'sedx::conv3x3_wino43_kernel<8, 2, true> (b4c2)'
     assert w['flops_per_launch'] == bench.conv_flops('b4c2', 32, 1001) * 36.0 / 144.0
     assert 'F(4x4,3x3)' in w['arith'] and 'b1c2 F(2x2,3x3)' in w['arith']
-    assert bench.conv_kernel_name('b2c2', 'winograd') == 'sedx::conv3x3_wino43_kernel<32, 1>'
-    assert bench.conv_kernel_name('b1c2', 'winograd') == 'sedx::wino_block1_kernel<2>'
+    assert bench.conv_kernel_name('b2c2', 'winograd') == 'sedx::conv3x3_wino43_kernel<32, 1, true>'
+    assert bench.conv_kernel_name('b1c2', 'winograd') == 'sedx::wino_block1_kernel<2, true>'
     try:
         bench.WINO_F43 = 0
         w = bench.roofline(stage, 32, 'winograd')

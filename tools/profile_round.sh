@@ -19,12 +19,14 @@ step() {
   if [ $rc -ne 0 ]; then echo "stopping"; exit $rc; fi
 }
 [ -n "$NO_FULL" ] || step bench_full 600 python bench.py --steps 20 --warmup 3
-# LEGS: extra profiled legs beside the precisions: config3 (Transformer) and
-# config4 (gammatone 32k frontend + forward), headline arithmetic
+# LEGS: extra profiled legs beside the precisions: config3 (Transformer),
+# config4 (gammatone 32k frontend + forward) and window (predict.py windows:
+# 192 x 5 s windows per call), headline arithmetic
 for P in ${PRECISIONS:-winograd exact x3} ${LEGS}; do
   case $P in
     config3) A="--no-cpu-baseline --no-side --streams 1 --model transformer" ;;
     config4) A="--no-cpu-baseline --no-side --streams 1 --mode gamma" ;;
+    window) A="--no-cpu-baseline --no-side --streams 1 --mode window" ;;
     *) A="--no-cpu-baseline --no-side --streams 1 --precision $P" ;;
   esac
   step kt_$P 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/$P/kt -o kt -- python bench.py --steps 10 --warmup 2 $A
