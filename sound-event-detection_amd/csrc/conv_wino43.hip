@@ -71,6 +71,21 @@ typedef float w43_f32x4 __attribute__((ext_vector_type(4)));
 #define SEDX_W43_ABL 0
 #endif
 
+// Diagnostic builds only (SEDX_W43_STAMPS, tools/wino43_bench.cpp): per-wave
+// s_memtime intervals summed over every wave of every 16th workgroup:
+// [0] item top (chunk-0 transform) [1] steps [2] epilogue [3] whole wave [4] items
+#ifdef SEDX_W43_STAMPS
+__device__ unsigned long long g_w43_stamps[8];
+#define W43_MARK(i)                                            \
+  {                                                            \
+    const unsigned long long n_ = __builtin_amdgcn_s_memtime(); \
+    w43_st[i] += n_ - w43_t;                                   \
+    w43_t = n_;                                                \
+  }
+#else
+#define W43_MARK(i)
+#endif
+
 template <int F>
 struct W43Geom {
   static constexpr int WAVES = 12, THREADS = 64 * WAVES;
@@ -407,6 +422,11 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
   // the first item's chunk 0: halo(0) landed (younger: the groups of steps
   // -2, -1 and the S dummy stores)
   w43_bar<2 * G::VM + S>();
+#ifdef SEDX_W43_STAMPS
+  unsigned long long w43_st[5] = {0, 0, 0, 0, 0};
+  unsigned long long w43_t = __builtin_amdgcn_s_memtime();
+  const unsigned long long w43_t0 = w43_t;
+#endif
   for (;;) {
     // V of the item's chunk 0.  A later item's halo(0) was DMA'd with the
     // previous item's step n - 3 and every wave waited for it before that
@@ -509,6 +529,7 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
       hs = hs1;
     };
     // steps in pairs (ping-pong V); nchunks even (launcher: Cin % 8 == 0, >= 16)
+    W43_MARK(0)
     step(va, vb, 0, std::true_type{}, std::false_type{});
     step(vb, va, 1, std::true_type{}, std::false_type{});
     for (int c = 2; c < nchunks - 2; c += 2) {
@@ -518,6 +539,7 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
     step(va, vb, nchunks - 2, std::false_type{}, std::false_type{});
     step(vb, va, nchunks - 1, std::false_type{}, std::true_type{});
 
+    W43_MARK(1)
     // ---- epilogue.  Exchange area: the U slot of the last step (us + 2 now);
     // every wave's reads of it are done at the first barrier below. ----
     float* const xfree = smem + G::U_OFF + (us == 0 ? 2 : us - 1) * G::USZ;
@@ -669,6 +691,10 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
         }
       }
     }
+    W43_MARK(2)
+#ifdef SEDX_W43_STAMPS
+    w43_st[4] += 1;
+#endif
     if (!has_next) break;
     item = nitem;
     b = nb_;
@@ -676,6 +702,13 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
     grp = ng;
     hof = nhof;
   }
+#ifdef SEDX_W43_STAMPS
+  if (lane == 0 && (blockIdx.x & 15) == 0) {
+    w43_st[3] = __builtin_amdgcn_s_memtime() - w43_t0;
+    for (int i = 0; i < 5; ++i) atomicAdd(&g_w43_stamps[i], w43_st[i]);
+    atomicAdd(&g_w43_stamps[5], 1ull);
+  }
+#endif
 }
 
 #define SEDX_W43_ROWS(F_, EPI_, C4_, ...)                              \
@@ -777,6 +810,17 @@ void launch_conv3x3_wino43(const float* in, int B, int T, int F, int Cin, int Co
     }
   }
 }
+
+#ifdef SEDX_W43_STAMPS
+void w43_stamps_rw(unsigned long long* h, bool reset) {
+  if (reset) {
+    static const unsigned long long z[8] = {};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_w43_stamps), z, sizeof(z));
+  } else {
+    (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_w43_stamps), 8 * sizeof(unsigned long long));
+  }
+}
+#endif
 
 // [B][C/4][T][F][4] -> [B][T][F][C]: one thread per 16-byte group
 __global__ __launch_bounds__(256) void c4_to_nhwc_kernel(const float4* __restrict__ src, int T, int F, int C4,

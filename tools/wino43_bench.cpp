@@ -16,6 +16,9 @@ namespace sedx {
 void launch_conv3x3_wino43(const float* in, int B, int T, int F, int Cin, int Cout, const float* U43,
                            const float* bias, float* out, int epi, float* trash, hipStream_t s, int order, bool c4);
 void pack_conv_wino43(const double* wf, int Cin, int Cout, float* U);
+#ifdef SEDX_W43_STAMPS
+void w43_stamps_rw(unsigned long long* h, bool reset);
+#endif
 }
 
 struct Layer { const char* name; int B, T, F, cin, cout, epi; bool full; };
@@ -183,6 +186,18 @@ int main(int argc, char** argv) {
       };
       m2 = timeit(w2);
       m4 = timeit(w4);
+#ifdef SEDX_W43_STAMPS
+      sedx::w43_stamps_rw(nullptr, true);
+      w4c();
+      hipDeviceSynchronize();
+      unsigned long long st[8];
+      sedx::w43_stamps_rw(st, false);
+      const double waves = (double)st[5], items = (double)st[4];
+      printf("  stamps %s: per wave: item top %.0f, steps %.0f, epilogue %.0f, whole %.0f cycles; items/wave %.2f; "
+             "per item: top %.0f steps %.0f epilogue %.0f\n",
+             l.name, st[0] / waves, st[1] / waves, st[2] / waves, st[3] / waves, items / waves, st[0] / items,
+             st[1] / items, st[2] / items);
+#endif
       m4c = timeit(w4c);
       tot_2 += m2;
       tot_4 += m4;
