@@ -92,9 +92,10 @@ DTYPE = {'exact': 'f32',
 # separate conv1 launch, 2 computes conv1 inside the Winograd launch)
 WINO_BLOCK1 = 2
 WINO_MUL = 16.0 / 36.0
-# blocks 2-4 as Winograd F(4x4,3x3) (SEDX_TUNE_WINO_F43, the library default):
-# 36 multiplies per 4x4 output tile where the direct conv does 144
-WINO_F43 = 1
+# Winograd F(4x4,3x3) (SEDX_TUNE_WINO_F43): 36 multiplies per 4x4 output tile
+# where the direct conv does 144 — 1: blocks 2-4; 2 (the library default):
+# blocks 1-4, block 1 as a conv1 launch + the F(4x4,3x3) conv2
+WINO_F43 = 2
 WINO43_MUL = 36.0 / 144.0
 # SEDX_TUNE_GRU_KERNEL values (include/sedx.h)
 GRU_KERNELS = {'coop': 0, 'simple': 1, 'tag16': 2, 'tag8': 3, 'coop16': 4, 'auto': 5, 'ksplit': 6}
@@ -108,7 +109,7 @@ def wino_mul(stage):
     """Matrix-pipe multiplies of a winograd-mode stage per direct-conv multiply."""
     if stage not in wino_stages():
         return 1.0
-    return WINO43_MUL if (WINO_F43 and stage != 'b1c2') else WINO_MUL
+    return WINO43_MUL if (WINO_F43 and (stage != 'b1c2' or WINO_F43 == 2)) else WINO_MUL
 # conv stages of sedx_stage_times: (F, Cin, Cout, number of 2x poolings before it)
 CONV_STAGES = {'b1c2': (64, 64, 64, 0), 'b2c1': (32, 64, 128, 1), 'b2c2': (32, 128, 128, 1),
                'b3c1': (16, 128, 256, 2), 'b3c2': (16, 256, 256, 2), 'b4c1': (8, 256, 512, 3),
@@ -469,9 +470,9 @@ def conv_kernel_name(stage, precision):
     # winograd with F(4x4,3x3) and block 1 in one launch: the chunk-of-4
     # activation layout between them (the kernels' last template argument)
     c4 = 'true' if (WINO_F43 and WINO_BLOCK1 == 2) else 'false'
-    if precision == 'winograd' and stage == 'b1c2' and WINO_BLOCK1 == 2:
+    if precision == 'winograd' and stage == 'b1c2' and WINO_BLOCK1 == 2 and WINO_F43 != 2:
         return 'sedx::wino_block1_kernel<2, %s>' % c4
-    if precision == 'winograd' and stage in wino_stages() and WINO_F43 and stage != 'b1c2':
+    if precision == 'winograd' and stage in wino_stages() and wino_mul(stage) == WINO43_MUL:
         return 'sedx::conv3x3_wino43_kernel<%d, %d, %s>' % (F, epi, c4)
     if precision == 'winograd' and stage in wino_stages():
         # 2 tile groups x 64 channels (8 row waves) at the bench shapes
@@ -877,9 +878,9 @@ def main():
                     help='N > 1 process-group backend: nccl (= RCCL, the default with GPUs; rank r on GPU r) or '
                          'gloo (every rank on GPU 0, gathers through host copies: a rehearsal of the N-rank path '
                          'with the real model on a one-GPU box)')
-    ap.add_argument('--wino-f43', type=int, choices=[0, 1], default=None,
-                    help='SEDX_TUNE_WINO_F43 (A/B runs): blocks 2-4 as Winograd F(4x4,3x3) (1, the default) or '
-                         'F(2x2,3x3) (0)')
+    ap.add_argument('--wino-f43', type=int, choices=[0, 1, 2], default=None,
+                    help='SEDX_TUNE_WINO_F43 (A/B runs): blocks 1-4 (2, the default) or 2-4 (1) as Winograd '
+                         'F(4x4,3x3), or all F(2x2,3x3) (0)')
     ap.add_argument('--wino-block1', type=int, choices=[0, 1, 2], default=None,
                     help='winograd precision: block 1 as Winograd with conv1 inside the launch (2), fed by a '
                          'separate conv1 launch (1), or as the direct fused kernel (0); default: WINO_BLOCK1')

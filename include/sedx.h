@@ -234,9 +234,10 @@ sedx_status sedx_forward_windows_vote(sedx_handle* h, const float* d_audio, int6
  *                       arithmetic (pytorch/models.py:614-615, :663-670),
  *                       direct 3x3 convolution.
  *  SEDX_PRECISION_WINOGRAD (default)  fp32 throughout as EXACT, with block 1's conv2
- *                       (SEDX_TUNE_WINO_BLOCK1) computed by Winograd
- *                       F(2x2,3x3) and the six conv layers of blocks 2-4 by
- *                       F(4x4,3x3) (SEDX_TUNE_WINO_F43; 0: F(2x2,3x3)):
+ *                       (SEDX_TUNE_WINO_BLOCK1) and the six conv layers
+ *                       of blocks 2-4 computed by Winograd F(4x4,3x3)
+ *                       (SEDX_TUNE_WINO_F43; 1: block 1 by F(2x2,3x3), 0:
+ *                       every layer by F(2x2,3x3)):
  *                       input / weight / output transforms and the
  *                       element-wise GEMMs all in fp32 (weights transformed
  *                       in float64, rounded once), 2.25x / 4x fewer
@@ -300,6 +301,10 @@ sedx_status sedx_set_precision(sedx_handle* h, int32_t mode);
  *                         1: the same conv2 fed by a separate conv1 launch
  *                         (the activation through HBM; bit-identical to 2);
  *                         0: block 1 as the direct fused fp32 kernel.
+ *                         With SEDX_TUNE_WINO_F43 2 (its default) 1 and 2
+ *                         both run conv1's own launch + the F(4x4,3x3) conv2
+ *                         (2: conv1 in the chunk-of-4 layout, 1: NHWC;
+ *                         bit-identical).
  *  SEDX_TUNE_GRU_SPIN     bound of every GRU hand-off spin, in polls (default
  *                         2^24 = 16777216).  A spin that runs out turns that
  *                         forward's outputs into NaN and is reported by
@@ -317,10 +322,14 @@ sedx_status sedx_set_precision(sedx_handle* h, int32_t mode);
  *                         as 8 tile blocks x 4 channel groups of 64 (4 slabs
  *                         per round through the XCD's L2 instead of 8);
  *                         0: tile block major.  Bit-identical outputs.
- *  SEDX_TUNE_WINO_F43     (winograd) 1 (default): the six conv layers of
- *                         blocks 2-4 as fp32 Winograd F(4x4,3x3) (36
- *                         multiplies per 4x4 tile, v_mfma_f32_16x16x4_f32,
- *                         csrc/conv_wino43.hip); 0: F(2x2,3x3).  Different
+ *  SEDX_TUNE_WINO_F43     (winograd) 2 (default): block 1's conv2 and the
+ *                         six conv layers of blocks 2-4 as fp32 Winograd
+ *                         F(4x4,3x3) (36 multiplies per 4x4 tile,
+ *                         v_mfma_f32_16x16x4_f32, csrc/conv_wino43.hip),
+ *                         block 1 as a conv1 launch + that conv2 (conv1's
+ *                         activation in the workspace); 1: blocks 2-4 only
+ *                         (block 1 per SEDX_TUNE_WINO_BLOCK1 on F(2x2,3x3));
+ *                         0: every layer F(2x2,3x3).  Different
  *                         rounding (both fp32 throughout; F(4,3)'s error vs a
  *                         float64 conv is ~6x the direct conv's, still ~1e-5
  *                         of the 1e-3 bar), so not bit-identical to each other.

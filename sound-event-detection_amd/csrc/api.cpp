@@ -49,7 +49,7 @@ struct DevWeights {
   float* cb[8] = {};    // folded biases
   void* wx3[8] = {};    // split bf16 hi/lo packs for conv3x3_x3 (same indices)
   float* wu[8] = {};    // Winograd U = G g G^T packs for conv3x3_wino (same indices)
-  float* wu43[8] = {};  // F(4x4,3x3) U packs for conv3x3_wino43 (blocks 2-4: indices 2..7)
+  float* wu43[8] = {};  // F(4x4,3x3) U packs for conv3x3_wino43 (block 1's conv2: 1, blocks 2-4: 2..7)
   float* w_ih = nullptr;   // [1536][512]
   float* b_ih = nullptr;   // [1536]
   float* whhT = nullptr;   // [2][256][768]
@@ -96,7 +96,7 @@ struct sedx_handle {
   int mel_mfma = 0;                        // SEDX_TUNE_MEL_MFMA (measured slower: opt-in)
   unsigned gru_spin = 1u << 24;            // SEDX_TUNE_GRU_SPIN: bound of every GRU hand-off spin (polls)
   int wino_order = 1;                      // SEDX_TUNE_WINO_ORDER (4 x 8 rounds on the 512-channel layers)
-  int wino_f43 = 1;                        // SEDX_TUNE_WINO_F43 (blocks 2-4 as Winograd F(4x4,3x3))
+  int wino_f43 = 2;                        // SEDX_TUNE_WINO_F43 (2: blocks 1-4 as F(4x4,3x3), 1: blocks 2-4)
   int gamma_spec = 0;                      // SEDX_TUNE_GAMMA_SPEC
   // sedx_set_capture: copy one stage's output of every later forward
   int cap_stage = -1;
@@ -334,7 +334,8 @@ WsLayout ws_layout(const sedx_handle* h, int64_t B, const Geometry& g) {
   // modes: conv1's 64-channel activation never exists), then the conv1
   // outputs of blocks 2-4, then the head scratch
   size_t a = block1_pad_floats((int)B, (int)g.T);
-  if (wino_block1_on(h) && h->wino_block1 == 1) a = std::max(a, (size_t)B * g.T * 64 * 64);   // conv1's activation
+  if (wino_block1_on(h) && (h->wino_block1 == 1 || h->wino_f43 == 2))
+    a = std::max(a, (size_t)B * g.T * 64 * 64);   // conv1's activation
   a = std::max(a, (size_t)B * g.T1 * 32 * 128);
   a = std::max(a, (size_t)B * g.T2 * 16 * 256);
   a = std::max(a, (size_t)B * g.T3 * 8 * 512);
@@ -397,8 +398,13 @@ sedx_status run_body(sedx_handle* h, int64_t B, const Geometry& g, float* ws, co
   // activations in the chunk-of-4 layout [B][C/4][T][F][4] (dense halo DMA)
   const bool c4 = h->precision == SEDX_PRECISION_WINOGRAD && h->wino_f43 && wb1 && h->wino_block1 == 2;
   // Winograd block 1: 1 = conv1's activation [B][T][64][64] into A by its
-  // own launch; 2 = conv1 inside the Winograd launch (reads X0 itself)
-  if (wb1 && h->wino_block1 == 1)
+  // own launch; 2 = conv1 inside the Winograd launch (reads X0 itself).
+  // F(4x4,3x3) block 1 (wino_f43 2): conv1 by its own launch in both (2: in
+  // the chunk-of-4 layout), then the F(4x4,3x3) conv2
+  const bool b1_43 = wb1 && h->wino_f43 == 2;
+  if (b1_43 && c4)
+    launch_conv1_c4(X0, iB, (int)g.T, w.c1_w, w.c1_b, A, s);
+  else if (wb1 && (h->wino_block1 == 1 || b1_43))
     launch_conv1_nhwc(X0, iB, (int)g.T, w.c1_w, w.c1_b, A, s);
   else if (!wb1)
     launch_pad_x0(X0, iB, (int)g.T, A, s);
@@ -420,6 +426,9 @@ sedx_status run_body(sedx_handle* h, int64_t B, const Geometry& g, float* ws, co
     if (x3 && i == 0)
       launch_block1_fused_x3(nullptr, iB, c.T, A, w.c1_wt, w.c1_b, w.wx3[c.idx], w.cb[c.idx], c.out,
                              sched, s);
+    else if (i == 0 && b1_43)
+      launch_conv3x3_wino43(A, iB, c.T, 64, 64, 64, w.wu43[c.idx], w.cb[c.idx], c.out, EPI_POOL2, w.trash, s,
+                            h->wino_order, c4);
     else if (i == 0 && wb1 && h->wino_block1 == 2)
       launch_block1_wino(X0, iB, c.T, w.c1_w, w.c1_b, w.wu[c.idx], w.cb[c.idx], c.out, w.zero, w.trash, s, c4);
     else if (i == 0 && wb1)
@@ -686,7 +695,7 @@ sedx_status sedx_set_tuning(sedx_handle* h, int32_t knob, int32_t value) {
       h->gamma_spec = value;
       return SEDX_OK;
     case SEDX_TUNE_WINO_F43:
-      if (value != 0 && value != 1) break;
+      if (value < 0 || value > 2) break;
       h->wino_f43 = value;
       return SEDX_OK;
     default:
@@ -906,7 +915,7 @@ sedx_status sedx_finalize_weights(sedx_handle* h) {
           for (size_t k = 0; k < (size_t)cin * 9; ++k) wf[(size_t)o * cin * 9 + k] = wt[(size_t)o * cin * 9 + k] * sc[o];
         packed_wu[idx].assign((size_t)cin * cout * 16, 0.f);
         pack_conv_wino(wf.data(), cin, cout, packed_wu[idx].data());
-        if (k >= 2) {   // blocks 2-4: F(4x4,3x3) pack as well
+        {   // block 1's conv2 and blocks 2-4: the F(4x4,3x3) pack as well
           packed_wu43[idx].assign((size_t)cin * cout * 36, 0.f);
           pack_conv_wino43(wf.data(), cin, cout, packed_wu43[idx].data());
         }

@@ -1089,6 +1089,57 @@ void launch_conv1_nhwc(const float* x0, int B, int T, const float* w1, const flo
   hipLaunchKernelGGL(conv1_nhwc_kernel, dim3((unsigned)blocks), dim3(256), 0, s, x0, T, rb, w1, b1, out);
 }
 
+// Block 1's conv1 into the chunk-of-4 layout [B][16][T][64][4] (the F(4x4,3x3)
+// block-1 conv2's input, conv_wino43.hip): a workgroup computes C1_ROWS
+// t-rows of one clip for all 16 chunks, a thread one pixel x 4 channels per
+// chunk (consecutive threads: consecutive bins, one 16-byte store each, so a
+// chunk's rows are one contiguous run).  Per channel the same fma chain as
+// conv1_nhwc_kernel: the two layouts hold bit-identical values.
+__global__ __launch_bounds__(256) void conv1_c4_kernel(const float* __restrict__ x0, int T, int rb_per_clip,
+                                                       const float* __restrict__ w1, const float* __restrict__ b1,
+                                                       float* __restrict__ out) {
+  __shared__ float s_w[64 * 9], s_b[64];
+  __shared__ float s_x[C1_ROWS + 2][66];
+  const int b = blockIdx.x / rb_per_clip;
+  const int t0 = (blockIdx.x - b * rb_per_clip) * C1_ROWS;
+  for (int i = threadIdx.x; i < 64 * 9; i += 256) s_w[i] = w1[i];
+  if (threadIdx.x < 64) s_b[threadIdx.x] = b1[threadIdx.x];
+  const float* xb = x0 + (int64_t)b * T * 64;
+  for (int i = threadIdx.x; i < (C1_ROWS + 2) * 66; i += 256) {
+    const int r = i / 66, c = i - r * 66;
+    const int t = t0 - 1 + r, f = c - 1;
+    s_x[r][c] = (t >= 0 && t < T && f >= 0 && f < 64) ? xb[t * 64 + f] : 0.0f;
+  }
+  __syncthreads();
+  static_assert(C1_ROWS * 64 == 256, "a thread per pixel");
+  const int r = threadIdx.x >> 6, f = threadIdx.x & 63;
+  if (t0 + r >= T) return;
+  float xv[9];
+#pragma unroll
+  for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+    for (int dx = 0; dx < 3; ++dx) xv[dy * 3 + dx] = s_x[r + dy][f + dx];
+  float* ob = out + (((int64_t)b * 16 * T + t0 + r) * 64 + f) * 4;
+  for (int cc = 0; cc < 16; ++cc) {
+    float y[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      float acc = 0.0f;
+#pragma unroll
+      for (int k = 0; k < 9; ++k) acc = fmaf(xv[k], s_w[(4 * cc + c) * 9 + k], acc);
+      y[c] = fmaxf(acc + s_b[4 * cc + c], 0.0f);
+    }
+    *reinterpret_cast<float4*>(ob + (int64_t)cc * T * 256) = make_float4(y[0], y[1], y[2], y[3]);
+  }
+}
+
+void launch_conv1_c4(const float* x0, int B, int T, const float* w1, const float* b1, float* out, hipStream_t s) {
+  const int rb = (T + C1_ROWS - 1) / C1_ROWS;
+  const int64_t blocks = (int64_t)B * rb;
+  if (B <= 0 || T <= 0 || blocks > INT32_MAX || (int64_t)T * 64 > INT32_MAX) return note_launch_error(hipErrorInvalidValue);
+  hipLaunchKernelGGL(conv1_c4_kernel, dim3((unsigned)blocks), dim3(256), 0, s, x0, T, rb, w1, b1, out);
+}
+
 #ifdef SEDX_WINO_STAMPS
 // diagnostic builds: the stamp sums (host side, this translation unit)
 void wino_stamps_rw(unsigned long long* h, bool reset) {

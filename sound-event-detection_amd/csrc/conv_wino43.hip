@@ -94,13 +94,14 @@ struct W43Geom {
   static constexpr int FT = F / 4;                   // tiles per tile row
   static constexpr int TRW = TILES / FT;             // tile rows per item
   // a tile group is TRG tile rows x TFG tile columns (lane n = tr TFG + tf)
-  static constexpr int TFG = F == 8 ? 2 : 4;
+  static constexpr int TFG = F == 8 ? 2 : F == 64 ? 16 : 4;
   static constexpr int TRG = 16 / TFG;
   static constexpr int RT = 4 * TRW + 2, CS = F + 2; // halo rows / columns
   // halo row stride: (4 tr RS + 4 tf) / 2 over the 16 tiles of a group must
   // take the 16 even values mod 32 (b64 bank pairs): 2 RS = 8 (mod 32) for
   // 4 x 4 groups, 2 RS = 20 (mod 32) for 8 x 2
-  static constexpr int RS = F == 32 ? 36 : F == 16 ? 20 : 10;
+  // (F = 64, block 1: one tile row of 16 per group, 2 tf = 0, 2, .., 30 for any even RS)
+  static constexpr int RS = F == 64 ? 66 : F == 32 ? 36 : F == 16 ? 20 : 10;
   // a plane's halo in 64-dword DMA blocks, one per wave 0..HB-1 (RT RS <= 704
   // for every F); wave 11 issues its four halo DMAs into an LDS trash block,
   // so every wave has the same DMA count per step
@@ -117,7 +118,7 @@ struct W43Geom {
   static constexpr int LDS_BYTES = 4 * (HTRASH_OFF + 64);
   static constexpr int VM = 7;                       // DMAs per wave per step (3 U units + 4 halo planes)
 
-  static_assert(F == 32 || F == 16 || F == 8, "F");
+  static_assert(F == 64 || F == 32 || F == 16 || F == 8, "F");
   static_assert(RT * RS <= 64 * HB, "halo plane fits its DMA blocks");
   static_assert(HB == WAVES - 1, "wave 11: trash halo block");
   static_assert(36 % WAVES == 0, "U units per wave");
@@ -226,7 +227,7 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
   if (!decode(item, b, t0, grp)) return;   // uniform
 
   // this lane's tile within the item
-  const int tr = (F == 16 ? 4 * tg : F == 8 ? 8 * tg : 0) + nn / G::TFG;
+  const int tr = (F == 16 ? 4 * tg : F == 8 ? 8 * tg : F == 64 ? tg : 0) + nn / G::TFG;
   const int tf = (F == 32 ? 4 * tg : 0) + nn % G::TFG;
 
   // ---- DMA sources.  Buffer resources: the input (pixels outside the clip
@@ -776,7 +777,9 @@ static void launch_w43_f(const float* in, int B, int T, int Cin, int Cout, const
                        (int)u_bytes, bias, out, trash, tb_per_clip, ngroups, order2d);                     \
     return;                                                                                                \
   }
-  if constexpr (F == 8) {
+  if constexpr (F == 64) {   // block 1's conv2 (conv1's output in, 2 x 2 pool)
+    if (epi == EPI_POOL2) SEDX_W43_LAUNCH(EPI_POOL2);
+  } else if constexpr (F == 8) {
     if (epi == EPI_STORE) SEDX_W43_LAUNCH(EPI_STORE);
     if (epi == EPI_FMEAN) SEDX_W43_LAUNCH(EPI_FMEAN);
   } else {
@@ -803,6 +806,7 @@ void launch_conv3x3_wino43(const float* in, int B, int T, int F, int Cin, int Co
     const float* in_s = in + b0 * in_clip;
     float* out_s = out + b0 * out_clip;
     switch (F) {
+      case 64: launch_w43_f<64>(in_s, bs, T, Cin, Cout, U43, bias, out_s, epi, trash, order, c4, s); break;
       case 32: launch_w43_f<32>(in_s, bs, T, Cin, Cout, U43, bias, out_s, epi, trash, order, c4, s); break;
       case 16: launch_w43_f<16>(in_s, bs, T, Cin, Cout, U43, bias, out_s, epi, trash, order, c4, s); break;
       case 8: launch_w43_f<8>(in_s, bs, T, Cin, Cout, U43, bias, out_s, epi, trash, order, c4, s); break;

@@ -152,6 +152,8 @@ void launch_block1_wino(const float* x0, int B, int T, const float* w1, const fl
 // block 1's conv1 + BN + ReLU: X0 [B][T][64] -> [B][T][64][64] (w1 [64][9] folded, b1 [64])
 void launch_conv1_nhwc(const float* x0, int B, int T, const float* w1, const float* b1, float* out,
                        hipStream_t s);
+// the same conv1 into the chunk-of-4 layout [B][16][T][64][4] (conv_wino.hip)
+void launch_conv1_c4(const float* x0, int B, int T, const float* w1, const float* b1, float* out, hipStream_t s);
 
 // Same contract on bf16 MFMA with a 3-term hi/lo split (fp32-class accuracy).
 // wp = host-packed split weights [Cout/BN][Cin/16][9][BN][4 x 16 B] (BN = 64 if

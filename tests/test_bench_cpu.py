@@ -64,18 +64,24 @@ def test_cpu_info(bench):
 
 
 def test_roofline_winograd_block1(bench):
-    """Winograd mode: b1c2 is a Winograd launch (executed FLOPs 16/36 of the
-    direct conv2) — by default with conv1 computed inside it on the VALU
-    (--wino-block1 2: not priced on the matrix pipe), or fed by its own b1c1
-    launch (1); with --wino-block1 0 it is the direct fused launch again."""
+    """Winograd mode: b1c2 is a Winograd launch — by default (--wino-f43 2)
+    the F(4x4,3x3) conv2 (36/144 of the direct conv2) fed by its own b1c1
+    conv1 launch in the chunk-of-4 layout; with --wino-f43 1 the F(2x2,3x3)
+    launch (16/36) with conv1 computed inside it on the VALU (--wino-block1
+    2: not priced on the matrix pipe) or fed by its own launch (1); with
+    --wino-block1 0 the direct fused launch."""
     stage = {s: 0.2 for s in bench.CONV_STAGES}
     stage['b1c2'] = 1.0
     stage['b1c1'] = 0.1
-    assert bench.WINO_BLOCK1 == 2
+    assert bench.WINO_BLOCK1 == 2 and bench.WINO_F43 == 2
     w = bench.roofline(stage, 32, 'winograd')
-    assert w['kernel'] == 'sedx::wino_block1_kernel<2, true> (b1c2)'
-    assert w['flops_per_launch'] == bench.conv_flops('b1c2', 32, 1001) * 16.0 / 36.0
+    assert w['kernel'] == 'sedx::conv3x3_wino43_kernel<64, 1, true> (b1c2)'
+    assert w['flops_per_launch'] == bench.conv_flops('b1c2', 32, 1001) * 36.0 / 144.0
     try:
+        bench.WINO_F43 = 1
+        w = bench.roofline(stage, 32, 'winograd')
+        assert w['kernel'] == 'sedx::wino_block1_kernel<2, true> (b1c2)'
+        assert w['flops_per_launch'] == bench.conv_flops('b1c2', 32, 1001) * 16.0 / 36.0
         bench.WINO_BLOCK1 = 1
         w = bench.roofline(stage, 32, 'winograd')
         assert w['kernel'] == 'sedx::conv3x3_wino_kernel<64, 1, 2, 2> (b1c2)'
@@ -84,31 +90,40 @@ def test_roofline_winograd_block1(bench):
         d = bench.roofline(stage, 32, 'winograd')
         assert d['kernel'].startswith('sedx::conv3x3_kernel<64, 64, 1, true')
         assert d['flops_per_launch'] == bench.conv_flops('b1c2', 32, 1001) + 2.0 * 32 * 1001 * 64 * 64 * 9
+        bench.WINO_F43 = 2
+        bench.WINO_BLOCK1 = 1
+        w = bench.roofline(stage, 32, 'winograd')
+        assert w['kernel'] == 'sedx::conv3x3_wino43_kernel<64, 1, false> (b1c2)'
     finally:
         bench.WINO_BLOCK1 = 2
+        bench.WINO_F43 = 2
 
 
 def test_roofline_winograd_f43(bench):
-    """Blocks 2-4 as Winograd F(4x4,3x3) (the default): their launches are
+    """Blocks 1-4 as Winograd F(4x4,3x3) (the default): their launches are
     conv3x3_wino43_kernel<F, EPI> and execute 36/144 of the direct conv's
-    multiplies; with --wino-f43 0 they are the F(2x2,3x3) row-wave kernels
-    (16/36); block 1 stays F(2x2,3x3) either way."""
+    multiplies; --wino-f43 1 keeps block 1 on F(2x2,3x3); with --wino-f43 0
+    every layer is an F(2x2,3x3) kernel (16/36)."""
     stage = {s: 0.1 for s in bench.CONV_STAGES}
     stage['b4c2'] = 1.0
-    assert bench.WINO_F43 == 1
+    assert bench.WINO_F43 == 2
     w = bench.roofline(stage, 32, 'winograd')
     assert w['kernel'] == 'sedx::conv3x3_wino43_kernel<8, 2, true> (b4c2)'
     assert w['flops_per_launch'] == bench.conv_flops('b4c2', 32, 1001) * 36.0 / 144.0
-    assert 'F(4x4,3x3)' in w['arith'] and 'b1c2 F(2x2,3x3)' in w['arith']
+    assert 'b1c2 F(4x4,3x3)' in w['arith'] and 'F(2x2,3x3)' not in w['arith']
     assert bench.conv_kernel_name('b2c2', 'winograd') == 'sedx::conv3x3_wino43_kernel<32, 1, true>'
-    assert bench.conv_kernel_name('b1c2', 'winograd') == 'sedx::wino_block1_kernel<2, true>'
+    assert bench.conv_kernel_name('b1c2', 'winograd') == 'sedx::conv3x3_wino43_kernel<64, 1, true>'
     try:
+        bench.WINO_F43 = 1
+        w = bench.roofline(stage, 32, 'winograd')
+        assert 'b1c2 F(2x2,3x3)' in w['arith']
+        assert bench.conv_kernel_name('b1c2', 'winograd') == 'sedx::wino_block1_kernel<2, true>'
         bench.WINO_F43 = 0
         w = bench.roofline(stage, 32, 'winograd')
         assert w['kernel'] == 'sedx::conv3x3_wino_kernel<8, 2, 2, 2> (b4c2)'
         assert w['flops_per_launch'] == bench.conv_flops('b4c2', 32, 1001) * 16.0 / 36.0
     finally:
-        bench.WINO_F43 = 1
+        bench.WINO_F43 = 2
 
 
 def test_roofline_fracs_are_fractions(bench):

@@ -776,19 +776,24 @@ def test_wino_block1_knob_errors():
     assert L.sedx_set_tuning(nat.h, _lib.TUNE_WINO_BLOCK1, 1) == 0
 
 
+@pytest.mark.parametrize('f43', [1, 2])
 @pytest.mark.parametrize('B,seconds', [(32, 10.0), (3, 7.33), (1, 2.0), (5, 0.33)])
-def test_wino_block1_conv1_fused_bit_identical(B, seconds):
-    """Block 1 with conv1 computed inside the Winograd launch (2) against the
-    separate conv1 launch (1): the same fma chain per channel, the same
-    conv2 — every block-1 output and the framewise output bit for bit equal,
-    at the headline batch, an odd length (partial last tile block, odd last
-    row dropped by the pool), one short clip and clips of a few frames."""
+def test_wino_block1_conv1_fused_bit_identical(B, seconds, f43):
+    """F(2x2,3x3) block 1 (SEDX_TUNE_WINO_F43 1): conv1 computed inside the
+    Winograd launch (WINO_BLOCK1 2) against the separate conv1 launch (1) —
+    the same fma chain per channel, the same conv2.  F(4x4,3x3) block 1 (2,
+    the default): conv1's launch into the chunk-of-4 layout + the C4 conv2
+    (2) against the NHWC pair (1).  Every block-1 output and the framewise
+    output bit for bit equal, at the headline batch, an odd length (partial
+    last tile block, odd last row dropped by the pool), one short clip and
+    clips of a few frames."""
     from sedx import _lib
     wave = synth.make_waveforms(B, seconds=seconds, sample_rate=16000, seed=31 + B)
     T = wave.shape[1] // 160 + 1                  # frames (hop 160, centred STFT)
     outs = []
     for v in (1, 2):
-        m = build(GRU).set_precision('winograd').set_tuning(_lib.TUNE_WINO_BLOCK1, v)
+        m = build(GRU).set_precision('winograd').set_tuning(_lib.TUNE_WINO_F43, f43)
+        m.set_tuning(_lib.TUNE_WINO_BLOCK1, v)
         b1 = _capture(m, 2, (B, T // 2, 32, 64), wave)
         assert not np.isnan(b1).any()
         outs.append((b1, run(m, wave)['framewise_output']))

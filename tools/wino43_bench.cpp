@@ -28,7 +28,8 @@ int main(int argc, char** argv) {
   const int reps = argc > 2 ? atoi(argv[2]) : 20;
   const char* only = argc > 3 ? argv[3] : nullptr;
   const int order = getenv("W43_ORDER") ? atoi(getenv("W43_ORDER")) : 1;
-  std::vector<Layer> LM = {{"b2c1", B, 500, 32, 64, 128, sedx::EPI_STORE, false},
+  std::vector<Layer> LM = {{"b1c2", B, 1001, 64, 64, 64, sedx::EPI_POOL2, false},
+                           {"b2c1", B, 500, 32, 64, 128, sedx::EPI_STORE, false},
                            {"b2c2", B, 500, 32, 128, 128, sedx::EPI_POOL2, false},
                            {"b3c1", B, 250, 16, 128, 256, sedx::EPI_STORE, false},
                            {"b3c2", B, 250, 16, 256, 256, sedx::EPI_POOL2, false},
@@ -40,7 +41,8 @@ int main(int argc, char** argv) {
                            {"e16p", 3, 9, 16, 64, 128, sedx::EPI_POOL2, true},
                            {"e16s", 1, 70, 16, 32, 64, sedx::EPI_STORE, true},
                            {"e8m", 2, 67, 8, 64, 192, sedx::EPI_FMEAN, true},
-                           {"e8s", 5, 3, 8, 16, 64, sedx::EPI_STORE, true}};
+                           {"e8s", 5, 3, 8, 16, 64, sedx::EPI_STORE, true},
+                           {"e64p", 2, 37, 64, 64, 64, sedx::EPI_POOL2, true}};
   float *d_in, *d_in4, *d_o1, *d_o2, *d_o3, *d_bias, *d_u, *d_u43, *d_zero, *d_trash;
   size_t max_in = 0, max_out = 0, max_w = 0;
   for (const Layer& l : LM) {
@@ -211,6 +213,66 @@ int main(int argc, char** argv) {
            m4c > 0 ? m2 / m4c : 0.0, e2max, e4max, std::sqrt(e4sq / std::max<size_t>(1, nchk)), omax, nchk, nan,
            c4diff, lok ? "OK" : "MISMATCH");
     fflush(stdout);
+  }
+  // block 1 as the library runs it: the fused F(2,3) launch against conv1
+  // (chunk-of-4 layout) + the F(4,3) conv2; conv1's two layouts bit-identical
+  if (!only || strcmp(only, "block1") == 0) {
+    const int T = 1001;
+    const size_t nx = (size_t)B * T * 64, na = nx * 64, no = (size_t)B * (T / 2) * 32 * 64;
+    std::vector<float> x0(nx), w1(64 * 9), b1(64), bias(64);
+    for (auto& v : x0) v = nd(rng);
+    for (auto& v : w1) v = 0.3f * nd(rng);
+    for (auto& v : b1) v = 0.1f * nd(rng);
+    for (auto& v : bias) v = 0.1f * nd(rng);
+    std::vector<double> w((size_t)64 * 64 * 9);
+    for (auto& v : w) v = (double)(float)(nd(rng) * std::sqrt(2.f / 576));
+    std::vector<float> U((size_t)64 * 64 * 16), U43((size_t)64 * 64 * 36);
+    sedx::pack_conv_wino(w.data(), 64, 64, U.data());
+    sedx::pack_conv_wino43(w.data(), 64, 64, U43.data());
+    float *d_x0, *d_w1, *d_b1, *d_a, *d_a4, *d_ob;
+    hipMalloc(&d_x0, nx * 4); hipMalloc(&d_w1, 64 * 9 * 4); hipMalloc(&d_b1, 64 * 4);
+    hipMalloc(&d_a, na * 4); hipMalloc(&d_a4, na * 4); hipMalloc(&d_ob, no * 4);
+    hipMemcpy(d_x0, x0.data(), nx * 4, hipMemcpyHostToDevice);
+    hipMemcpy(d_w1, w1.data(), w1.size() * 4, hipMemcpyHostToDevice);
+    hipMemcpy(d_b1, b1.data(), b1.size() * 4, hipMemcpyHostToDevice);
+    hipMemcpy(d_bias, bias.data(), 64 * 4, hipMemcpyHostToDevice);
+    hipMemcpy(d_u, U.data(), U.size() * 4, hipMemcpyHostToDevice);
+    hipMemcpy(d_u43, U43.data(), U43.size() * 4, hipMemcpyHostToDevice);
+    sedx::launch_conv1_nhwc(d_x0, B, T, d_w1, d_b1, d_a, 0);
+    sedx::launch_conv1_c4(d_x0, B, T, d_w1, d_b1, d_a4, 0);
+    hipDeviceSynchronize();
+    std::vector<float> a(na), a4(na);
+    hipMemcpy(a.data(), d_a, na * 4, hipMemcpyDeviceToHost);
+    hipMemcpy(a4.data(), d_a4, na * 4, hipMemcpyDeviceToHost);
+    size_t ndiff = 0;
+    for (int b = 0; b < B; ++b)
+      for (int t = 0; t < T; ++t)
+        for (int f = 0; f < 64; ++f)
+          for (int c = 0; c < 64; ++c)
+            ndiff += std::memcmp(&a[(((size_t)b * T + t) * 64 + f) * 64 + c],
+                                 &a4[((((size_t)b * 16 + c / 4) * T + t) * 64 + f) * 4 + c % 4], 4) != 0;
+    ok = ok && ndiff == 0;
+    auto timeit = [&](auto fn) {
+      fn();
+      hipEventRecord(e0, 0);
+      for (int r = 0; r < reps; ++r) fn();
+      hipEventRecord(e1, 0);
+      hipEventSynchronize(e1);
+      float ms = 0;
+      hipEventElapsedTime(&ms, e0, e1);
+      return ms / reps;
+    };
+    const float m_f23 = timeit([&]() {
+      sedx::launch_block1_wino(d_x0, B, T, d_w1, d_b1, d_u, d_bias, d_ob, d_zero, d_trash, 0, true);
+    });
+    const float m_c1 = timeit([&]() { sedx::launch_conv1_c4(d_x0, B, T, d_w1, d_b1, d_a4, 0); });
+    const float m_c2 = timeit([&]() {
+      sedx::launch_conv3x3_wino43(d_a4, B, T, 64, 64, 64, d_u43, d_bias, d_ob, sedx::EPI_POOL2, d_trash, 0, order, true);
+    });
+    printf("block1 B=%d T=%d  fused F(2,3) %.4f ms  conv1_c4 %.4f + F(4,3) conv2 %.4f = %.4f ms  (x%.2f)  "
+           "conv1 c4 vs nhwc differing %zu\n",
+           B, T, m_f23, m_c1, m_c2, m_c1 + m_c2, m_f23 / (m_c1 + m_c2), ndiff);
+    hipFree(d_x0); hipFree(d_w1); hipFree(d_b1); hipFree(d_a); hipFree(d_a4); hipFree(d_ob);
   }
   printf("total F(2,3) %.4f ms  F(4,3) nhwc %.4f ms  c4 %.4f ms  (x%.2f)  %s  (err=%s, launch=%s)\n", tot_2, tot_4,
          tot_4c, tot_4c > 0 ? tot_2 / tot_4c : 0.0, ok ? "ALL OK" : "MISMATCH", hipGetErrorString(hipGetLastError()),
