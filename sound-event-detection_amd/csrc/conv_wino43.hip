@@ -66,7 +66,8 @@ typedef float w43_f32x4 __attribute__((ext_vector_type(4)));
 
 // Ablation builds (tools/wino43_bench.cpp only, results WRONG, timing only):
 // SEDX_W43_ABL bit 1 drops the halo DMAs, 2 the U DMAs, 4 the epilogue's
-// exchange and output transform (stores kept), 8 the epilogue's barriers
+// exchange and output transform (stores kept), 8 the epilogue's barriers,
+// 16 the STORE epilogue's scatter (every store to one coalesced 1 KiB run)
 #ifndef SEDX_W43_ABL
 #define SEDX_W43_ABL 0
 #endif
@@ -110,9 +111,11 @@ struct W43Geom {
   static constexpr int HALO = 4 * PS;                // dwords per halo slot
   static constexpr int USZ = 36 * 4 * NCH;           // dwords per U slot ([p][k][m][nt])
   static constexpr int NB = 3;                       // ring depth (U and halo)
-  // epilogue exchange per round: [row 6][reg 2][b pair 2][lane 64][2] per tile
-  // group, in the U slot freed by the item's last step
-  static constexpr int XTG = 6 * 2 * 2 * 128;
+  // epilogue exchange per round: [row 6][reg 2][kc 4][16 tiles + 1 pad][4 z]
+  // per tile group, in the U slot freed by the item's last step (the pad:
+  // a STORE finisher's reads of 4 kc x 16 (tile, column) words hit 64 banks)
+  static constexpr int XRS = 4 * 68;
+  static constexpr int XTG = 6 * 2 * XRS;
   static constexpr int U_OFF = 0, H_OFF = NB * USZ, BIAS_OFF = H_OFF + NB * HALO, BIAS_MAX = 512;
   static constexpr int HTRASH_OFF = BIAS_OFF + BIAS_MAX;   // 64 dwords: wave 11's halo DMAs
   static constexpr int LDS_BYTES = 4 * (HTRASH_OFF + 64);
@@ -545,11 +548,13 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
     // every wave's reads of it are done at the first barrier below. ----
     float* const xfree = smem + G::U_OFF + (us == 0 ? 2 : us - 1) * G::USZ;
     float* const xbuf0 = xfree + tg * G::XTG;
-    auto xs = [&](int row, int s, int bp) { return ((row * 2 + s) * 2 + bp) * 128 + 2 * lane; };
     // output element base of the item: first output row t0 of clip b
     int le = lane;
     asm volatile("" : "+v"(le));   // opaque: offsets computed here, not hoisted as live registers
     const int kc = le >> 4;
+    // z of (row, register s) of lane (kc', tile n'): 4 words at xs(row, s) + 68 kc' + 4 n'
+    auto xs = [&](int row, int s) { return (row * 2 + s) * G::XRS; };
+    const int xl = 68 * kc + 4 * (le & 15);   // this lane's entry
     const int trg = t0 / 4 + tr;   // the lane's tile row in the clip
     w43_f32x4 ost[4];              // POOL2 / FMEAN: one 4-channel group per channel tile
     w43_f32x4 ost2[4];             // STORE: the 2 x 2 pixels of the current channel tile
@@ -603,8 +608,7 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
 #pragma unroll
         for (int j = 0; j < 6; ++j) m[j] = acc[j][nt][r];
         w43_at(m, z);
-        *reinterpret_cast<float2*>(xb + xs(ROW, s, 0)) = make_float2(z[0], z[1]);
-        *reinterpret_cast<float2*>(xb + xs(ROW, s, 1)) = make_float2(z[2], z[3]);
+        *reinterpret_cast<float4*>(xb + xs(ROW, s) + xl) = make_float4(z[0], z[1], z[2], z[3]);
       }
       if constexpr (!(SEDX_W43_ABL & 8)) w43_lds_bar();
       if constexpr (ROW < 4) {
@@ -619,9 +623,8 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
             float z[6][4];
 #pragma unroll
             for (int i = 0; i < 6; ++i) {
-              const float2 lo = *reinterpret_cast<const float2*>(xb + xs(i, s, 0));
-              const float2 hi = *reinterpret_cast<const float2*>(xb + xs(i, s, 1));
-              z[i][0] = lo.x; z[i][1] = lo.y; z[i][2] = hi.x; z[i][3] = hi.y;
+              const float4 v = *reinterpret_cast<const float4*>(xb + xs(i, s) + xl);
+              z[i][0] = v.x; z[i][1] = v.y; z[i][2] = v.z; z[i][3] = v.w;
             }
             float sum = 0.0f;
 #pragma unroll
@@ -634,13 +637,28 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
             }
             const float other = __shfl_xor(sum, 1);
             ost[nt][r] = ((tf & 1) ? other + sum : sum + other) * (1.0f / F);
+          } else if constexpr (EPI == EPI_STORE) {
+            // output row a = ROW; for store j the lane computes column
+            // c = lane & 3 of tile (lane & 12) | j — another lane's z — so the
+            // 4 lanes of a quad hold one tile row's 4 pixels (64 contiguous
+            // bytes of a 4-channel group) per store instruction
+            const int c = le & 3;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const float* src = xb + 68 * kc + 4 * ((le & 12) | j) + c;
+              float col[6], yy[4];
+#pragma unroll
+              for (int i = 0; i < 6; ++i) col[i] = src[xs(i, s)];
+              w43_at(col, yy);
+              ost2[j][r] = fmaxf(yy[ROW] + bv, 0.0f);
+            }
           } else {
-            // the 2 x 2 block (2A, 2A + 1) x (2B, 2B + 1) of the tile
+            // POOL2: the 2 x 2 block (2A, 2A + 1) x (2B, 2B + 1) of the tile
             constexpr int A = ROW >> 1, Bc = ROW & 1;
             float z[6][2];
 #pragma unroll
             for (int i = 0; i < 6; ++i) {
-              const float2 w = *reinterpret_cast<const float2*>(xb + xs(i, s, Bc));
+              const float2 w = *reinterpret_cast<const float2*>(xb + xs(i, s) + xl + 2 * Bc);
               z[i][0] = w.x;
               z[i][1] = w.y;
             }
@@ -654,27 +672,20 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
               y[0][c] = fmaxf(yy[2 * A] + bv, 0.0f);
               y[1][c] = fmaxf(yy[2 * A + 1] + bv, 0.0f);
             }
-            if constexpr (EPI == EPI_POOL2) {
-              ost[nt][r] = (((y[0][0] + y[0][1]) + y[1][0]) + y[1][1]) * 0.25f;
-            } else {
-#pragma unroll
-              for (int a = 0; a < 2; ++a)
-#pragma unroll
-                for (int c = 0; c < 2; ++c) ost2[2 * a + c][r] = y[a][c];
-            }
+            ost[nt][r] = (((y[0][0] + y[0][1]) + y[1][0]) + y[1][1]) * 0.25f;
           }
         }
         if constexpr (EPI == EPI_STORE) {
-          if (q & 1) {   // the channel tile's 4 registers done: 4 pixels x 4 channels
+          if (q & 1) {   // the channel tile's 4 registers done: 4 tiles' pixels x 4 channels
 #pragma unroll
-            for (int a = 0; a < 2; ++a) {
-              const int t = 4 * trg + 2 * (ROW >> 1) + a;
-#pragma unroll
-              for (int c = 0; c < 2; ++c) {
-                const int f = 4 * tf + 2 * (ROW & 1) + c;
-                float* dst = t < T ? opix(t, f, n, T, F) : tr_lane;
-                *reinterpret_cast<w43_f32x4*>(dst) = ost2[2 * a + c];
-              }
+            for (int j = 0; j < 4; ++j) {
+              const int tj = (le & 12) | j;   // the tile of store j
+              const int trj = (F == 16 ? 4 * tg : F == 8 ? 8 * tg : F == 64 ? tg : 0) + tj / G::TFG;
+              const int tfj = (F == 32 ? 4 * tg : 0) + tj % G::TFG;
+              const int t = 4 * (t0 / 4 + trj) + ROW, f = 4 * tfj + (le & 3);
+              float* dst = t < T ? opix(t, f, n, T, F) : tr_lane;
+              if constexpr (SEDX_W43_ABL & 16) dst = tr_lane;   // timing: fully coalesced stores
+              *reinterpret_cast<w43_f32x4*>(dst) = ost2[j];
             }
           }
         } else {   // POOL2 / FMEAN: the channel tile's 4 registers done: one 4-channel group
