@@ -111,9 +111,11 @@ struct W43Geom {
   static constexpr int HALO = 4 * PS;                // dwords per halo slot
   static constexpr int USZ = 36 * 4 * NCH;           // dwords per U slot ([p][k][m][nt])
   static constexpr int NB = 3;                       // ring depth (U and halo)
-  // epilogue exchange per round: [row 6][reg 2][kc 4][16 tiles + 1 pad][4 z]
-  // per tile group, in the U slot freed by the item's last step (the pad:
-  // a STORE finisher's reads of 4 kc x 16 (tile, column) words hit 64 banks)
+  // epilogue exchange per round, per tile group, in the U slot freed by the
+  // item's last step: STORE [row 6][reg 2][kc 4][16 tiles + 1 pad][4 z] (the
+  // pad: a finisher's reads of 4 kc x 16 (tile, column) words hit 64
+  // banks), else [row 6][reg 2][z pair 2][lane 64][2] (a finisher's
+  // ds_read_b64 of its own pair: conflict-free)
   static constexpr int XRS = 4 * 68;
   static constexpr int XTG = 6 * 2 * XRS;
   static constexpr int U_OFF = 0, H_OFF = NB * USZ, BIAS_OFF = H_OFF + NB * HALO, BIAS_MAX = 512;
@@ -552,9 +554,11 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
     int le = lane;
     asm volatile("" : "+v"(le));   // opaque: offsets computed here, not hoisted as live registers
     const int kc = le >> 4;
-    // z of (row, register s) of lane (kc', tile n'): 4 words at xs(row, s) + 68 kc' + 4 n'
+    // STORE: z of (row, register s) of lane (kc', tile n') = 4 words at
+    // xs(row, s) + 68 kc' + 4 n'; else pair bp of this lane at xp(row, s, bp)
     auto xs = [&](int row, int s) { return (row * 2 + s) * G::XRS; };
-    const int xl = 68 * kc + 4 * (le & 15);   // this lane's entry
+    const int xl = 68 * kc + 4 * (le & 15);   // this lane's STORE entry
+    auto xp = [&](int row, int s, int bp) { return ((row * 2 + s) * 2 + bp) * 128 + 2 * le; };
     const int trg = t0 / 4 + tr;   // the lane's tile row in the clip
     w43_f32x4 ost[4];              // POOL2 / FMEAN: one 4-channel group per channel tile
     w43_f32x4 ost2[4];             // STORE: the 2 x 2 pixels of the current channel tile
@@ -608,7 +612,12 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
 #pragma unroll
         for (int j = 0; j < 6; ++j) m[j] = acc[j][nt][r];
         w43_at(m, z);
-        *reinterpret_cast<float4*>(xb + xs(ROW, s) + xl) = make_float4(z[0], z[1], z[2], z[3]);
+        if constexpr (EPI == EPI_STORE) {
+          *reinterpret_cast<float4*>(xb + xs(ROW, s) + xl) = make_float4(z[0], z[1], z[2], z[3]);
+        } else {
+          *reinterpret_cast<float2*>(xb + xp(ROW, s, 0)) = make_float2(z[0], z[1]);
+          *reinterpret_cast<float2*>(xb + xp(ROW, s, 1)) = make_float2(z[2], z[3]);
+        }
       }
       if constexpr (!(SEDX_W43_ABL & 8)) w43_lds_bar();
       if constexpr (ROW < 4) {
@@ -623,8 +632,9 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
             float z[6][4];
 #pragma unroll
             for (int i = 0; i < 6; ++i) {
-              const float4 v = *reinterpret_cast<const float4*>(xb + xs(i, s) + xl);
-              z[i][0] = v.x; z[i][1] = v.y; z[i][2] = v.z; z[i][3] = v.w;
+              const float2 lo = *reinterpret_cast<const float2*>(xb + xp(i, s, 0));
+              const float2 hi = *reinterpret_cast<const float2*>(xb + xp(i, s, 1));
+              z[i][0] = lo.x; z[i][1] = lo.y; z[i][2] = hi.x; z[i][3] = hi.y;
             }
             float sum = 0.0f;
 #pragma unroll
@@ -658,7 +668,7 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
             float z[6][2];
 #pragma unroll
             for (int i = 0; i < 6; ++i) {
-              const float2 w = *reinterpret_cast<const float2*>(xb + xs(i, s) + xl + 2 * Bc);
+              const float2 w = *reinterpret_cast<const float2*>(xb + xp(i, s, Bc));
               z[i][0] = w.x;
               z[i][1] = w.y;
             }
