@@ -83,9 +83,19 @@ PEAK_TF = {'exact': 157.3, 'winograd': 157.3, 'x3': 2500.0 / 3}
 PEAK_HBM_GBPS = 8000.0
 PEAK_FP64_TF = 78.6        # MI355X datasheet FP64 vector (not in MI355X_MICROARCH.md)
 DTYPE = {'exact': 'f32',
-         'winograd': 'f32 (conv2 of block 1 as Winograd F(2x2,3x3), blocks 2-4 as Winograd F(4x4,3x3): f32 '
-                     'transforms, f32 MFMA, f32 accumulate)',
          'x3': 'bf16x3-split (3 bf16 MFMAs per f32 MAC: hi*hi + hi*lo + lo*hi, f32 accumulate)'}
+
+
+def dtype_of(precision):
+    """The arithmetic a precision computes in (winograd: which layers run which
+    Winograd form, per WINO_F43 / WINO_BLOCK1)."""
+    if precision != 'winograd':
+        return dtype_of(precision)
+    b1 = ('conv1 + conv2 of block 1 as the direct fused conv' if not WINO_BLOCK1 else
+          'conv2 of block 1 as Winograd F(4x4,3x3)' if WINO_F43 == 2 else
+          'conv2 of block 1 as Winograd F(2x2,3x3)')
+    rest = 'blocks 2-4 as Winograd F(4x4,3x3)' if WINO_F43 else 'blocks 2-4 as Winograd F(2x2,3x3)'
+    return 'f32 (%s, %s: f32 transforms, f32 MFMA, f32 accumulate)' % (b1, rest)
 # Winograd F(2x2,3x3): 16 matrix-pipe multiplies per 2x2 output tile where the
 # direct conv does 36 ('winograd' mode: blocks 2-4, and block 1's conv2 unless
 # --wino-block1 0 keeps block 1 as the direct fused launch; 1 feeds it from a
@@ -639,7 +649,7 @@ def gamma_leg(args, dev, precision):
     traffic, rocprof_fe = gamma_profile(B)
     return {'workload': 'Cnn_9layers_Gru_FrameAtt gammatone 32k, %d x 10 s @ 32 kHz clips per step '
                         '(float64 gammatone features + forward)' % B,
-            'value': round(value, 2), 'unit': 'clips/s', 'dtype': DTYPE[precision] + '; gammatone frontend f64',
+            'value': round(value, 2), 'unit': 'clips/s', 'dtype': dtype_of(precision) + '; gammatone frontend f64',
             'ms_per_step': round(elapsed / args.steps * 1e3, 4),
             'roofline': roofline(stage_ms, B, precision, T=T, iso_ms=iso,
                                  summary=GAMMA_PROFILE_SUMMARY if B == 32 else None),
@@ -679,7 +689,7 @@ def window_leg(model, wave, args, dev, precision):
             'ms_per_clip_p50_note': 'device input, one batch of %d clips (its %d windows) at a time, per clip'
                                     % (B, nwin),
             'roofline': roof, 'stage_ms_isolated': iso,
-            'dtype': DTYPE[precision],
+            'dtype': dtype_of(precision),
             'note': '5 s windows, 1 s stride, all windows of the batch in one launch, merged + avg_merge '
                     'on the GPU (predict.py:297-349)'}
 
@@ -696,7 +706,7 @@ def config5_leg(model, wave, args, world, rank, dev, precision, isolated=True):
            'global_batch': B * world, 'batch_per_gpu': B,
            'backend': dist.get_backend() if world > 1 else None,
            'ms_per_step': round(e / args.steps * 1e3, 4), 'ms_per_clip_p50_device': round(p50, 4),
-           'scaling': 'weak', 'dtype': DTYPE.get(precision, precision),
+           'scaling': 'weak', 'dtype': dtype_of(precision) if precision in PEAK_TF else precision,
            'gathered': 'framewise_output + clipwise_output to rank 0 every step'}
     if st is not None:
         out['roofline'] = roofline(st, B, precision, iso_ms=iso)
@@ -994,7 +1004,7 @@ def main():
             extra['latency_b1_%s' % other] = latency_b1(model, dev)
             model.set_precision(args.precision)
             v2, e2, st2, p2, _, iso2 = clip_leg(model, wave, args, 1, 0, dev, other, isolated=True)
-            extra['value_%s' % other] = {'value': round(v2, 2), 'unit': 'clips/s', 'dtype': DTYPE[other],
+            extra['value_%s' % other] = {'value': round(v2, 2), 'unit': 'clips/s', 'dtype': dtype_of(other),
                                          'ms_per_step': round(e2 / args.steps * 1e3, 4),
                                          'ms_per_clip_p50_device': round(p2, 4),
                                          'roofline': roofline(st2, B, other, iso_ms=iso2), 'stage_ms': st2,
@@ -1008,7 +1018,7 @@ def main():
             cfgs['config3'] = {'workload': 'Cnn_9layers_Transformer_FrameAtt logmel 16k, %d x 10 s clips '
                                            'per step (clip mode)' % B,
                                'metric': METRICS['transformer'],
-                               'value': round(v3, 2), 'unit': 'clips/s', 'dtype': DTYPE[args.precision],
+                               'value': round(v3, 2), 'unit': 'clips/s', 'dtype': dtype_of(args.precision),
                                'ms_per_step': round(e3 / args.steps * 1e3, 4),
                                'ms_per_clip_p50_device': round(p3, 4),
                                'roofline': roofline(st3, B, args.precision, iso_ms=iso3), 'stage_ms': st3}
@@ -1035,7 +1045,7 @@ def main():
             'ms_per_step': round(elapsed / args.steps * 1e3, 4),
             'ms_per_clip_p50': round(p50, 4) if p50 is not None else None,
             'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
-            'dtype': DTYPE[args.precision],
+            'dtype': dtype_of(args.precision),
             'data': 'synthetic (seeded 0.1*N(0,1) + gated tones; random-init weights)',
             'config': {'workload': '%s logmel 16k, %d x 10 s clips per GPU per step (%s mode)'
                                    % (name, B, args.mode),
