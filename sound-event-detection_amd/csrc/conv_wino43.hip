@@ -753,6 +753,13 @@ __global__ __launch_bounds__(768, 1) void conv3x3_wino43_kernel(const float* __r
 }
 #undef SEDX_W43_ROWS
 
+// items per workgroup.  Alone on the chip 16 (one persistent workgroup per
+// CU: one exposed prologue per CU) is fastest — blocks 1-4 2.41 -> 2.35 ms
+// (tools/gpu_r05n.sh, profiles/r05n_w43_items.log; 3 and 6 are slower:
+// their grids break the L2 round order) — but in the two-stream headline
+// long-lived workgroups hold the CUs the other batch's frontend / GRU /
+// head need: 11,362-11,424 clips/s at 16, 11,546-11,585 at 4,
+// 11,708-11,724 at 2 (profiles/r05p_items_ab.log).  2 stays.
 #ifndef SEDX_W43_ITEMS
 #define SEDX_W43_ITEMS 2
 #endif

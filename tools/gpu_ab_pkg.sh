@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 for r in ${ROUNDS:-1 2}; do
   for v in tree ${VARIANTS}; do
-    if [ $v = tree ]; then P=""; else P="--ab-package $PWD/sound-event-detection_amd/build/ab/$v"; fi
+    if [ $v = tree ]; then P=""; else P="--ab-package $PWD/sound-event-detection_amd/${AB_ROOT:-build/ab}/$v"; fi
     timeout -k 10 300 python bench.py $P --steps ${STEPS:-30} --warmup 3 --no-cpu-baseline ${BENCH_ARGS:---no-side} \
       > gpurun_out/abp_$v$r.log 2>&1 || exit $?
     python3 -c "
