@@ -994,10 +994,17 @@ def main():
         progress('events + latency_b1')
         extra.update(events_side(model, wave))
         extra['latency_b1'] = latency_b1(model, dev)
+        if args.precision == 'winograd' and WINO_F43:
+            # a handle tuned for one-clip latency: every conv on F(2x2,3x3),
+            # whose items are a quarter the size, so a 1-clip grid keeps more
+            # CUs busy (profiles/r05q_small_batch.log); outputs of one handle
+            # never depend on the batch, so the form is a per-handle choice
+            model.set_tuning(_lib.TUNE_WINO_F43, 0)
+            extra['latency_b1_wino_f23'] = latency_b1(model, dev)
+            model.set_tuning(_lib.TUNE_WINO_F43, int(WINO_F43))
         notes = {'x3': 'opt-in arithmetic (operands narrowed to 16 significant bits), same workload',
                  'exact': 'fp32, direct 3x3 conv everywhere (bit-reproducible reference arithmetic), same workload',
-                 'winograd': 'fp32, block 1 conv2 as Winograd F(2x2,3x3) and blocks 2-4 as F(4x4,3x3), same '
-                             'workload'}
+                 'winograd': dtype_of('winograd') + ', same workload'}
         for other in [p for p in ('exact', 'winograd', 'x3') if p != args.precision]:
             progress('value_%s leg' % other)
             model.set_precision(other)

@@ -189,13 +189,23 @@ __device__ __forceinline__ void w43_at(const float (&m)[6], float (&z)[4]) {
 // output; the freq-mean output is [B][T][C] either way), else NHWC
 // [B][T][F][C].  A chunk's halo plane is then a dense run of 16-byte pixels
 // (a halo DMA of 64 lanes touches ~9 cache lines instead of 64).
-template <int F, int EPI, int ROW, bool C4>
+//
+// NT: channel tiles per item.  4 (64 channels) on full grids; 1 (16 channels,
+// the launcher's choice when the 64-channel items would leave CUs idle,
+// e.g. one clip): four times the items, each tile's accumulation chain the
+// same instructions in the same order — bit-identical to NT 4.  An item
+// still DMAs its 64-channel U slab and reads its 16 channels' words.
+template <int F, int EPI, int ROW, bool C4, int NT>
 __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, int T, int Cin, int Cout,
                                          const float* __restrict__ U, int u_bytes, const float* __restrict__ bias,
                                          float* __restrict__ out, float* __restrict__ trash, int tb_per_clip,
                                          int ngroups, int order2d) {
   using G = W43Geom<F>;
   constexpr int RS = G::RS, PS = G::PS;
+  static_assert(NT == 4 || NT == 1, "channel tiles per item");
+  // a U fragment: the lane's words of its NT channel tiles
+  using UF = typename std::conditional<NT == 4, w43_f32x4, float>::type;
+  auto g64 = [](int g_) { return NT == 4 ? g_ : g_ >> 2; };   // 64-channel U slab group of channel group g_
   extern __shared__ __attribute__((aligned(16))) float smem[];   // G::LDS_BYTES (dynamic)
 
   const int tid = threadIdx.x;
@@ -279,7 +289,7 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
 
   // epilogue stores per wave per item (all issued: out-of-range ones go to
   // this workgroup's trash); finisher waves 0-3 only
-  constexpr int S = ROW >= 4 ? 0 : EPI == EPI_STORE ? 16 : 4;
+  constexpr int S = ROW >= 4 ? 0 : (EPI == EPI_STORE ? 4 : 1) * NT;
   float* const tr_lane = trash + (blockIdx.x & 31) * 256 + 4 * lane;
   // 4-channel group n .. n + 3 of output pixel (t, f) (rows To x cols Fo)
   auto opix = [&](int t, int f, int n, int To, int Fo) -> float* {
@@ -297,9 +307,9 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
   }
   uint32_t hof = halo_off(b, t0);
   dma_h(hof, 0, 0);
-  dma_u(grp, 0, 0);
+  dma_u(g64(grp), 0, 0);
   dma_h(hof, 1, 1);
-  dma_u(grp, 1, 1);
+  dma_u(g64(grp), 1, 1);
   dma_h(hof, 2, 2);
   if constexpr (S > 0) {
     float* const vt = tr_lane;   // exactly S stores (never merged), as the epilogue's
@@ -337,17 +347,20 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
     asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(x[2]) : "v"(a), "n"(4 * (R * RS + 4)));
   };
   // U fragment of position 6 ROW + J (byte address a of the lane in the U slot)
-  auto read_u = [](uint32_t a, auto j_tag, w43_f32x4& u) {
+  auto read_u = [](uint32_t a, auto j_tag, UF& u) {
     constexpr int J = decltype(j_tag)::value;
-    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(u) : "v"(a), "n"(4 * (6 * ROW + J) * 256));
+    if constexpr (NT == 4)
+      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(u) : "v"(a), "n"(4 * (6 * ROW + J) * 256));
+    else
+      asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(u) : "v"(a), "n"(4 * (6 * ROW + J) * 256));
   };
-  auto wait_u = [](auto n_tag, w43_f32x4& u) {
+  auto wait_u = [](auto n_tag, UF& u) {
     asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(u) : "n"(decltype(n_tag)::value));
   };
-  auto wait_r = [](auto n_tag, f2v (&x)[3], w43_f32x4& u) {
+  auto wait_r = [](auto n_tag, f2v (&x)[3], UF& u) {
     asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(u) : "n"(decltype(n_tag)::value));
   };
-  auto wait_rr = [](auto n_tag, f2v (&x)[3], f2v (&y)[3], w43_f32x4& u) {
+  auto wait_rr = [](auto n_tag, f2v (&x)[3], f2v (&y)[3], UF& u) {
     asm volatile("s_waitcnt lgkmcnt(%7)"
                  : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(y[0]), "+v"(y[1]), "+v"(y[2]), "+v"(u)
                  : "n"(decltype(n_tag)::value));
@@ -394,13 +407,14 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
   using I4 = std::integral_constant<int, 4>;
   using I5 = std::integral_constant<int, 5>;
   const uint32_t h_lane = w43_lds_addr(smem + G::H_OFF + p_base);     // + slot * 4 HALO
-  const uint32_t u_lane = w43_lds_addr(smem + G::U_OFF + 4 * lane);   // + slot * 4 USZ
+  // + slot * 4 USZ; NT 1: + the item's 16-channel tile (grp & 3)
+  uint32_t u_lane = w43_lds_addr(smem + G::U_OFF + 4 * lane + (NT == 1 ? (grp & 3) : 0));
   // V of the lane's 6 positions for the chunk in halo slot hs_ (item top: no
   // MFMAs to hide behind)
   auto transform = [&](int hs_, float (&v)[6]) {
     const uint32_t a = h_lane + hs_ * (4 * G::HALO);
     f2v xa[3], xb[3], xc[3], xd[3];
-    w43_f32x4 dummy = {0.0f, 0.0f, 0.0f, 0.0f};
+    UF dummy = {};
     read_row(a, IPA{}, xa);
     if constexpr (PB >= 0) read_row(a, IPB{}, xb);
     read_row(a, IPC{}, xc);
@@ -415,14 +429,18 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
     pin6(v);
   };
 
-  w43_f32x4 acc[6][4];
+  w43_f32x4 acc[6][NT];
   float va[6], vb[6];
   int us = 0, hs = 0;   // slots of the current chunk's U and halo
 
   auto fence = []() { __builtin_amdgcn_sched_barrier(0); };
-  auto mfma4 = [&](int j, const w43_f32x4& u, float v) {
+  auto mfma4 = [&](int j, const UF& u, float v) {
+    if constexpr (NT == 1) {
+      acc[j][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(u, v, acc[j][0], 0, 0, 0);
+    } else {
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) acc[j][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(u[nt], v, acc[j][nt], 0, 0, 0);
+      for (int nt = 0; nt < 4; ++nt) acc[j][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(u[nt], v, acc[j][nt], 0, 0, 0);
+    }
   };
 
   // the first item's chunk 0: halo(0) landed (younger: the groups of steps
@@ -450,7 +468,7 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
 #pragma unroll
     for (int j = 0; j < 6; ++j)
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) acc[j][nt] = w43_f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+      for (int nt = 0; nt < NT; ++nt) acc[j][nt] = w43_f32x4{0.0f, 0.0f, 0.0f, 0.0f};
 
     // step c: MFMAs of chunk c with V (vc) and U(c) read just in time (at most
     // two positions ahead); V of chunk c + 1 from halo(c + 1) into vn, its
@@ -468,15 +486,15 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
       const int hs1 = hs == 2 ? 0 : hs + 1;
       const uint32_t ua = u_lane + us * (4 * G::USZ);
       const uint32_t ha = h_lane + hs1 * (4 * G::HALO);
-      w43_f32x4 u0, u1, u2, u3, u4, u5;
+      UF u0, u1, u2, u3, u4, u5;
       f2v xa[3], xb[3], xc[3], xd[3];
       float e[6];
       read_u(ua, I0{}, u0);
       read_u(ua, I1{}, u1);
       // group of step c: U(c + 2) -> the U slot of c - 1, halo(c + 3) -> the
       // halo slot of c (read during step c - 1)
-      if (c + 2 < nchunks) dma_u(grp, c + 2, us2);
-      else dma_u(ng, c + 2 - nchunks, us2);
+      if (c + 2 < nchunks) dma_u(g64(grp), c + 2, us2);
+      else dma_u(g64(ng), c + 2 - nchunks, us2);
       if (c + 3 < nchunks) dma_h(hof, c + 3, hs);
       else dma_h(nhof, c + 3 - nchunks, hs);
       fence();
@@ -560,10 +578,10 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
     const int xl = 68 * kc + 4 * (le & 15);   // this lane's STORE entry
     auto xp = [&](int row, int s, int bp) { return ((row * 2 + s) * 2 + bp) * 128 + 2 * le; };
     const int trg = t0 / 4 + tr;   // the lane's tile row in the clip
-    w43_f32x4 ost[4];              // POOL2 / FMEAN: one 4-channel group per channel tile
+    w43_f32x4 ost[NT];             // POOL2 / FMEAN: one 4-channel group per channel tile
     w43_f32x4 ost2[4];             // STORE: the 2 x 2 pixels of the current channel tile
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
+    for (int q = 0; q < 2 * NT; ++q) {
       const int nt = q >> 1;
       if constexpr (SEDX_W43_ABL & 4) {   // timing build: no exchange / output transform
         if constexpr (ROW < 4) {
@@ -582,7 +600,7 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
           }
           if constexpr (EPI == EPI_STORE) {
             if (q & 1) {
-              const int n = grp * 64 + 16 * nt + 4 * kc;
+              const int n = grp * 16 * NT + 16 * nt + 4 * kc;
 #pragma unroll
               for (int a = 0; a < 2; ++a) {
                 const int t = 4 * trg + 2 * (ROW >> 1) + a;
@@ -621,7 +639,7 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
       }
       if constexpr (!(SEDX_W43_ABL & 8)) w43_lds_bar();
       if constexpr (ROW < 4) {
-        const int n = grp * 64 + 16 * nt + 4 * kc;   // first of the lane's 4 channels
+        const int n = grp * 16 * NT + 16 * nt + 4 * kc;   // first of the lane's 4 channels
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
           const int r = 2 * (q & 1) + s;
@@ -723,6 +741,7 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
     t0 = nt0;
     grp = ng;
     hof = nhof;
+    if constexpr (NT == 1) u_lane = w43_lds_addr(smem + G::U_OFF + 4 * lane + (grp & 3));
   }
 #ifdef SEDX_W43_STAMPS
   if (lane == 0 && (blockIdx.x & 15) == 0) {
@@ -733,23 +752,23 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
 #endif
 }
 
-#define SEDX_W43_ROWS(F_, EPI_, C4_, ...)                              \
+#define SEDX_W43_ROWS(F_, EPI_, C4_, NT_, ...)                         \
   switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >> 1) {    \
-    case 0: w43_body<F_, EPI_, 0, C4_>(__VA_ARGS__); break;           \
-    case 1: w43_body<F_, EPI_, 1, C4_>(__VA_ARGS__); break;           \
-    case 2: w43_body<F_, EPI_, 2, C4_>(__VA_ARGS__); break;           \
-    case 3: w43_body<F_, EPI_, 3, C4_>(__VA_ARGS__); break;           \
-    case 4: w43_body<F_, EPI_, 4, C4_>(__VA_ARGS__); break;           \
-    default: w43_body<F_, EPI_, 5, C4_>(__VA_ARGS__); break;          \
+    case 0: w43_body<F_, EPI_, 0, C4_, NT_>(__VA_ARGS__); break;      \
+    case 1: w43_body<F_, EPI_, 1, C4_, NT_>(__VA_ARGS__); break;      \
+    case 2: w43_body<F_, EPI_, 2, C4_, NT_>(__VA_ARGS__); break;      \
+    case 3: w43_body<F_, EPI_, 3, C4_, NT_>(__VA_ARGS__); break;      \
+    case 4: w43_body<F_, EPI_, 4, C4_, NT_>(__VA_ARGS__); break;      \
+    default: w43_body<F_, EPI_, 5, C4_, NT_>(__VA_ARGS__); break;     \
   }
 
-template <int F, int EPI, bool C4>
+template <int F, int EPI, bool C4, int NT = 4>
 __global__ __launch_bounds__(768, 1) void conv3x3_wino43_kernel(const float* __restrict__ in, int B, int T, int Cin,
                                                                 int Cout, const float* __restrict__ U, int u_bytes,
                                                                 const float* __restrict__ bias, float* __restrict__ out,
                                                                 float* __restrict__ trash, int tb_per_clip,
                                                                 int ngroups, int order2d) {
-  SEDX_W43_ROWS(F, EPI, C4, in, B, T, Cin, Cout, U, u_bytes, bias, out, trash, tb_per_clip, ngroups, order2d)
+  SEDX_W43_ROWS(F, EPI, C4, NT, in, B, T, Cin, Cout, U, u_bytes, bias, out, trash, tb_per_clip, ngroups, order2d)
 }
 #undef SEDX_W43_ROWS
 
@@ -772,21 +791,24 @@ static void launch_w43_f(const float* in, int B, int T, int Cin, int Cout, const
   const int rows = epi == EPI_POOL2 ? 2 * (T / 2) : T;
   const int trows = (rows + 3) / 4;
   const int tb_per_clip = (trows + G::TRW - 1) / G::TRW;
-  const int ngroups = Cout / G::NCH;
   const int64_t tblocks = (int64_t)B * tb_per_clip;
+  int ncu = 256, dev = 0;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  // 16-channel items (NT 1, bit-identical) when 64-channel ones would not
+  // give every CU one
+  const bool nt1 = (tblocks + 7) / 8 * 8 * (Cout / G::NCH) < ncu;
+  const int ngroups = Cout / (nt1 ? 16 : G::NCH);
   const int64_t nitems = (tblocks + 7) / 8 * 8 * ngroups;
   const int64_t u_bytes = (int64_t)Cin * Cout * 36 * 4;
   if (nitems > INT32_MAX || tblocks <= 0 || (int64_t)B * T * F * Cin * 4 >= INT32_MAX || u_bytes >= INT32_MAX)
     return note_launch_error(hipErrorInvalidValue);
-  int ncu = 256, dev = 0;
-  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
   const int64_t resident = (int64_t)ncu / 8 * 8;
   const int64_t per = (nitems + SEDX_W43_ITEMS - 1) / SEDX_W43_ITEMS;
   const int64_t nwg = std::min<int64_t>(nitems, std::max<int64_t>(std::max<int64_t>(8, resident), (per + 7) / 8 * 8));
   // rounds of 32 / G tile blocks x G channel groups (conv_wino.hip): the G
   // whose round streams the fewest bytes through an XCD's L2
   int order2d = 0;
-  if (order && nwg % 256 == 0 && (nitems / 8) % 32 == 0) {
+  if (order && !nt1 && nwg % 256 == 0 && (nitems / 8) % 32 == 0) {
     const int64_t slab = (int64_t)36 * Cin * G::NCH * 4, halo = (int64_t)G::RT * G::CS * Cin * 4;
     int64_t best = (int64_t)ngroups * slab + (32 / std::min(ngroups, 32)) * halo;
     for (int gr = 1; gr <= 8 && gr < ngroups; gr *= 2) {
@@ -799,7 +821,8 @@ static void launch_w43_f(const float* in, int B, int T, int Cin, int Cout, const
   }
 #define SEDX_W43_LAUNCH(E)                                                                                 \
   {                                                                                                        \
-    auto* k_ = c4 ? conv3x3_wino43_kernel<F, E, true> : conv3x3_wino43_kernel<F, E, false>;                \
+    auto* k_ = nt1 ? (c4 ? conv3x3_wino43_kernel<F, E, true, 1> : conv3x3_wino43_kernel<F, E, false, 1>)   \
+                   : (c4 ? conv3x3_wino43_kernel<F, E, true, 4> : conv3x3_wino43_kernel<F, E, false, 4>);  \
     if (!launch_info(reinterpret_cast<const void*>(k_), G::THREADS, G::LDS_BYTES).ok) return;              \
     hipLaunchKernelGGL(k_, dim3((unsigned)nwg), dim3(G::THREADS), G::LDS_BYTES, s, in, B, T, Cin, Cout, U, \
                        (int)u_bytes, bias, out, trash, tb_per_clip, ngroups, order2d);                     \
