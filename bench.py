@@ -888,6 +888,9 @@ def main():
                     help='N > 1 process-group backend: nccl (= RCCL, the default with GPUs; rank r on GPU r) or '
                          'gloo (every rank on GPU 0, gathers through host copies: a rehearsal of the N-rank path '
                          'with the real model on a one-GPU box)')
+    ap.add_argument('--gru-handoff', choices=['auto', 'global', 'spread'], default=None,
+                    help='SEDX_TUNE_GRU_HANDOFF (A/B runs): XCD-local when placed on one XCD (auto), always the '
+                         'global protocol, or the global protocol with the slices dealt over every XCD (spread)')
     ap.add_argument('--wino-f43', type=int, choices=[0, 1, 2], default=None,
                     help='SEDX_TUNE_WINO_F43 (A/B runs): blocks 1-4 (2, the default) or 2-4 (1) as Winograd '
                          'F(4x4,3x3), or all F(2x2,3x3) (0)')
@@ -924,6 +927,8 @@ def main():
     model.set_tuning(_lib.TUNE_GRU_KERNEL, GRU_KERNELS[args.gru_kernel])
     if args.wino_order is not None:
         model.set_tuning(_lib.TUNE_WINO_ORDER, args.wino_order)
+    if args.gru_handoff is not None:
+        model.set_tuning(_lib.TUNE_GRU_HANDOFF, {'auto': 0, 'global': 1, 'spread': 2}[args.gru_handoff])
     B = args.batch
     wave = torch.from_numpy(synth.make_waveforms(B, 10.0, 16000, seed=1234 + rank)).to(dev)
 
@@ -1063,7 +1068,8 @@ def main():
                        'backend': dist.get_backend() if world > 1 else None,
                        'streams': args.streams,
                        'pipelined': args.streams > 1 and not args.no_pipeline,
-                       'gru_kernel': args.gru_kernel if args.model == 'gru' else None},
+                       'gru_kernel': args.gru_kernel if args.model == 'gru' else None,
+                       'gru_handoff': (args.gru_handoff or 'auto') if args.model == 'gru' else None},
             'ms_per_clip_p99': round(p99, 4) if p99 is not None else None,
             'ms_per_clip_p50_note': 'per batch, one at a time, from pinned host input (H2D on a copy '
                                     'stream) to framewise in pinned host memory on rank 0',

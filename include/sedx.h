@@ -283,9 +283,14 @@ sedx_status sedx_set_precision(sedx_handle* h, int32_t mode);
  *                         multiplies and loading their h straight into its
  *                         MFMA operands (no LDS gather); bit-identical.
  *  SEDX_TUNE_GRU_HANDOFF  (COOP) SEDX_GRU_HANDOFF_AUTO (default): XCD-local hand-off
- *                         when all 8 slices share an XCD, else global;
+ *                         when all 8 slices share an XCD, else global; on a
+ *                         pipelined handle (sedx_set_pipelined) SPREAD;
  *                         SEDX_GRU_HANDOFF_GLOBAL: always the global protocol
- *                         (same bytes, bit-identical results).
+ *                         (same bytes, bit-identical results);
+ *                         SEDX_GRU_HANDOFF_SPREAD: the global protocol with a
+ *                         (group, direction)'s workgroups dealt over every XCD
+ *                         (beside a concurrent conv stack no XCD loses a
+ *                         quarter of its CUs; bit-identical).
  *  SEDX_TUNE_MEL_MFMA     (n_fft 512) 0 (default): the log-mel frontend's mel
  *                         projection as VALU band sums; 1: on
  *                         v_mfma_f32_16x16x4_f32, the workgroup's 16 frames x
@@ -360,7 +365,7 @@ enum {
   SEDX_GRU_KERNEL_AUTO = 5,
   SEDX_GRU_KERNEL_KSPLIT = 6
 };
-enum { SEDX_GRU_HANDOFF_AUTO = 0, SEDX_GRU_HANDOFF_GLOBAL = 1 };
+enum { SEDX_GRU_HANDOFF_AUTO = 0, SEDX_GRU_HANDOFF_GLOBAL = 1, SEDX_GRU_HANDOFF_SPREAD = 2 };
 sedx_status sedx_set_tuning(sedx_handle* h, int32_t knob, int32_t value);
 
 /* Asynchronous failures of forwards already issued: a GRU recurrence whose

@@ -488,7 +488,14 @@ sedx_status run_body(sedx_handle* h, int64_t B, const Geometry& g, float* ws, co
                       // kernel holds half the CUs; one batch at a time 16 slices halve
                       // the recurrence's serial product
                       : h->gru_kernel == SEDX_GRU_KERNEL_AUTO ? (h->pipelined ? 2 : 3) : 2,
-                      h->gru_err_dev, h->gru_spin, s);
+                      h->gru_err_dev, h->gru_spin, s,
+                      // AUTO on a pipelined handle: the recurrence runs beside the
+                      // next batch's conv stack, whose items are dealt to the 8
+                      // XCDs evenly — slices on one XCD cost that XCD a quarter
+                      // of its CUs and the whole launch waits for it (b1c2 0.61
+                      // vs 0.51 ms in the timed region, profiles/r05t_*)
+                      h->gru_handoff == SEDX_GRU_HANDOFF_SPREAD ||
+                          (h->gru_handoff == SEDX_GRU_HANDOFF_AUTO && h->pipelined));
   } else {
     linear(S, w.wqkv, w.wqkv_x3, 1536, 128, w.bqkv, G, 0);
     launch_mha(G, iB, (int)g.T3, O, s);
@@ -671,7 +678,7 @@ sedx_status sedx_set_tuning(sedx_handle* h, int32_t knob, int32_t value) {
       h->gru_kernel = value;
       return SEDX_OK;
     case SEDX_TUNE_GRU_HANDOFF:
-      if (value != SEDX_GRU_HANDOFF_AUTO && value != SEDX_GRU_HANDOFF_GLOBAL) break;
+      if (value != SEDX_GRU_HANDOFF_AUTO && value != SEDX_GRU_HANDOFF_GLOBAL && value != SEDX_GRU_HANDOFF_SPREAD) break;
       h->gru_handoff = value;
       return SEDX_OK;
     case SEDX_TUNE_WINO_BLOCK1:

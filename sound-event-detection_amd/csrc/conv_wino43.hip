@@ -67,7 +67,8 @@ typedef float w43_f32x4 __attribute__((ext_vector_type(4)));
 // Ablation builds (tools/wino43_bench.cpp only, results WRONG, timing only):
 // SEDX_W43_ABL bit 1 drops the halo DMAs, 2 the U DMAs, 4 the epilogue's
 // exchange and output transform (stores kept), 8 the epilogue's barriers,
-// 16 the STORE epilogue's scatter (every store to one coalesced 1 KiB run)
+// 16 the STORE epilogue's scatter (every store to one coalesced 1 KiB run),
+// 32 the POOL2 epilogue's
 #ifndef SEDX_W43_ABL
 #define SEDX_W43_ABL 0
 #endif
@@ -722,6 +723,7 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
             if constexpr (EPI == EPI_POOL2) {
               const int to = 2 * trg + (ROW >> 1), fo = 2 * tf + (ROW & 1);
               dst = to < T / 2 ? opix(to, fo, n, T / 2, F / 2) : tr_lane;
+              if constexpr (SEDX_W43_ABL & 32) dst = tr_lane;   // timing: coalesced pool stores
             } else {
               const int t = 4 * trg + ROW;
               dst = (t < T && !(tf & 1)) ? out + (int64_t)(b * T + t) * Cout + n : tr_lane;

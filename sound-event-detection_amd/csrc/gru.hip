@@ -143,7 +143,7 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
                                                        const float* __restrict__ bhh,
                                                        float* __restrict__ H, float* X,
                                                        GruSync* sync, int nslots, int allow_fast,
-                                                       unsigned* host_err, unsigned spin_limit) {
+                                                       unsigned* host_err, unsigned spin_limit, int spread) {
   __shared__ uint4 Aimg[16 * 32 * 4];          // h_{s-1} hi/lo, [kstep][clip][4 slots]
   // partial gate pre-activations: K quarters (x3) / eighths (exact: two
   // independent chains per wave, summed in order in the gate phase)
@@ -156,8 +156,13 @@ __global__ __launch_bounds__(768) void gru_coop_kernel(const float* __restrict__
   static_assert(NS == 8 || (NS == 16 && EXACT && !VALU), "16 slices: the exact MFMA product");
   constexpr int US = 256 / NS;                 // hidden units per slice
   constexpr int NPAIR = 32 * US;               // (clip, unit) pairs of a slice's gate phase
-  const int pair = blockIdx.x & 7;             // dispatch residue -> one XCD (observed)
-  const int p = blockIdx.x >> 3;               // slice 0 .. NS - 1
+  // default: the slices of a pair on blocks b = pair + 8 k — one dispatch
+  // residue, one XCD (observed) — for the XCD-local hand-off; spread: slice
+  // p on block NS pair + p, so a pair's slices cover every XCD (beside a
+  // concurrent conv stack whose items are dealt to XCDs evenly, no XCD loses
+  // a quarter of its CUs to the recurrence)
+  const int pair = spread ? (int)blockIdx.x / NS : (int)(blockIdx.x & 7);
+  const int p = spread ? (int)blockIdx.x % NS : (int)(blockIdx.x >> 3);   // slice 0 .. NS - 1
   const int slot = pair >> 1, dir = pair & 1;
   if (slot >= nslots) return;                  // whole workgroup exits (uniform)
   const int nt = wave % 3, kq = wave / 3, h = lane >> 5;
@@ -996,7 +1001,9 @@ static void launch_gru_tag(const float* G, int B, int T, const float* whh, const
 
 void launch_gru_coop(const float* G, int B, int T, const float* whh, const float* bhh, float* H,
                      void* ws, bool exact, bool allow_fast, int variant, unsigned* host_err, unsigned spin,
-                     hipStream_t s) {
+                     hipStream_t s, bool spread) {
+  const int sp = spread ? 1 : 0;
+  if (spread) allow_fast = false;
   GruSync* sync = static_cast<GruSync*>(ws);
   const size_t sync_bytes = (sizeof(GruSync) + 255) & ~size_t(255);
   float* X = reinterpret_cast<float*>(static_cast<char*>(ws) + sync_bytes);
@@ -1023,16 +1030,16 @@ void launch_gru_coop(const float* G, int B, int T, const float* whh, const float
   (void)hipMemsetAsync(sync, 0, sync_bytes + (valu ? (size_t)2 * 2 * GRU_VALU_CLIPS * 256 * 8 : 0), s);
   if (valu)
     launch_kernel(gru_coop_kernel<true, true>, dim3(64), 768, s, G, B, T, whh, bhh, H, X, sync, nslots,
-                  allow_fast ? 1 : 0, host_err, spin);
+                  allow_fast ? 1 : 0, host_err, spin, sp);
   else if (exact && variant == 3)   // 16 slices per (group, direction)
     launch_kernel(gru_coop_kernel<true, false, 16>, dim3(128), 768, s, G, B, T, whh, bhh, H, X, sync, nslots,
-                  allow_fast ? 1 : 0, host_err, spin);
+                  allow_fast ? 1 : 0, host_err, spin, sp);
   else if (exact)
     launch_kernel(gru_coop_kernel<true, false>, dim3(64), 768, s, G, B, T, whh, bhh, H, X, sync, nslots,
-                  allow_fast ? 1 : 0, host_err, spin);
+                  allow_fast ? 1 : 0, host_err, spin, sp);
   else
     launch_kernel(gru_coop_kernel<false, false>, dim3(64), 768, s, G, B, T, whh, bhh, H, X, sync, nslots,
-                  allow_fast ? 1 : 0, host_err, spin);
+                  allow_fast ? 1 : 0, host_err, spin, sp);
 }
 
 }  // namespace sedx

@@ -294,9 +294,11 @@ size_t gru_coop_workspace_bytes(int B);
 // always), 0 the 16-clip data-tagged kernel with 16 slices, 1 with 8 slices,
 // 3 the flag kernel on 16 slices, 4 the K-split hand-off on 16 slices.
 // spin: bound of every hand-off spin in polls (the handle's SEDX_TUNE_GRU_SPIN, 2^24 by default).
+// spread (flag kernels): a (group, direction)'s slices on every XCD instead of
+// one (global protocol; bit-identical).
 void launch_gru_coop(const float* G, int B, int T, const float* whh, const float* bhh, float* H,
                      void* ws, bool exact, bool allow_fast, int variant, unsigned* host_err, unsigned spin,
-                     hipStream_t s);
+                     hipStream_t s, bool spread = false);
 
 // MHA core: QKV [B][T][1536] (q|k|v, head h = cols 64h..64h+63) -> O [B][T][512]
 void launch_mha(const float* QKV, int B, int T, float* O, hipStream_t s);

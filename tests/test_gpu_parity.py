@@ -176,24 +176,32 @@ def _tune(m, knob, value):
 
 @pytest.mark.parametrize('prec', ['exact', 'x3'])
 def test_gru_handoff_modes_bit_identical(prec):
-    """XCD-local and global GRU hand-off protocols move the same bytes: the
-    outputs must be bit-identical (and the faster one is used by default)."""
+    """XCD-local and global GRU hand-off protocols — the latter also with the
+    slices dealt over every XCD (SPREAD) — move the same bytes: the outputs
+    must be bit-identical (and the faster one is used by default)."""
     import time
     from sedx import _lib
     m = build(GRU).set_precision(prec)
     wave = synth.make_waveforms(32, seconds=10.0, sample_rate=16000, seed=8)
     outs, times = {}, {}
-    for mode in (1, 0):        # SEDX_GRU_HANDOFF_GLOBAL, SEDX_GRU_HANDOFF_AUTO
+    for mode in (1, 2, 0):     # SEDX_GRU_HANDOFF_GLOBAL, _SPREAD, _AUTO
         _tune(m, _lib.TUNE_GRU_HANDOFF, mode)
         run(m, wave)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         outs[mode] = run(m, wave)['framewise_output']
         times[mode] = time.perf_counter() - t0
-    print('GRU hand-off (%s): global %.3f ms, auto %.3f ms (whole forward)' %
-          (prec, times[1] * 1e3, times[0] * 1e3))
+    print('GRU hand-off (%s): global %.3f ms, spread %.3f ms, auto %.3f ms (whole forward)' %
+          (prec, times[1] * 1e3, times[2] * 1e3, times[0] * 1e3))
     assert np.isfinite(outs[0]).all()
     assert np.array_equal(outs[1], outs[0])
+    assert np.array_equal(outs[2], outs[0])
+    # spread with the pipelined (8-slice) kernel too, 40 clips (two groups)
+    w40 = synth.make_waveforms(40, seconds=4.0, sample_rate=16000, seed=9)
+    mp = build(GRU).set_precision(prec).set_pipelined(True)
+    ref = run(mp, w40)['framewise_output']
+    _tune(mp, _lib.TUNE_GRU_HANDOFF, 2)
+    assert np.array_equal(run(mp, w40)['framewise_output'], ref)
 
 
 @pytest.mark.parametrize('n_clips', [40, 80])
