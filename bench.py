@@ -90,7 +90,7 @@ def dtype_of(precision):
     """The arithmetic a precision computes in (winograd: which layers run which
     Winograd form, per WINO_F43 / WINO_BLOCK1)."""
     if precision != 'winograd':
-        return dtype_of(precision)
+        return DTYPE[precision]
     b1 = ('conv1 + conv2 of block 1 as the direct fused conv' if not WINO_BLOCK1 else
           'conv2 of block 1 as Winograd F(4x4,3x3)' if WINO_F43 == 2 else
           'conv2 of block 1 as Winograd F(2x2,3x3)')

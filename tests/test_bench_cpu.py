@@ -212,3 +212,17 @@ def test_config4_profile_fields(bench):
     traffic, ms = bench.gamma_profile(32)
     assert traffic is not None and traffic > 49e6 and ms is not None and 0.0 < ms < 1.0
     assert bench.gamma_profile(8) == (None, None)
+
+
+def test_dtype_strings(bench):
+    """Every precision's dtype string: the arithmetic, and for winograd which
+    layers run which Winograd form under the current knobs."""
+    assert bench.dtype_of('exact') == 'f32'
+    assert bench.dtype_of('x3').startswith('bf16x3')
+    w = bench.dtype_of('winograd')
+    assert 'block 1 as Winograd F(4x4,3x3)' in w and 'blocks 2-4 as Winograd F(4x4,3x3)' in w
+    try:
+        bench.WINO_F43 = 1
+        assert 'block 1 as Winograd F(2x2,3x3)' in bench.dtype_of('winograd')
+    finally:
+        bench.WINO_F43 = 2
