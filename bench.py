@@ -451,13 +451,13 @@ def stage_times_isolated(model, wave, dev, reps):
 # from the rocprofv3 passes of this bench command (tools/profile_round.sh ->
 # tools/pmc_summary.py; FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE),
 # committed under profiles/.
-PROFILE_SUMMARY = os.path.join(REPO, 'profiles', 'r05h_winograd_kernel_summary.json')
+PROFILE_SUMMARY = os.path.join(REPO, 'profiles', 'r05w_winograd_kernel_summary.json')
 # the same passes over the config-4 leg (bench.py --mode gamma: B = 32 x 10 s
 # @ 32 kHz, T = 994 frames)
-GAMMA_PROFILE_SUMMARY = os.path.join(REPO, 'profiles', 'r05h_config4_kernel_summary.json')
+GAMMA_PROFILE_SUMMARY = os.path.join(REPO, 'profiles', 'r05w_config4_kernel_summary.json')
 # the same passes over the window-mode leg (bench.py --mode window: B' = 192
 # windows x 501 frames per call)
-WINDOW_PROFILE_SUMMARY = os.path.join(REPO, 'profiles', 'r05h_window_kernel_summary.json')
+WINDOW_PROFILE_SUMMARY = os.path.join(REPO, 'profiles', 'r05w_window_kernel_summary.json')
 GAMMA_KERNELS = ('sedx::gamma_init_kernel', 'sedx::gamma_spec_kernel<2048>', 'sedx::gamma_erb_kernel',
                  'sedx::gamma_quant_kernel')
 
@@ -483,7 +483,8 @@ def conv_kernel_name(stage, precision):
     if precision == 'winograd' and stage == 'b1c2' and WINO_BLOCK1 == 2 and WINO_F43 != 2:
         return 'sedx::wino_block1_kernel<2, %s>' % c4
     if precision == 'winograd' and stage in wino_stages() and wino_mul(stage) == WINO43_MUL:
-        return 'sedx::conv3x3_wino43_kernel<%d, %d, %s>' % (F, epi, c4)
+        # (the last argument: 4 channel tiles per item at the bench's B = 32)
+        return 'sedx::conv3x3_wino43_kernel<%d, %d, %s, 4>' % (F, epi, c4)
     if precision == 'winograd' and stage in wino_stages():
         # 2 tile groups x 64 channels (8 row waves) at the bench shapes
         return 'sedx::conv3x3_wino_kernel<%d, %d, 2, 2>' % (F, epi)
