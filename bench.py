@@ -108,7 +108,7 @@ WINO_MUL = 16.0 / 36.0
 WINO_F43 = 2
 WINO43_MUL = 36.0 / 144.0
 # SEDX_TUNE_GRU_KERNEL values (include/sedx.h)
-GRU_KERNELS = {'coop': 0, 'simple': 1, 'tag16': 2, 'tag8': 3, 'coop16': 4, 'auto': 5, 'ksplit': 6}
+GRU_KERNELS = {'coop': 0, 'simple': 1, 'tag16': 2, 'tag8': 3, 'coop16': 4, 'auto': 5, 'ksplit': 6, 'pair': 7}
 
 
 def wino_stages():

@@ -282,6 +282,11 @@ sedx_status sedx_set_precision(sedx_handle* h, int32_t mode);
  *                         K-eighth wave waiting only for the two slices it
  *                         multiplies and loading their h straight into its
  *                         MFMA operands (no LDS gather); bit-identical.
+ *                         SEDX_GRU_KERNEL_PAIR (exact, more than 8 clips):
+ *                         the K-split structure with each 32-clip group's
+ *                         two 16-clip halves stepped alternately in one
+ *                         workgroup (one half's hand-off behind the other's
+ *                         product); bit-identical.
  *  SEDX_TUNE_GRU_HANDOFF  (COOP) SEDX_GRU_HANDOFF_AUTO (default): XCD-local hand-off
  *                         when all 8 slices share an XCD, else global; on a
  *                         pipelined handle (sedx_set_pipelined) SPREAD;
@@ -363,7 +368,8 @@ enum {
   SEDX_GRU_KERNEL_TAG8 = 3,
   SEDX_GRU_KERNEL_COOP16 = 4,
   SEDX_GRU_KERNEL_AUTO = 5,
-  SEDX_GRU_KERNEL_KSPLIT = 6
+  SEDX_GRU_KERNEL_KSPLIT = 6,
+  SEDX_GRU_KERNEL_PAIR = 7
 };
 enum { SEDX_GRU_HANDOFF_AUTO = 0, SEDX_GRU_HANDOFF_GLOBAL = 1, SEDX_GRU_HANDOFF_SPREAD = 2 };
 sedx_status sedx_set_tuning(sedx_handle* h, int32_t knob, int32_t value);

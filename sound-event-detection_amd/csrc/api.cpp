@@ -484,6 +484,7 @@ sedx_status run_body(sedx_handle* h, int64_t B, const Geometry& g, float* ws, co
                       h->gru_kernel == SEDX_GRU_KERNEL_TAG16 ? 0 : h->gru_kernel == SEDX_GRU_KERNEL_TAG8 ? 1
                       : h->gru_kernel == SEDX_GRU_KERNEL_COOP16 ? 3
                       : h->gru_kernel == SEDX_GRU_KERNEL_KSPLIT ? 4
+                      : h->gru_kernel == SEDX_GRU_KERNEL_PAIR ? 5
                       // AUTO: beside the next batch's conv stack (pipelined) the 8-slice
                       // kernel holds half the CUs; one batch at a time 16 slices halve
                       // the recurrence's serial product
@@ -673,7 +674,7 @@ sedx_status sedx_set_tuning(sedx_handle* h, int32_t knob, int32_t value) {
     case SEDX_TUNE_GRU_KERNEL:
       if (value != SEDX_GRU_KERNEL_COOP && value != SEDX_GRU_KERNEL_SIMPLE && value != SEDX_GRU_KERNEL_TAG16 &&
           value != SEDX_GRU_KERNEL_TAG8 && value != SEDX_GRU_KERNEL_COOP16 && value != SEDX_GRU_KERNEL_AUTO &&
-          value != SEDX_GRU_KERNEL_KSPLIT)
+          value != SEDX_GRU_KERNEL_KSPLIT && value != SEDX_GRU_KERNEL_PAIR)
         break;
       h->gru_kernel = value;
       return SEDX_OK;

@@ -975,6 +975,196 @@ __global__ __launch_bounds__(512) void gru_ksplit_kernel(const float* __restrict
 #undef GRU_KSTAMP
 }
 
+// ---------------------------------------------------------------------------
+// Two interleaved 16-clip recurrences per workgroup (round 5, launch variant
+// 5): the K-split structure above (16 slices of 16 hidden units per 32-clip
+// group and direction; 8 waves = the 8 K eighths, each waiting only for the
+// flags of its two slices and loading their h(t-1) straight into its
+// v_mfma_f32_16x16x4_f32 A fragments) with the group's two halves (clips
+// 0-15, 16-31) as two recurrences stepped alternately: phase (half X, step s)
+// multiplies X's h(s-1) (loaded during the previous phase), then — while its
+// partials are summed and its gates run — polls the flags of the other half
+// Y's step that just finished and issues Y's loads, so Y's hand-off (flag
+// propagation and the L2 round trip) hides behind X's product and gates
+// instead of stalling the workgroup.  Per phase: 24 MFMAs per wave, one
+// LDS barrier for the partials, the gate phase on (clip, unit) threads,
+// payload stores, vmcnt(0), barrier, the slice's per-half flag.
+// Exchange: the K-split layout, half h in rows 16 h .. 16 h + 15 of each
+// parity's [32][256]; flags Fl[slice * 16 + 8 h].  Hazards as in the K-split
+// kernel, per half: a slice publishes X(s + 2) only after its waves saw
+// X(s + 1) from every slice, each of which read X(s) before publishing
+// X(s + 1).  Arithmetic: the same per-eighth fma chains, partials summed in K
+// order, gru_cell — bit-identical to every exact kernel here.
+__global__ __launch_bounds__(512) void gru_pair_kernel(const float* __restrict__ G, int B, int T,
+                                                       const float* __restrict__ whh, const float* __restrict__ bhh,
+                                                       float* __restrict__ H, float* X, GruSync* sync, int nslots,
+                                                       unsigned* host_err, unsigned spin_limit, int spread) {
+  __shared__ float part[8][3][16][GRU_KS_LD];  // [eighth][gate][clip][unit]
+  __shared__ int s_err;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int e = __builtin_amdgcn_readfirstlane(tid >> 6);   // K eighth of this wave
+  const int pair = spread ? (int)blockIdx.x / 16 : (int)(blockIdx.x & 7);
+  const int p = spread ? (int)blockIdx.x % 16 : (int)(blockIdx.x >> 3);   // slice 0..15
+  const int slot = pair >> 1, dir = pair & 1;
+  if (slot >= nslots) return;                  // whole workgroup exits (uniform)
+  if (tid == 0) s_err = 0;
+  __syncthreads();
+  const int ngroups = (B + 31) / 32;
+  const int n16 = lane & 15, kk = lane >> 4;
+  float Wf[3][8];
+#pragma unroll
+  for (int g = 0; g < 3; ++g)
+#pragma unroll
+    for (int st = 0; st < 8; ++st)
+      Wf[g][st] = whh[((int64_t)dir * 768 + g * 256 + 16 * p + n16) * 256 + 32 * e + 4 * st + kk];
+  // gate-phase thread (threads 0..255): (clip gc of the half, unit gu of the slice)
+  const bool gt = tid < 256;
+  const int gc = (tid >> 4) & 15, gu = tid & 15;
+  const int uo = 16 * p + gu;
+  const float br = bhh[dir * 768 + uo], bz = bhh[dir * 768 + 256 + uo], bn = bhh[dir * 768 + 512 + uo];
+  const int upos = gru_kperm(uo);
+  float* const Xs = X + (int64_t)pair * 2 * 32 * 256;
+  unsigned* const Fl = &sync->flag[pair][0][0];
+#ifdef SEDX_GRU_STAMPS
+  // [0] product  [1] next phase's flag wait + load issue  [2] gates  [3] drain + flag
+  unsigned long long st_acc[4] = {0, 0, 0, 0};
+  unsigned long long st_last = __builtin_amdgcn_s_memtime();
+#define GRU_PSTAMP(i)                                                                   \
+  if (tid == 0 && pair == 0 && p == 0) {                                                \
+    const unsigned long long now_ = __builtin_amdgcn_s_memtime();                       \
+    st_acc[i] += now_ - st_last;                                                        \
+    st_last = now_;                                                                     \
+  }
+#else
+#define GRU_PSTAMP(i)
+#endif
+  int j = 0;
+  for (int grp = slot; grp < ngroups; grp += nslots, ++j) {
+    const int c0 = grp * 32;
+    const int nc = min(32, B - c0);
+    // gate inputs of (half h, step s_) for this thread
+    auto load_gi = [&](int h, int s_, float (&v)[3]) {
+      const int t_ = dir ? T - 1 - s_ : s_;
+      const int c = 16 * h + gc;
+      if (gt && c < nc) {
+        const float* gp = G + ((int64_t)(c0 + c) * T + t_) * 1536 + dir * 768 + uo;
+        v[0] = gp[0];
+        v[1] = gp[256];
+        v[2] = gp[512];
+      } else {
+        v[0] = v[1] = v[2] = 0.f;
+      }
+    };
+    // wait for half h's step gs_ - 1 from this wave's two slices, then load
+    // its 8 k of h(gs_ - 1) for every clip of the half (zeros at gs_ == j T)
+    auto fetch = [&](int h, int gs_, bool first, float (&a)[8]) {
+      if (!first && lane < 2) {
+        unsigned spins = 0;
+        while (!gru_dead(&s_err) && g_ld(Fl + (2 * e + lane) * 16 + 8 * h) < (unsigned)gs_) {
+          if (++spins > spin_limit) {
+            gru_fail(sync, host_err, 2u);
+            s_err = 1;
+            break;
+          }
+        }
+      }
+      const int c = 16 * h + n16;
+      if (!first && c < nc) {
+        const unsigned long long* q = reinterpret_cast<const unsigned long long*>(
+            Xs + ((gs_ - 1) & 1) * 32 * 256 + c * 256 + 32 * e + 8 * kk);
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          const unsigned long long v = __hip_atomic_load(q + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          a[2 * w] = __uint_as_float((uint32_t)v);
+          a[2 * w + 1] = __uint_as_float((uint32_t)(v >> 32));
+        }
+      } else {
+#pragma unroll
+        for (int st = 0; st < 8; ++st) a[st] = 0.f;
+      }
+    };
+    float hreg0 = 0.f, hreg1 = 0.f;           // this thread's h(t-1), halves 0 / 1
+    float acur[8], anext[8], gcur[3], gnext[3];
+    const int gs0 = j * T;
+    fetch(0, gs0, true, acur);
+    load_gi(0, 0, gcur);
+    // phase (half H, step s); order (0, 0), (1, 0), (0, 1), (1, 1), ...
+    auto phase = [&](auto h_tag, int s) {
+      constexpr int h = decltype(h_tag)::value;
+      const int gs = gs0 + s;
+      const int t = dir ? T - 1 - s : s;
+      if (tid == 0) gru_forced_fail(spin_limit, gs, sync, host_err, &s_err);
+      f32x4_g acc[3];
+#pragma unroll
+      for (int g = 0; g < 3; ++g) acc[g] = f32x4_g{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int st = 0; st < 8; ++st)
+#pragma unroll
+        for (int g = 0; g < 3; ++g) acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(acur[st], Wf[g][st], acc[g], 0, 0, 0);
+#pragma unroll
+      for (int g = 0; g < 3; ++g)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) part[e][g][4 * kk + i][n16] = acc[g][i];
+      GRU_PSTAMP(0);
+      // the next phase's operands: half h ^ 1 at step s + h (its flags were
+      // set a phase ago), and its gate inputs
+      constexpr int nh = h ^ 1;
+      const int ns = s + h;
+      const bool more = ns < T;
+      if (more) {
+        fetch(nh, gs0 + ns, ns == 0, anext);
+        load_gi(nh, ns, gnext);
+      }
+      GRU_PSTAMP(1);
+      gru_lds_barrier();                       // partials written (payload stores stay in flight)
+      float hv = 0.f;
+      const int c = 16 * h + gc;
+      if (gt && c < nc) {
+        float ghr = part[0][0][gc][gu], ghz = part[0][1][gc][gu], ghn = part[0][2][gc][gu];
+#pragma unroll
+        for (int q = 1; q < 8; ++q) {          // partials in K order
+          ghr += part[q][0][gc][gu];
+          ghz += part[q][1][gc][gu];
+          ghn += part[q][2][gc][gu];
+        }
+        ghr += br;
+        ghz += bz;
+        ghn += bn;
+        const float hn = gru_cell(gcur[0], gcur[1], gcur[2], ghr, ghz, ghn, h ? hreg1 : hreg0);
+        hv = gru_dead(&s_err) ? __builtin_nanf("") : hn;   // NaN propagates to every slice
+        __hip_atomic_store(reinterpret_cast<unsigned*>(Xs + (gs & 1) * 32 * 256 + c * 256 + upos),
+                           __float_as_uint(hv), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (h) hreg1 = hv;
+      else hreg0 = hv;
+      GRU_PSTAMP(2);
+      // payload stores (and the next phase's loads) drained, partial reads
+      // done, then the slice's flag for half h
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0)
+        __hip_atomic_store(Fl + p * 16 + 8 * h, (unsigned)(gs + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      GRU_PSTAMP(3);
+      if (gt && c < nc) H[((int64_t)(c0 + c) * T + t) * 512 + dir * 256 + uo] = hv;
+      if (more) {
+#pragma unroll
+        for (int st = 0; st < 8; ++st) acur[st] = anext[st];
+#pragma unroll
+        for (int g = 0; g < 3; ++g) gcur[g] = gnext[g];
+      }
+    };
+    for (int s = 0; s < T; ++s) {
+      phase(std::integral_constant<int, 0>{}, s);
+      phase(std::integral_constant<int, 1>{}, s);
+    }
+  }
+#ifdef SEDX_GRU_STAMPS
+  if (tid == 0 && pair == 0 && p == 0)
+    for (int i = 0; i < 4; ++i) sync->stamps[i] = st_acc[i];
+#endif
+#undef GRU_PSTAMP
+}
+
 size_t gru_coop_workspace_bytes(int B) {
   (void)B;
   // sync block, then the exchange space: 32-clip kernel 8 pairs x 2 parities
@@ -1013,6 +1203,13 @@ void launch_gru_coop(const float* G, int B, int T, const float* whh, const float
     const int nslots = ngroups < GRU_MAX_SLOTS ? ngroups : GRU_MAX_SLOTS;
     (void)hipMemsetAsync(sync, 0, sync_bytes, s);
     launch_kernel(gru_ksplit_kernel, dim3(128), 512, s, G, B, T, whh, bhh, H, X, sync, nslots, host_err, spin);
+    return;
+  }
+  if (exact && !valu && variant == 5) {   // two interleaved 16-clip recurrences, 16 slices
+    const int ngroups = (B + 31) / 32;
+    const int nslots = ngroups < GRU_MAX_SLOTS ? ngroups : GRU_MAX_SLOTS;
+    (void)hipMemsetAsync(sync, 0, sync_bytes, s);
+    launch_kernel(gru_pair_kernel, dim3(128), 512, s, G, B, T, whh, bhh, H, X, sync, nslots, host_err, spin, sp);
     return;
   }
   if (exact && !valu && variant != 2 && variant != 3) {

@@ -213,21 +213,26 @@ def test_gru_tag_kernels_bit_identical(n_clips):
     slices) keep the exact kernels' arithmetic contract (eight in-order K
     partials, summed in order): bit-identical to the 8-slice 32-clip kernel,
     ragged last group and more groups than resident slots (80 clips) included;
-    AUTO (the default: COOP16 on an unpipelined handle) too."""
+    AUTO (the default: COOP16 on an unpipelined handle) and PAIR (a group's
+    two 16-clip halves stepped alternately in one workgroup, with the
+    SPREAD placement too) as well."""
     from sedx import _lib
     m = build(GRU).set_precision('exact')
     wave = synth.make_waveforms(n_clips, seconds=2.0, sample_rate=16000, seed=n_clips + 3)
     outs = {}
-    for knob in (0, 2, 3, 4, 5, 6):     # COOP, TAG16, TAG8, COOP16, AUTO, KSPLIT
+    for knob in (0, 2, 3, 4, 5, 6, 7):  # COOP, TAG16, TAG8, COOP16, AUTO, KSPLIT, PAIR
         _tune(m, _lib.TUNE_GRU_KERNEL, knob)
         outs[knob] = run(m, wave)['framewise_output']
+    _tune(m, _lib.TUNE_GRU_HANDOFF, 2)
+    outs['pair_spread'] = run(m, wave)['framewise_output']
+    _tune(m, _lib.TUNE_GRU_HANDOFF, 0)
     _tune(m, _lib.TUNE_GRU_KERNEL, 5)
     assert np.isfinite(outs[0]).all()
-    for knob in (2, 3, 4, 5, 6):
+    for knob in (2, 3, 4, 5, 6, 7, 'pair_spread'):
         assert np.array_equal(outs[knob], outs[0]), knob
 
 
-@pytest.mark.parametrize('kernel,n_clips', [(0, 32), (4, 32), (0, 4), (2, 40), (6, 40)])
+@pytest.mark.parametrize('kernel,n_clips', [(0, 32), (4, 32), (0, 4), (2, 40), (6, 40), (7, 40)])
 def test_gru_spin_timeout_surfaces(kernel, n_clips):
     """A GRU hand-off spin that runs out (forced with SEDX_TUNE_GRU_SPIN = 0
     polls: every step that would wait fails, deterministically) turns that forward's outputs into NaN and is reported by

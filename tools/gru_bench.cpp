@@ -38,12 +38,13 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   hipEventCreate(&e0); hipEventCreate(&e1);
   // variants: 0 = tagged 16-clip groups x 16 slices, 1 = tagged x 8 slices, 3 = coop on 16 slices,
-  // 2 = the 32-clip flag kernel (fast = XCD-local hand-off allowed), 4 = K-split hand-off on 16 slices
+  // 2 = the 32-clip flag kernel (fast = XCD-local hand-off allowed), 4 = K-split hand-off on 16 slices,
+  // 5 = two interleaved 16-clip halves per workgroup (K-split structure)
   std::vector<float> ref;
   for (int exact = 1; exact >= 0; --exact)
-    for (int variant = 0; variant < 5; ++variant)
+    for (int variant = 0; variant < 6; ++variant)
     for (int fast = 0; fast < 2; ++fast) {
-      if ((!exact || variant < 2 || variant == 4) && !fast) continue;
+      if ((!exact || variant < 2 || variant >= 4) && !fast) continue;
       if (!exact && (variant < 2 || variant >= 3)) continue;
       sedx::launch_gru_coop(G, B, T, W, Bb, H, ws, exact, fast, variant, nullptr, 1u << 24, 0);
       hipDeviceSynchronize();
