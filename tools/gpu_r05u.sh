@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 5 final check: F(4,3) tool, full GPU suite, smoke, default bench
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-O=gpurun_out/r05u
+O=gpurun_out/r05y
 mkdir -p $O
 timeout -k 10 200 tools/bin/w43_bench 32 10 > $O/w43.log 2>&1; rc=$?
 grep -h "total" $O/w43.log
