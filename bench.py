@@ -873,7 +873,7 @@ def main():
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
     ap.add_argument('--gru-kernel', choices=list(GRU_KERNELS), default='auto',
                     help='GRU recurrence kernel (SEDX_TUNE_GRU_KERNEL; A/B runs); auto: the library default '
-                         '(the 8-slice kernel on a pipelined handle, 16 slices one batch at a time)')
+                         '(16 slices; on a pipelined handle dealt over every XCD)')
     ap.add_argument('--wino-order', type=int, choices=[0, 1], default=None,
                     help='SEDX_TUNE_WINO_ORDER (A/B runs): Winograd item order on the 512-channel layers')
     ap.add_argument('--gamma-spec', type=int, choices=[0, 1], default=None,

@@ -256,11 +256,10 @@ sedx_status sedx_set_precision(sedx_handle* h, int32_t mode);
 
 /* Implementation choices that leave the arithmetic's meaning unchanged (A/B
  * measurement and tests; the defaults are the fastest measured):
- *  SEDX_TUNE_GRU_KERNEL   SEDX_GRU_KERNEL_AUTO (default): COOP on a pipelined
- *                         handle (sedx_set_pipelined: the recurrence runs
- *                         beside the next batch's conv stack, fewer CUs held
- *                         measured faster), COOP16 otherwise (one batch at a
- *                         time: the shorter recurrence);
+ *  SEDX_TUNE_GRU_KERNEL   SEDX_GRU_KERNEL_AUTO (default): COOP16 (the shorter
+ *                         recurrence), on a pipelined handle with its
+ *                         workgroups dealt over every XCD (the recurrence
+ *                         runs beside the next batch's conv stack);
  *                         SEDX_GRU_KERNEL_COOP: the cooperative
  *                         recurrence, 8 workgroups per (32-clip group,
  *                         direction) exchanging h slices every step (up to 8
@@ -346,11 +345,10 @@ sedx_status sedx_set_precision(sedx_handle* h, int32_t mode);
  *
  * Co-residency: the cooperative GRU kernels need all workgroups of a
  * (32-clip group, direction) resident at once — 8 CUs (COOP) or 16 (COOP16)
- * per pair, one workgroup per CU — and spin on each other.  AUTO picks COOP16
- * only for a handle that is not pipelined; a caller that runs several
- * forwards concurrently on other streams without sedx_set_pipelined leaves
- * fewer CUs free for it: the spins are bounded (SEDX_TUNE_GRU_SPIN), so the
- * worst case is a NaN batch reported by sedx_check_error, never a hang. */
+ * per pair, one workgroup per CU — and spin on each other.  AUTO picks
+ * COOP16; forwards running concurrently on other streams leave fewer CUs free
+ * for it: the spins are bounded (SEDX_TUNE_GRU_SPIN), so the worst case is a
+ * NaN batch reported by sedx_check_error, never a hang. */
 typedef enum {
   SEDX_TUNE_GRU_KERNEL = 0,
   SEDX_TUNE_GRU_HANDOFF = 1,

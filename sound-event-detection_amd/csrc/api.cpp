@@ -485,10 +485,12 @@ sedx_status run_body(sedx_handle* h, int64_t B, const Geometry& g, float* ws, co
                       : h->gru_kernel == SEDX_GRU_KERNEL_COOP16 ? 3
                       : h->gru_kernel == SEDX_GRU_KERNEL_KSPLIT ? 4
                       : h->gru_kernel == SEDX_GRU_KERNEL_PAIR ? 5
-                      // AUTO: beside the next batch's conv stack (pipelined) the 8-slice
-                      // kernel holds half the CUs; one batch at a time 16 slices halve
-                      // the recurrence's serial product
-                      : h->gru_kernel == SEDX_GRU_KERNEL_AUTO ? (h->pipelined ? 2 : 3) : 2,
+                      // AUTO: 16 slices (half the recurrence's serial product); on a
+                      // pipelined handle dealt over every XCD (SPREAD, below): beside
+                      // the next batch's conv stack the shorter recurrence then costs
+                      // it less than the 8-slice kernel's half-size footprint
+                      // (12,238-12,303 vs 11,886-11,923 clips/s, profiles/r05za_*)
+                      : h->gru_kernel == SEDX_GRU_KERNEL_AUTO ? 3 : 2,
                       h->gru_err_dev, h->gru_spin, s,
                       // AUTO on a pipelined handle: the recurrence runs beside the
                       // next batch's conv stack, whose items are dealt to the 8
