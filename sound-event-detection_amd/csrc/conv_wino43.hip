@@ -796,9 +796,11 @@ static void launch_w43_f(const float* in, int B, int T, int Cin, int Cout, const
   const int64_t tblocks = (int64_t)B * tb_per_clip;
   int ncu = 256, dev = 0;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-  // 16-channel items (NT 1, bit-identical) when 64-channel ones would not
-  // give every CU one
-  const bool nt1 = (tblocks + 7) / 8 * 8 * (Cout / G::NCH) < ncu;
+  // 16-channel items (NT 1, bit-identical) when 64-channel ones would give
+  // at most a quarter of the CUs one (measured, profiles/r05q_small_batch.log:
+  // at 128 items — b3c2 at B = 4, b4 at B = 8 — NT 1's four times the items
+  // at a quarter the work each were slower; at <= 64 faster)
+  const bool nt1 = (tblocks + 7) / 8 * 8 * (Cout / G::NCH) <= ncu / 4;
   const int ngroups = Cout / (nt1 ? 16 : G::NCH);
   const int64_t nitems = (tblocks + 7) / 8 * 8 * ngroups;
   const int64_t u_bytes = (int64_t)Cin * Cout * 36 * 4;

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 5: small-batch F(2,3) vs F(4,3) per layer (B = 1, 2, 4, 8)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-O=gpurun_out/r05q
+O=gpurun_out/r05q2
 mkdir -p $O
 for b in 1 2 4 8 32; do
   timeout -k 10 200 tools/bin/w43_bench $b 20 > $O/w43_b$b.log 2>&1; rc=$?
