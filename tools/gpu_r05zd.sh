@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round 5: gamma spectrum with twiddles / window read per stage (SEDX_TUNE_GAMMA_SPEC 2 = 4 waves/SIMD,
 # 3 = 5 waves/SIMD): gamma parity tests, then frontend A/B and a kernel trace
+# (historical: variants 2 / 3 were measured slower and removed; this script no longer runs as is)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 O=gpurun_out/r05zd
 mkdir -p $O
