@@ -113,11 +113,11 @@ struct W43Geom {
   static constexpr int USZ = 36 * 4 * NCH;           // dwords per U slot ([p][k][m][nt])
   static constexpr int NB = 3;                       // ring depth (U and halo)
   // epilogue exchange per round, per tile group, in the U slot freed by the
-  // item's last step: STORE [row 6][reg 2][kc 4][16 tiles + 1 pad][4 z] (the
-  // pad: a finisher's reads of 4 kc x 16 (tile, column) words hit 64
-  // banks), else [row 6][reg 2][z pair 2][lane 64][2] (a finisher's
+  // item's last step: STORE [row 6][reg 2][kc 4][16 tiles + 4 pad][4 z] (the
+  // pad: a finisher's reads of 4 kc x 16 consecutive (tile, column) words
+  // hit 64 banks), else [row 6][reg 2][z pair 2][lane 64][2] (a finisher's
   // ds_read_b64 of its own pair: conflict-free)
-  static constexpr int XRS = 4 * 68;
+  static constexpr int XRS = 4 * 80;
   static constexpr int XTG = 6 * 2 * XRS;
   static constexpr int U_OFF = 0, H_OFF = NB * USZ, BIAS_OFF = H_OFF + NB * HALO, BIAS_MAX = 512;
   static constexpr int HTRASH_OFF = BIAS_OFF + BIAS_MAX;   // 64 dwords: wave 11's halo DMAs
@@ -574,9 +574,9 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
     asm volatile("" : "+v"(le));   // opaque: offsets computed here, not hoisted as live registers
     const int kc = le >> 4;
     // STORE: z of (row, register s) of lane (kc', tile n') = 4 words at
-    // xs(row, s) + 68 kc' + 4 n'; else pair bp of this lane at xp(row, s, bp)
+    // xs(row, s) + 80 kc' + 4 n'; else pair bp of this lane at xp(row, s, bp)
     auto xs = [&](int row, int s) { return (row * 2 + s) * G::XRS; };
-    const int xl = 68 * kc + 4 * (le & 15);   // this lane's STORE entry
+    const int xl = 80 * kc + 4 * (le & 15);   // this lane's STORE entry
     auto xp = [&](int row, int s, int bp) { return ((row * 2 + s) * 2 + bp) * 128 + 2 * le; };
     const int trg = t0 / 4 + tr;   // the lane's tile row in the clip
     w43_f32x4 ost[NT];             // POOL2 / FMEAN: one 4-channel group per channel tile
@@ -668,13 +668,14 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
             ost[nt][r] = ((tf & 1) ? other + sum : sum + other) * (1.0f / F);
           } else if constexpr (EPI == EPI_STORE) {
             // output row a = ROW; for store j the lane computes column
-            // c = lane & 3 of tile (lane & 12) | j — another lane's z — so the
-            // 4 lanes of a quad hold one tile row's 4 pixels (64 contiguous
-            // bytes of a 4-channel group) per store instruction
+            // c = lane & 3 of tile 4 j + ((lane >> 2) & 3) — another lane's
+            // z — so the 16 lanes of a kc hold 16 consecutive pixels of a
+            // tile-group row (256 contiguous bytes of a 4-channel group, or
+            // two 128-byte rows at F = 8) per store instruction
             const int c = le & 3;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-              const float* src = xb + 68 * kc + 4 * ((le & 12) | j) + c;
+              const float* src = xb + 80 * kc + 4 * (4 * j + ((le >> 2) & 3)) + c;
               float col[6], yy[4];
 #pragma unroll
               for (int i = 0; i < 6; ++i) col[i] = src[xs(i, s)];
@@ -708,7 +709,7 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
           if (q & 1) {   // the channel tile's 4 registers done: 4 tiles' pixels x 4 channels
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-              const int tj = (le & 12) | j;   // the tile of store j
+              const int tj = 4 * j + ((le >> 2) & 3);   // the tile of store j
               const int trj = (F == 16 ? 4 * tg : F == 8 ? 8 * tg : F == 64 ? tg : 0) + tj / G::TFG;
               const int tfj = (F == 32 ? 4 * tg : 0) + tj % G::TFG;
               const int t = 4 * (t0 / 4 + trj) + ROW, f = 4 * tfj + (le & 3);
