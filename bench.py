@@ -451,7 +451,7 @@ def stage_times_isolated(model, wave, dev, reps):
 # from the rocprofv3 passes of this bench command (tools/profile_round.sh ->
 # tools/pmc_summary.py; FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE),
 # committed under profiles/.
-PROFILE_SUMMARY = os.path.join(REPO, 'profiles', 'r05w_winograd_kernel_summary.json')
+PROFILE_SUMMARY = os.path.join(REPO, 'profiles', 'r05zl_winograd_kernel_summary.json')
 # the same passes over the config-4 leg (bench.py --mode gamma: B = 32 x 10 s
 # @ 32 kHz, T = 994 frames)
 GAMMA_PROFILE_SUMMARY = os.path.join(REPO, 'profiles', 'r05w_config4_kernel_summary.json')
