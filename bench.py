@@ -823,6 +823,32 @@ class StubModel:
         return {'framewise_output': fw, 'clipwise_output': fw.max(dim=1).values}
 
 
+def rank0_cpu_baseline(args, world, rank, run):
+    """The CPU baseline on rank 0 only, after every timed leg, at any N: the
+    other ranks go on to the closing barrier and wait there while rank 0
+    times the oracle (so the N > 1 line carries cpu_baseline too; its sample
+    is the same bounded B = 32 oracle run as at N = 1, on rank 0's host
+    threads)."""
+    if rank != 0 or args.no_cpu_baseline:
+        return None
+    return run()
+
+
+def stub_cpu_baseline(B):
+    """--stub: the StubModel forward timed on the host (the shape of the real
+    record: value / unit / cores / kind / sample)."""
+    m = StubModel()
+    wave = torch.from_numpy(synth.make_waveforms(B, 0.1, 16000, seed=7))
+    ts = []
+    for _ in range(3):
+        a = time.perf_counter()
+        m(wave)
+        ts.append(time.perf_counter() - a)
+    return {'value': round(B * len(ts) / max(sum(ts), 1e-9), 3), 'unit': 'clips/s',
+            'cores': torch.get_num_threads(), 'kind': 'port', 'stub': True,
+            'sample': '3 iterations of the CPU stand-in model at B=%d' % B}
+
+
 def stub_main(args, world, rank):
     """--stub: the launcher + clip_leg's N > 1 branch (gather to rank 0 in
     every step, barrier, all_reduce(MAX) of the elapsed time) on the CPU."""
@@ -840,11 +866,13 @@ def stub_main(args, world, rank):
         dist.gather_object(env, envs, dst=0)
     else:
         envs = [env]
+    cpu = rank0_cpu_baseline(args, world, rank, lambda: stub_cpu_baseline(args.batch))
     if rank == 0:
         print(json.dumps({'metric': 'stub', 'value': round(value, 3), 'unit': 'clips/s', 'n_gpus': world,
                           'steps': args.steps, 'warmup': args.warmup,
                           'ms_per_step': round(elapsed / args.steps * 1e3, 4), 'stub': True,
-                          'rank_env': envs, 'configs': {'config5': c5}}))
+                          'config': {'world_size': dist.get_world_size() if world > 1 else 1},
+                          'cpu_baseline': cpu, 'rank_env': envs, 'configs': {'config5': c5}}))
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
@@ -1043,13 +1071,15 @@ def main():
         model.set_precision(args.precision)
         extra['configs'] = cfgs
 
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    def run_cpu():
         progress('cpu baseline (%d threads)' % cpu_threads())
-        cpu = cpu_baseline(name, model, dev, args.cpu_seconds, B)
-        if args.mode == 'clip' and not args.no_side:
+        c = cpu_baseline(name, model, dev, args.cpu_seconds, B)
+        if args.mode == 'clip' and not args.no_side and world == 1:
             progress('cpu baseline, window mode')
-            cpu['window_mode'] = cpu_baseline_window(name, min(args.cpu_seconds, 10.0))
+            c['window_mode'] = cpu_baseline_window(name, min(args.cpu_seconds, 10.0))
+        return c
+
+    cpu = rank0_cpu_baseline(args, world, rank, run_cpu)
 
     if rank == 0:
         line = {
@@ -1067,6 +1097,7 @@ def main():
                        'parallelism': 'dp%d clip-sharded, %s gather of framewise + clipwise to rank 0'
                                       % (world, 'gloo (host copies, all ranks on GPU 0)' if GATHER_CPU else 'RCCL'),
                        'backend': dist.get_backend() if world > 1 else None,
+                       'world_size': dist.get_world_size() if world > 1 else 1,
                        'streams': args.streams,
                        'pipelined': args.streams > 1 and not args.no_pipeline,
                        'gru_kernel': args.gru_kernel if args.model == 'gru' else None,

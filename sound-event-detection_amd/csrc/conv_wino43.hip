@@ -200,7 +200,7 @@ template <int F, int EPI, int ROW, bool C4, int NT>
 __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, int T, int Cin, int Cout,
                                          const float* __restrict__ U, int u_bytes, const float* __restrict__ bias,
                                          float* __restrict__ out, float* __restrict__ trash, int tb_per_clip,
-                                         int ngroups, int order2d) {
+                                         int ngroups, int order2d, int wv) {
   using G = W43Geom<F>;
   constexpr int RS = G::RS, PS = G::PS;
   static_assert(NT == 4 || NT == 1, "channel tiles per item");
@@ -209,9 +209,12 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
   auto g64 = [](int g_) { return NT == 4 ? g_ : g_ >> 2; };   // 64-channel U slab group of channel group g_
   extern __shared__ __attribute__((aligned(16))) float smem[];   // G::LDS_BYTES (dynamic)
 
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // the lane from mbcnt (rematerialised where needed) and the wave from one
+  // readfirstlane: the workitem id itself is dead after these two, so it is
+  // neither kept live nor spilled (a 4-byte scratch spill of it in the
+  // 168-VGPR POOL2 builds put vmcnt(0) drains in the prologue)
+  // (wv: the wave, wave-uniform, read once by the kernel entry)
+  const int lane = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
   const int tg = wv & 1;
   const int kk = lane >> 4, nn = lane & 15;
 
@@ -756,7 +759,7 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
 }
 
 #define SEDX_W43_ROWS(F_, EPI_, C4_, NT_, ...)                         \
-  switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >> 1) {    \
+  switch (wv >> 1) {                                                  \
     case 0: w43_body<F_, EPI_, 0, C4_, NT_>(__VA_ARGS__); break;      \
     case 1: w43_body<F_, EPI_, 1, C4_, NT_>(__VA_ARGS__); break;      \
     case 2: w43_body<F_, EPI_, 2, C4_, NT_>(__VA_ARGS__); break;      \
@@ -771,7 +774,8 @@ __global__ __launch_bounds__(768, 1) void conv3x3_wino43_kernel(const float* __r
                                                                 const float* __restrict__ bias, float* __restrict__ out,
                                                                 float* __restrict__ trash, int tb_per_clip,
                                                                 int ngroups, int order2d) {
-  SEDX_W43_ROWS(F, EPI, C4, NT, in, B, T, Cin, Cout, U, u_bytes, bias, out, trash, tb_per_clip, ngroups, order2d)
+  const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+  SEDX_W43_ROWS(F, EPI, C4, NT, in, B, T, Cin, Cout, U, u_bytes, bias, out, trash, tb_per_clip, ngroups, order2d, wv)
 }
 #undef SEDX_W43_ROWS
 
@@ -824,11 +828,19 @@ static void launch_w43_f(const float* in, int B, int T, int Cin, int Cout, const
       }
     }
   }
+  // Counted vmcnt waits and spills: the chunk-of-4 builds (the product
+  // path) are refused if the compiler ever makes them spill (launch_info
+  // no_scratch; 0 bytes in this build, -Rpass-analysis / the ISA's
+  // ScratchSize).  The NHWC builds (opt-in: SEDX_TUNE_WINO_BLOCK1 0 or 1, the
+  // NHWC A/B of the C4 layout) spill 12-192 bytes in their epilogue index
+  // math: a scratch op the compiler inserts only ever ADDS vector-memory ops
+  // to a wave's in-order count, so a counted wait then retires more of the
+  // older DMAs than it names, never fewer — stricter, not looser.
 #define SEDX_W43_LAUNCH(E)                                                                                 \
   {                                                                                                        \
     auto* k_ = nt1 ? (c4 ? conv3x3_wino43_kernel<F, E, true, 1> : conv3x3_wino43_kernel<F, E, false, 1>)   \
                    : (c4 ? conv3x3_wino43_kernel<F, E, true, 4> : conv3x3_wino43_kernel<F, E, false, 4>);  \
-    if (!launch_info(reinterpret_cast<const void*>(k_), G::THREADS, G::LDS_BYTES).ok) return;              \
+    if (!launch_info(reinterpret_cast<const void*>(k_), G::THREADS, G::LDS_BYTES, c4).ok) return;          \
     hipLaunchKernelGGL(k_, dim3((unsigned)nwg), dim3(G::THREADS), G::LDS_BYTES, s, in, B, T, Cin, Cout, U, \
                        (int)u_bytes, bias, out, trash, tb_per_clip, ngroups, order2d);                     \
     return;                                                                                                \

@@ -200,7 +200,11 @@ struct LaunchInfo {
   size_t dyn = 0;
 };
 // dyn_need: dynamic LDS the kernel uses (set as its maximum once).
-inline LaunchInfo launch_info(const void* kernel, int block_threads, size_t dyn_need) {
+// no_scratch: the kernel's counted vmcnt waits assume it issues no scratch
+// (register spill) loads / stores, which would count in vmcnt too and make
+// the waits too loose (LDS read before its DMA landed: silently wrong
+// outputs).  A build that spills is refused here, loudly, instead.
+inline LaunchInfo launch_info(const void* kernel, int block_threads, size_t dyn_need, bool no_scratch = false) {
   static std::mutex mu;
   static std::map<std::pair<int, const void*>, LaunchInfo> cache;
   int dev = 0;
@@ -227,6 +231,17 @@ inline LaunchInfo launch_info(const void* kernel, int block_threads, size_t dyn_
       hipSuccess) {
     note_launch_error(e);
     return LaunchInfo{};
+  }
+  if (no_scratch) {
+    hipFuncAttributes fa{};
+    if ((e = hipFuncGetAttributes(&fa, kernel)) != hipSuccess) {
+      note_launch_error(e);
+      return LaunchInfo{};
+    }
+    if (fa.localSizeBytes != 0) {
+      note_launch_error(hipErrorInvalidDeviceFunction);
+      return LaunchInfo{};
+    }
   }
   if (li.per_cu < 1) li.per_cu = 1;
   if (li.ncu < 1) li.ncu = 256;

@@ -133,6 +133,11 @@ def lib():
         'sedx_resample_workspace_size': ([I64, I32, I32, I32, PSZ], I32),
         'sedx_resample': ([P, I64, I32, I32, I32, P, P, SZ, P], I32),
     }
+    # an ABI <= 4 library has no sedx_abi_version (nor later entry points):
+    # say "rebuild" before the argtypes loop trips over a missing symbol
+    if not hasattr(L, 'sedx_abi_version'):
+        raise RuntimeError('libsedx.so ABI <= 4 (no sedx_abi_version), this binding expects %d '
+                           '(include/sedx.h SEDX_ABI_VERSION): rebuild the library' % ABI_VERSION)
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
         fn.argtypes = args

@@ -314,7 +314,9 @@ class _SedModel(nn.Module):
         """GEMM arithmetic (conv stack, GRU / MHA projections and recurrence,
         AttBlock projection): 'winograd' (default; fp32 operands, transforms
         and accumulation, block 1's conv2 and blocks 2-4 as Winograd
-        F(2x2,3x3): error vs float64 at or below the direct conv's), 'exact'
+        F(4x4,3x3) — _lib.TUNE_WINO_F43 0 / 1 select F(2x2,3x3) in every layer
+        / in block 1 only; error vs float64 max <= 2.5e-5, rms <= 1.7e-6 per
+        layer), 'exact'
         (fp32 direct convolution, the reference's operation order) or 'x3'
         (opt-in; 3xbf16-split MFMA, fp32 accumulate, ~1e-6 from fp32)."""
         if mode not in _lib.PRECISION:

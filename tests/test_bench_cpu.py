@@ -187,6 +187,13 @@ def test_bench_launches_n_ranks(n):
     assert c5['backend'] == 'gloo' and 'clipwise' in c5['gathered']
     assert 'Transformer' in c5['metric'] and c5['scaling'] == 'weak'
     assert abs(c5['value'] - n * B * steps / (c5['ms_per_step'] * steps / 1e3)) <= 0.01 * c5['value'] + 1e-3
+    # the N > 1 line is complete: rank 0 times the CPU baseline after the
+    # timed legs (the other ranks wait at the closing barrier), and the
+    # process group's world size is recorded
+    cpu = d['cpu_baseline']
+    assert cpu is not None and cpu['value'] > 0 and cpu['unit'] == 'clips/s' and cpu['kind'] == 'port'
+    assert cpu['cores'] >= 1 and cpu['sample']
+    assert d['config']['world_size'] == n
 
 
 def test_bench_launcher_fails_when_a_rank_fails():

@@ -96,6 +96,32 @@ def test_batch32_vs_oracle(model):
         assert e <= TOL * scale
 
 
+@pytest.mark.parametrize('f43', [0, 1, 2], ids=['f23', 'f43b24', 'f43'])
+@pytest.mark.parametrize('mt', [GRU, TRF])
+def test_batch32_vs_oracle_wino_forms(mt, f43):
+    """test_batch32_vs_oracle for every Winograd form (SEDX_TUNE_WINO_F43):
+    the headline batch against the CPU oracle at the Winograd bar (2e-5, far
+    inside north_star's 1e-3), with the oracle's thresholded events, and a
+    ragged 7.33 s batch (partial last tile rows, odd rows dropped by the
+    pools) at the same bar."""
+    from sedx import inference
+    m = build_prec(mt, 'winograd', f43)
+    st = O.full_state(synth.make_state_dict(mt, seed=SEEDS[mt]))
+    params = {'sed_high_threshold': 0.5, 'sed_low_threshold': 0.3, 'n_smooth': 10, 'n_salt': 10}
+    for n, sec, seed in ((32, 10.0, 4321), (3, 7.33, 5)):
+        wave = synth.make_waveforms(n, seconds=sec, sample_rate=16000, seed=seed)
+        out = run(m, wave)
+        ref = O.forward(st, mt, wave=wave)
+        for k in ('framewise_output', 'clipwise_output', 'embedding'):
+            assert np.isfinite(out[k]).all(), k
+            scale = max(1.0, float(ref[k].abs().max()))
+            e = err(out[k], ref[k].numpy())
+            print(mt, 'f43=%d' % f43, 'B=%d' % n, k, 'max|d| =', e)
+            assert e <= 2e-5 * scale, (k, e)
+        ev = inference.events_from_framewise(out['framewise_output'], params)
+        assert ev == inference.events_from_framewise(ref['framewise_output'].numpy(), params)
+
+
 @pytest.mark.parametrize('seconds', [61.3])
 def test_long_clip_vs_oracle(model, seconds):
     """A long, ragged clip (6131 frames: many t-tiles per clip, the last one
@@ -645,15 +671,30 @@ def ctypes_ptr(t):
     return ctypes.c_void_p(t.data_ptr())
 
 
-@pytest.mark.parametrize('prec', ['exact', 'x3', 'winograd'])
+# Winograd forms (SEDX_TUNE_WINO_F43): 0 = F(2x2,3x3) in every layer (block 1
+# the fused conv1 + F(2,3) launch, blocks 2-4 conv_wino.hip), 1 = block 1 on
+# F(2,3) and blocks 2-4 on F(4x4,3x3), 2 = F(4x4,3x3) everywhere (default)
+WINO_FORMS = [('exact', None), ('x3', None), ('winograd', 0), ('winograd', 1), ('winograd', 2)]
+WINO_IDS = ['exact', 'x3', 'wino-f23', 'wino-f43b24', 'wino-f43']
+
+
+def build_prec(mt, prec, f43=None):
+    m = build(mt).set_precision(prec)
+    if f43 is not None:
+        from sedx import _lib
+        m.set_tuning(_lib.TUNE_WINO_F43, f43)
+    return m
+
+
+@pytest.mark.parametrize('prec,f43', WINO_FORMS, ids=WINO_IDS)
 @pytest.mark.parametrize('mt', [GRU, TRF])
-def test_stage_goldens(mt, prec, golden_dir):
+def test_stage_goldens(mt, prec, f43, golden_dir):
     """Every stage of the HIP path against the reference's own per-stage
     activations (tests/golden/stages_*.npz): bn0 output, the pooled output of
     blocks 1-3, block 4 + freq mean and the GRU / MHA output, so a
-    regression names its stage."""
+    regression names its stage.  Every Winograd form is checked."""
     g = np.load(os.path.join(golden_dir, 'stages_%s.npz' % mt))
-    m = build(mt).set_precision(prec)
+    m = build_prec(mt, prec, f43)
     wave = g['wave']
     B = wave.shape[0]
     T = g['bn0'].shape[2]
@@ -693,25 +734,33 @@ def test_mel_mfma_bit_identical(n_clips, seconds):
     assert np.array_equal(x0[1], x0[0])
 
 
+@pytest.mark.parametrize('f43', [0, 1, 2], ids=['f23', 'f43b24', 'f43'])
 @pytest.mark.parametrize('mt', [GRU, TRF])
-def test_winograd_vs_exact(mt):
-    """fp32 Winograd F(2x2,3x3) conv (blocks 2-4) against the direct fp32 conv
-    on the headline batch: same arithmetic type, different rounding — the two
-    agree far inside the 1e-3 bar, the thresholded events are identical, and
-    both sit at the same distance from the oracle."""
+def test_winograd_vs_exact(mt, f43):
+    """Each fp32 Winograd form (SEDX_TUNE_WINO_F43 0: F(2x2,3x3) in every
+    layer; 1: block 1 F(2x2,3x3), blocks 2-4 F(4x4,3x3); 2, the default:
+    F(4x4,3x3) everywhere) against the direct fp32 conv and the CPU oracle on
+    the headline batch (B = 32 x 10 s): same arithmetic type, different
+    rounding — framewise within 2e-5 of both, and the thresholded events of
+    the Winograd form, the direct conv and the oracle all identical."""
     from sedx import inference
     wave = synth.make_waveforms(32, seconds=10.0, sample_rate=16000, seed=4321)
     ex = run(build(mt).set_precision('exact'), wave)
-    wg = run(build(mt).set_precision('winograd'), wave)
+    wg = run(build_prec(mt, 'winograd', f43), wave)
     ref = O.forward(O.full_state(synth.make_state_dict(mt, seed=SEEDS[mt])), mt, wave=wave)
+    for k in ('framewise_output', 'clipwise_output', 'embedding'):
+        assert np.isfinite(wg[k]).all(), k
     e_we = err(wg['framewise_output'], ex['framewise_output'])
     e_w = err(wg['framewise_output'], ref['framewise_output'].numpy())
     e_e = err(ex['framewise_output'], ref['framewise_output'].numpy())
-    print(mt, 'winograd vs exact %.3g, vs oracle %.3g (exact vs oracle %.3g)' % (e_we, e_w, e_e))
-    assert e_we <= 2e-5 and e_w <= 2e-5
+    e_c = err(wg['clipwise_output'], ref['clipwise_output'].numpy())
+    print(mt, 'f43=%d winograd vs exact %.3g, vs oracle %.3g (clipwise %.3g; exact vs oracle %.3g)'
+          % (f43, e_we, e_w, e_c, e_e))
+    assert e_we <= 2e-5 and e_w <= 2e-5 and e_c <= 2e-5
     params = {'sed_high_threshold': 0.5, 'sed_low_threshold': 0.3, 'n_smooth': 10, 'n_salt': 10}
     ev = inference.events_from_framewise(wg['framewise_output'], params)
     assert len(ev) > 0 and ev == inference.events_from_framewise(ex['framewise_output'], params)
+    assert ev == inference.events_from_framewise(ref['framewise_output'].numpy(), params)
 
 
 def test_config5_transformer_b256():

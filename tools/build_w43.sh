@@ -1,12 +1,13 @@
 #!/bin/bash
-# Build tools/bin/w43_bench (+ variants) here on the CPU: the F(2,3) / direct
+# Build tools/run/w43_bench (+ variants) here on the CPU (OUT=dir to override;
+# tools/run travels to the GPU box, tools/bin does not — empty tools/run after use): the F(2,3) / direct
 # conv objects once, conv_wino43.hip per variant.
-#   tools/build_w43.sh                 -> tools/bin/w43_bench
+#   tools/build_w43.sh                 -> tools/run/w43_bench
 #   VARIANTS="abl1:-DSEDX_W43_ABL=1 abl2:-DSEDX_W43_ABL=2" tools/build_w43.sh
 set -e
 cd "$(dirname "$0")/.."
 C=sound-event-detection_amd/csrc
-O=tools/bin
+O=${OUT:-tools/run}
 mkdir -p $O
 H="/opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -Wno-unused-result -Wno-unused-value -fno-slp-vectorize -fno-vectorize -I$C"
 for src in conv conv_wino; do

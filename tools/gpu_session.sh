@@ -1,0 +1,44 @@
+#!/bin/bash
+# One gpurun call made of named steps (replaces round 5's per-call one-off
+# scripts):  tools/gpu_session.sh TAG STEP [STEP ...]
+# Outputs go under gpurun_out/TAG/<step>.log.  Every step runs under its own
+# time limit; the session stops at the first step that fails, faults, aborts
+# or times out (no retries).
+#   smoke          __graft_entry__ build() + smoke()
+#   tests          pytest -m gpu (all GPU tests)
+#   tests=EXPR     pytest -m gpu -k EXPR  (',' in EXPR reads as ' ')
+#   bench          python bench.py (default command)
+#   bench=ARGS     python bench.py ARGS   (',' in ARGS reads as ' ')
+#   w43=B          tools/run/w43_bench B 20 (build first: tools/build_w43.sh)
+#   w43v=NAME:B    tools/run/w43_bench_NAME B 20 (a VARIANTS build)
+#   prof           tools/profile_round.sh (rocprof kernel trace + PMC passes; env as there)
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+TAG=${1:?tag}; shift
+O=gpurun_out/$TAG
+mkdir -p "$O"
+n=0
+step() {  # name timeout cmd...
+  local name=$1 t=$2; shift 2
+  n=$((n + 1))
+  echo "== [$n] $name: $*"
+  timeout -k 10 "$t" "$@" > "$O/$n.$name.log" 2>&1
+  local rc=$?
+  echo "== [$n] $name rc=$rc"; tail -n ${TAIL:-12} "$O/$n.$name.log" | cut -c1-400
+  if [ $rc -ne 0 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+}
+for s in "$@"; do
+  arg=${s#*=}; arg=${arg//,/ }
+  case $s in
+    smoke) step smoke 300 python -u -c "import __graft_entry__ as g; g.build(); g.smoke()" ;;
+    tests) step pytest 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ;;
+    tests=*) step pytest 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "$arg" ;;
+    bench) step bench 600 python -u bench.py ;;
+    bench=*) step bench 600 python -u bench.py $arg ;;
+    w43=*) step w43_b$arg 200 tools/run/w43_bench $arg 20 ;;
+    w43v=*) v=${arg%%:*}; b=${arg#*:}; step w43_${v}_b$b 200 tools/run/w43_bench_$v $b 20 ;;
+    prof) step prof 1100 tools/profile_round.sh ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
+echo "== session $TAG done"
