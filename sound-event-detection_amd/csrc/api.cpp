@@ -926,7 +926,7 @@ sedx_status sedx_finalize_weights(sedx_handle* h) {
         packed_wu[idx].assign((size_t)cin * cout * 16, 0.f);
         pack_conv_wino(wf.data(), cin, cout, packed_wu[idx].data());
         {   // block 1's conv2 and blocks 2-4: the F(4x4,3x3) pack as well
-          packed_wu43[idx].assign((size_t)cin * cout * 36, 0.f);
+          packed_wu43[idx].assign((size_t)2 * cin * cout * 36, 0.f);
           pack_conv_wino43(wf.data(), cin, cout, packed_wu43[idx].data());
         }
       }

@@ -111,6 +111,7 @@ struct W43Geom {
   static constexpr int PS = 64 * HB + 2;             // plane stride, = 2 mod 4 (odd bank pairs for odd k)
   static constexpr int HALO = 4 * PS;                // dwords per halo slot
   static constexpr int USZ = 36 * 4 * NCH;           // dwords per U slot ([p][k][m][nt])
+  static constexpr int USZ1 = 36 * 4 * 16;           // NT 1: one 16-channel tile's slab ([p][k][m]), 9 KiB
   static constexpr int NB = 3;                       // ring depth (U and halo)
   // epilogue exchange per round, per tile group, in the U slot freed by the
   // item's last step: STORE [row 6][reg 2][kc 4][16 tiles + 4 pad][4 z] (the
@@ -194,8 +195,14 @@ __device__ __forceinline__ void w43_at(const float (&m)[6], float (&z)[4]) {
 // NT: channel tiles per item.  4 (64 channels) on full grids; 1 (16 channels,
 // the launcher's choice when the 64-channel items would leave CUs idle,
 // e.g. one clip): four times the items, each tile's accumulation chain the
-// same instructions in the same order — bit-identical to NT 4.  An item
-// still DMAs its 64-channel U slab and reads its 16 channels' words.
+// same instructions in the same order — bit-identical to NT 4.  An NT 1 item
+// DMAs only its 16 channels' U slab (9 KiB per chunk, from the second,
+// [Cout/16][Cin/4][36][4][16] pack that follows the NT 4 pack): one 1 KiB
+// unit per wave (waves 9-11 read out of range into the slot's unused tail),
+// 5 DMAs per wave per step instead of 7.  NT 1 items are dealt over all
+// eight XCDs (channel tile g on XCD g mod 8, every tile block of it there):
+// at one clip the 512-channel layers have 2 tile blocks, which the tile
+// block-major decode put on two XCDs.
 template <int F, int EPI, int ROW, bool C4, int NT>
 __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, int T, int Cin, int Cout,
                                          const float* __restrict__ U, int u_bytes, const float* __restrict__ bias,
@@ -206,7 +213,7 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
   static_assert(NT == 4 || NT == 1, "channel tiles per item");
   // a U fragment: the lane's words of its NT channel tiles
   using UF = typename std::conditional<NT == 4, w43_f32x4, float>::type;
-  auto g64 = [](int g_) { return NT == 4 ? g_ : g_ >> 2; };   // 64-channel U slab group of channel group g_
+  constexpr int VM = NT == 4 ? G::VM : 5;   // DMAs per wave per step: U units + 4 halo planes
   extern __shared__ __attribute__((aligned(16))) float smem[];   // G::LDS_BYTES (dynamic)
 
   // the lane from mbcnt (rematerialised where needed) and the wave from one
@@ -224,6 +231,14 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
   auto decode = [&](int item, int& b_, int& t0_, int& g_) -> bool {
     const int xcd = item & 7, j = item >> 3;
     int jb, cgi;
+    if constexpr (NT == 1) {   // channel tile 8 gi + xcd, tile block j mod tblocks
+      const int tbl = B * tb_per_clip, gi = j / tbl, tb = j - gi * tbl;
+      g_ = 8 * gi + xcd;
+      if (g_ >= ngroups) return false;
+      b_ = tb / tb_per_clip;
+      t0_ = 4 * G::TRW * (tb - b_ * tb_per_clip);
+      return true;
+    }
     if (order2d) {
       const int tbr = 32 / order2d;
       const int idx = j & 31, r = j >> 5, ncg = ngroups / order2d;
@@ -266,11 +281,20 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
     return ok ? (uint32_t)((((b_ * T + t) * F + f) * Cin) * 4) : 0x80000000u;
   };
   const uint32_t u_voff = 16 * lane + 1024 * wv;
+  // NT 1: waves 9-11 have no unit (out of range: zeros into the slot's tail)
+  const uint32_t u_voff1 = wv < 9 ? u_voff : 0x80000000u;
   const uint32_t bytes_per_chunk_u = 4 * G::USZ;
   // DMA of chunk cc of an item (halo offsets hof, channel group g_) into the
   // given slots; U units wv, wv + 12, wv + 24 and this wave's halo block
   auto dma_u = [&](int g_, int cc, int uslot) {
     if constexpr (SEDX_W43_ABL & 2) return;
+    if constexpr (NT == 1) {   // unit wv of the 9 KiB slab (the 16-channel pack after the NT 4 pack)
+      const uint32_t so = __builtin_amdgcn_readfirstlane(
+          (uint32_t)(u_bytes / 2 + (g_ * nchunks + cc) * (4 * G::USZ1)));
+      const uint32_t m0 = __builtin_amdgcn_readfirstlane(w43_lds_addr(smem + G::U_OFF + uslot * G::USZ + 256 * wv));
+      w43_dma16(u_voff1, r_u, so, m0);
+      return;
+    }
     const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)((g_ * nchunks + cc) * bytes_per_chunk_u));
     const uint32_t m0 = __builtin_amdgcn_readfirstlane(w43_lds_addr(smem + G::U_OFF + uslot * G::USZ + 256 * wv));
 #pragma unroll
@@ -311,9 +335,9 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
   }
   uint32_t hof = halo_off(b, t0);
   dma_h(hof, 0, 0);
-  dma_u(g64(grp), 0, 0);
+  dma_u(grp, 0, 0);
   dma_h(hof, 1, 1);
-  dma_u(g64(grp), 1, 1);
+  dma_u(grp, 1, 1);
   dma_h(hof, 2, 2);
   if constexpr (S > 0) {
     float* const vt = tr_lane;   // exactly S stores (never merged), as the epilogue's
@@ -356,7 +380,7 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
     if constexpr (NT == 4)
       asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(u) : "v"(a), "n"(4 * (6 * ROW + J) * 256));
     else
-      asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(u) : "v"(a), "n"(4 * (6 * ROW + J) * 256));
+      asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(u) : "v"(a), "n"(4 * (6 * ROW + J) * 64));
   };
   auto wait_u = [](auto n_tag, UF& u) {
     asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(u) : "n"(decltype(n_tag)::value));
@@ -411,8 +435,8 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
   using I4 = std::integral_constant<int, 4>;
   using I5 = std::integral_constant<int, 5>;
   const uint32_t h_lane = w43_lds_addr(smem + G::H_OFF + p_base);     // + slot * 4 HALO
-  // + slot * 4 USZ; NT 1: + the item's 16-channel tile (grp & 3)
-  uint32_t u_lane = w43_lds_addr(smem + G::U_OFF + 4 * lane + (NT == 1 ? (grp & 3) : 0));
+  // + slot * 4 USZ; NT 4: the lane's 4 channel tiles' words, NT 1: its word
+  const uint32_t u_lane = w43_lds_addr(smem + G::U_OFF + (NT == 1 ? lane : 4 * lane));
   // V of the lane's 6 positions for the chunk in halo slot hs_ (item top: no
   // MFMAs to hide behind)
   auto transform = [&](int hs_, float (&v)[6]) {
@@ -449,7 +473,7 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
 
   // the first item's chunk 0: halo(0) landed (younger: the groups of steps
   // -2, -1 and the S dummy stores)
-  w43_bar<2 * G::VM + S>();
+  w43_bar<2 * VM + S>();
 #ifdef SEDX_W43_STAMPS
   unsigned long long w43_st[5] = {0, 0, 0, 0, 0};
   unsigned long long w43_t = __builtin_amdgcn_s_memtime();
@@ -485,7 +509,7 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
       constexpr int NP0 = LASTSTEP ? 0 : (PB >= 0 ? 6 : 3), NP = LASTSTEP ? 0 : 3;
       // U(c) and halo(c + 1) landed: issued two steps ago; younger: the
       // previous step's group (+ the epilogue stores over an item's first two steps)
-      w43_bar<G::VM + (FIRST ? S : 0)>();
+      w43_bar<VM + (FIRST ? S : 0)>();
       const int us1 = us == 2 ? 0 : us + 1, us2 = us1 == 2 ? 0 : us1 + 1;
       const int hs1 = hs == 2 ? 0 : hs + 1;
       const uint32_t ua = u_lane + us * (4 * G::USZ);
@@ -497,8 +521,8 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
       read_u(ua, I1{}, u1);
       // group of step c: U(c + 2) -> the U slot of c - 1, halo(c + 3) -> the
       // halo slot of c (read during step c - 1)
-      if (c + 2 < nchunks) dma_u(g64(grp), c + 2, us2);
-      else dma_u(g64(ng), c + 2 - nchunks, us2);
+      if (c + 2 < nchunks) dma_u(grp, c + 2, us2);
+      else dma_u(ng, c + 2 - nchunks, us2);
       if (c + 3 < nchunks) dma_h(hof, c + 3, hs);
       else dma_h(nhof, c + 3 - nchunks, hs);
       fence();
@@ -747,7 +771,6 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
     t0 = nt0;
     grp = ng;
     hof = nhof;
-    if constexpr (NT == 1) u_lane = w43_lds_addr(smem + G::U_OFF + 4 * lane + (grp & 3));
   }
 #ifdef SEDX_W43_STAMPS
   if (lane == 0 && (blockIdx.x & 15) == 0) {
@@ -792,7 +815,7 @@ __global__ __launch_bounds__(768, 1) void conv3x3_wino43_kernel(const float* __r
 
 template <int F>
 static void launch_w43_f(const float* in, int B, int T, int Cin, int Cout, const float* U, const float* bias,
-                         float* out, int epi, float* trash, int order, bool c4, hipStream_t s) {
+                         float* out, int epi, float* trash, int order, bool c4, int nt_force, hipStream_t s) {
   using G = W43Geom<F>;
   // output rows the epilogue covers: POOL2 drops an odd last row
   const int rows = epi == EPI_POOL2 ? 2 * (T / 2) : T;
@@ -805,10 +828,11 @@ static void launch_w43_f(const float* in, int B, int T, int Cin, int Cout, const
   // at most a quarter of the CUs one (measured, profiles/r05q_small_batch.log:
   // at 128 items — b3c2 at B = 4, b4 at B = 8 — NT 1's four times the items
   // at a quarter the work each were slower; at <= 64 faster)
-  const bool nt1 = (tblocks + 7) / 8 * 8 * (Cout / G::NCH) <= ncu / 4;
+  const bool nt1 = nt_force ? nt_force == 1 : (tblocks + 7) / 8 * 8 * (Cout / G::NCH) <= ncu / 4;
   const int ngroups = Cout / (nt1 ? 16 : G::NCH);
-  const int64_t nitems = (tblocks + 7) / 8 * 8 * ngroups;
-  const int64_t u_bytes = (int64_t)Cin * Cout * 36 * 4;
+  // NT 1: 8 XCD lanes x ceil(groups / 8) channel tiles x every tile block
+  const int64_t nitems = nt1 ? 8 * ((ngroups + 7) / 8) * tblocks : (tblocks + 7) / 8 * 8 * ngroups;
+  const int64_t u_bytes = 2 * (int64_t)Cin * Cout * 36 * 4;   // the NT 4 pack, then the NT 1 pack
   if (nitems > INT32_MAX || tblocks <= 0 || (int64_t)B * T * F * Cin * 4 >= INT32_MAX || u_bytes >= INT32_MAX)
     return note_launch_error(hipErrorInvalidValue);
   const int64_t resident = (int64_t)ncu / 8 * 8;
@@ -859,7 +883,8 @@ static void launch_w43_f(const float* in, int B, int T, int Cin, int Cout, const
 }
 
 void launch_conv3x3_wino43(const float* in, int B, int T, int F, int Cin, int Cout, const float* U43,
-                           const float* bias, float* out, int epi, float* trash, hipStream_t s, int order, bool c4) {
+                           const float* bias, float* out, int epi, float* trash, hipStream_t s, int order, bool c4,
+                           int nt_force) {
   if (Cin % 8 != 0 || Cin < 16 || Cout % 64 != 0 || Cout > 512 || B <= 0 || T <= 0)
     return note_launch_error(hipErrorInvalidValue);
   // byte offsets are 32-bit (buffer DMA): batches whose input passes 2^31
@@ -874,10 +899,10 @@ void launch_conv3x3_wino43(const float* in, int B, int T, int F, int Cin, int Co
     const float* in_s = in + b0 * in_clip;
     float* out_s = out + b0 * out_clip;
     switch (F) {
-      case 64: launch_w43_f<64>(in_s, bs, T, Cin, Cout, U43, bias, out_s, epi, trash, order, c4, s); break;
-      case 32: launch_w43_f<32>(in_s, bs, T, Cin, Cout, U43, bias, out_s, epi, trash, order, c4, s); break;
-      case 16: launch_w43_f<16>(in_s, bs, T, Cin, Cout, U43, bias, out_s, epi, trash, order, c4, s); break;
-      case 8: launch_w43_f<8>(in_s, bs, T, Cin, Cout, U43, bias, out_s, epi, trash, order, c4, s); break;
+      case 64: launch_w43_f<64>(in_s, bs, T, Cin, Cout, U43, bias, out_s, epi, trash, order, c4, nt_force, s); break;
+      case 32: launch_w43_f<32>(in_s, bs, T, Cin, Cout, U43, bias, out_s, epi, trash, order, c4, nt_force, s); break;
+      case 16: launch_w43_f<16>(in_s, bs, T, Cin, Cout, U43, bias, out_s, epi, trash, order, c4, nt_force, s); break;
+      case 8: launch_w43_f<8>(in_s, bs, T, Cin, Cout, U43, bias, out_s, epi, trash, order, c4, nt_force, s); break;
       default: return note_launch_error(hipErrorInvalidValue);
     }
   }
@@ -917,10 +942,12 @@ void launch_c4_to_nhwc(const float* src, int B, int T, int F, int C, float* dst,
 }
 
 // U = G g G^T per (input channel, output channel) in float64 from the
-// BN-folded weights wf [Cout][Cin][9], rounded once to fp32, packed
+// BN-folded weights wf [Cout][Cin][9], rounded once to fp32, packed twice:
 // [Cout/64][Cin/4][36 p][4 k][16 m][4 nt] with output channel 64 group +
 // 16 nt + m and input channel 4 chunk + k (a chunk's slab is the LDS image;
-// lane l = 16 k + m reads its 4 channel tiles as one 16-byte word).
+// lane l = 16 k + m reads its 4 channel tiles as one 16-byte word), then the
+// same values as [Cout/16][Cin/4][36 p][4 k][16 m] (16-channel items: a
+// chunk's 9 KiB slab of one channel tile).  Up: 2 Cin Cout 36 floats.
 void pack_conv_wino43(const double* wf, int Cin, int Cout, float* Up) {
   static const double Gm[6][3] = {{1.0 / 4, 0, 0},
                                   {-1.0 / 6, -1.0 / 6, -1.0 / 6},
@@ -941,6 +968,7 @@ void pack_conv_wino43(const double* wf, int Cin, int Cout, float* Up) {
           const double u = tmp[a][0] * Gm[c][0] + tmp[a][1] * Gm[c][1] + tmp[a][2] * Gm[c][2];
           const int p = 6 * a + c;
           Up[(((((size_t)grp * nch + chunk) * 36 + p) * 4 + k) * 16 + m) * 4 + nt] = (float)u;
+          Up[(size_t)Cin * Cout * 36 + ((((size_t)(o / 16) * nch + chunk) * 36 + p) * 4 + k) * 16 + m] = (float)u;
         }
     }
 }

@@ -128,7 +128,9 @@ void launch_conv3x3_wino(const float* in, int B, int T, int F, int Cin, int Cout
 void pack_conv_wino(const double* wf, int Cin, int Cout, float* U);   // U: Cin * Cout * 16 floats
 // Same contract as fp32 Winograd F(4x4,3x3) (conv_wino43.hip), blocks 2-4:
 // F in {32, 16, 8}, Cin % 8 == 0 and >= 16, Cout % 64 == 0 and <= 512; U43
-// from pack_conv_wino43 (Cin * Cout * 36 floats); pixels outside the clip are
+// from pack_conv_wino43 (2 Cin Cout 36 floats: the 64- and the 16-channel
+// item packs); nt_force: 0 = the launcher's choice of 64- or 16-channel
+// items, 4 / 1 = that one (A/B and tests; bit-identical); pixels outside the clip are
 // zero-filled by the buffer DMA's range check (no zero block); trash >= 64 x
 // 128 floats of device scratch for the out-of-range epilogue stores.
 // c4: input and output in the chunk-of-4 layout [B][C/4][T][F][4] (the
@@ -136,10 +138,10 @@ void pack_conv_wino(const double* wf, int Cin, int Cout, float* U);   // U: Cin 
 // clips, so B-major offsets hold in both layouts.
 void launch_conv3x3_wino43(const float* in, int B, int T, int F, int Cin, int Cout, const float* U43,
                            const float* bias, float* out, int epi, float* trash, hipStream_t s, int order = 0,
-                           bool c4 = false);
+                           bool c4 = false, int nt_force = 0);
 // [B][C/4][T][F][4] -> [B][T][F][C] (stage captures of the C4 layers)
 void launch_c4_to_nhwc(const float* src, int B, int T, int F, int C, float* dst, hipStream_t s);
-void pack_conv_wino43(const double* wf, int Cin, int Cout, float* U);   // U: Cin * Cout * 36 floats
+void pack_conv_wino43(const double* wf, int Cin, int Cout, float* U);   // U: 2 * Cin * Cout * 36 floats
 // block 1 as one Winograd launch: conv1 (w1 [64][9] folded, b1 [64], ReLU)
 // computed into conv2's halo images in LDS, conv2 (U of block 1's conv2) +
 // bias + ReLU + 2x2 pool: X0 [B][T][64] -> [B][T/2][32][64]; bit-identical to

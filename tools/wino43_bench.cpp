@@ -14,7 +14,8 @@
 
 namespace sedx {
 void launch_conv3x3_wino43(const float* in, int B, int T, int F, int Cin, int Cout, const float* U43,
-                           const float* bias, float* out, int epi, float* trash, hipStream_t s, int order, bool c4);
+                           const float* bias, float* out, int epi, float* trash, hipStream_t s, int order, bool c4,
+                           int nt_force);
 void pack_conv_wino43(const double* wf, int Cin, int Cout, float* U);
 #ifdef SEDX_W43_STAMPS
 void w43_stamps_rw(unsigned long long* h, bool reset);
@@ -43,15 +44,15 @@ int main(int argc, char** argv) {
                            {"e8m", 2, 67, 8, 64, 192, sedx::EPI_FMEAN, true},
                            {"e8s", 5, 3, 8, 16, 64, sedx::EPI_STORE, true},
                            {"e64p", 2, 37, 64, 64, 64, sedx::EPI_POOL2, true}};
-  float *d_in, *d_in4, *d_o1, *d_o2, *d_o3, *d_bias, *d_u, *d_u43, *d_zero, *d_trash;
+  float *d_in, *d_in4, *d_o1, *d_o2, *d_o3, *d_o4, *d_bias, *d_u, *d_u43, *d_zero, *d_trash;
   size_t max_in = 0, max_out = 0, max_w = 0;
   for (const Layer& l : LM) {
     max_in = std::max(max_in, (size_t)l.B * l.T * l.F * l.cin);
     max_out = std::max(max_out, (size_t)l.B * l.T * l.F * l.cout);
-    max_w = std::max(max_w, (size_t)l.cin * l.cout * 36);
+    max_w = std::max(max_w, (size_t)2 * l.cin * l.cout * 36);
   }
   hipMalloc(&d_in, max_in * 4); hipMalloc(&d_o1, max_out * 4); hipMalloc(&d_o2, max_out * 4);
-  hipMalloc(&d_in4, max_in * 4); hipMalloc(&d_o3, max_out * 4);
+  hipMalloc(&d_in4, max_in * 4); hipMalloc(&d_o3, max_out * 4); hipMalloc(&d_o4, max_out * 4);
   hipMalloc(&d_bias, 512 * 4); hipMalloc(&d_u, max_w * 4); hipMalloc(&d_u43, max_w * 4);
   hipMalloc(&d_zero, 4096); hipMemset(d_zero, 0, 4096);
   hipMalloc(&d_trash, 64 * 256 * 4);
@@ -59,7 +60,7 @@ int main(int argc, char** argv) {
   hipEventCreate(&e0); hipEventCreate(&e1);
   std::mt19937 rng(7);
   std::normal_distribution<float> nd(0.f, 1.f);
-  double tot_2 = 0, tot_4 = 0, tot_4c = 0;
+  double tot_2 = 0, tot_4 = 0, tot_4c = 0, tot_n1 = 0, tot_n4 = 0;
   bool ok = true;
   for (const Layer& l : LM) {
     if (only && strcmp(only, l.name) != 0) continue;
@@ -70,7 +71,7 @@ int main(int argc, char** argv) {
     const float ws = std::sqrt(2.f / (9 * l.cin));
     for (auto& v : w) v = (double)(float)(nd(rng) * ws);
     for (auto& v : bias) v = 0.1f * nd(rng);
-    std::vector<float> U((size_t)l.cin * l.cout * 16), U43((size_t)l.cin * l.cout * 36);
+    std::vector<float> U((size_t)l.cin * l.cout * 16), U43((size_t)2 * l.cin * l.cout * 36);
     sedx::pack_conv_wino(w.data(), l.cin, l.cout, U.data());
     sedx::pack_conv_wino43(w.data(), l.cin, l.cout, U43.data());
     hipMemcpy(d_in, in.data(), nin * 4, hipMemcpyHostToDevice);
@@ -94,21 +95,37 @@ int main(int argc, char** argv) {
     hipMemset(d_o1, 0xff, nout * 4);
     hipMemset(d_o2, 0xff, nout * 4);
     hipMemset(d_o3, 0xff, nout * 4);
+    hipMemset(d_o4, 0xff, nout * 4);
     const bool with2 = !l.full || l.cin >= 32;   // F(2,3) launcher: Cin >= 32
     auto w2 = [&]() {
       sedx::launch_conv3x3_wino(d_in, l.B, l.T, l.F, l.cin, l.cout, d_u, d_bias, d_o1, l.epi, d_zero, d_trash, 0, order);
     };
     auto w4 = [&]() {
       sedx::launch_conv3x3_wino43(d_in, l.B, l.T, l.F, l.cin, l.cout, d_u43, d_bias, d_o2, l.epi, d_trash, 0, order,
-                                  false);
+                                  false, 0);
     };
     auto w4c = [&]() {   // chunk-of-4 layout in and out (the library's F(4,3) chain)
       sedx::launch_conv3x3_wino43(d_in4, l.B, l.T, l.F, l.cin, l.cout, d_u43, d_bias, d_o3, l.epi, d_trash, 0, order,
-                                  true);
+                                  true, 0);
+    };
+    // the C4 launch forced to 64-channel (4) / 16-channel (1) items: the
+    // launcher's choice of item width never changes a bit of the output
+    auto w4f = [&](int ntf, float* o) {
+      sedx::launch_conv3x3_wino43(d_in4, l.B, l.T, l.F, l.cin, l.cout, d_u43, d_bias, o, l.epi, d_trash, 0, order,
+                                  true, ntf);
     };
     if (with2) w2();
     w4();
     w4c();
+    size_t ntdiff = 0;
+    for (int ntf : {4, 1}) {   // each forced width against the launcher's choice
+      w4f(ntf, d_o4);
+      hipDeviceSynchronize();
+      std::vector<float> a(nout), b(nout);
+      hipMemcpy(a.data(), d_o3, nout * 4, hipMemcpyDeviceToHost);
+      hipMemcpy(b.data(), d_o4, nout * 4, hipMemcpyDeviceToHost);
+      for (size_t i = 0; i < nout; ++i) ntdiff += std::memcmp(&a[i], &b[i], 4) != 0;
+    }
     const hipError_t ke = hipDeviceSynchronize();
     std::vector<float> o1(nout), o2(nout), o3(nout), o3n(nout);
     hipMemcpy(o1.data(), d_o1, nout * 4, hipMemcpyDeviceToHost);
@@ -172,9 +189,9 @@ int main(int argc, char** argv) {
       ++nchk;
     }
     const double tol = 2e-4 * std::max(1.0, omax);
-    const bool lok = ke == hipSuccess && nan == 0 && e4max < tol && c4diff == 0;
+    const bool lok = ke == hipSuccess && nan == 0 && e4max < tol && c4diff == 0 && ntdiff == 0;
     ok = ok && lok;
-    float m2 = 0, m4 = 0, m4c = 0;
+    float m2 = 0, m4 = 0, m4c = 0, mn1 = 0, mn4 = 0;
     if (!l.full) {
       auto timeit = [&](auto fn) {
         fn();
@@ -201,6 +218,10 @@ int main(int argc, char** argv) {
              st[1] / items, st[2] / items);
 #endif
       m4c = timeit(w4c);
+      mn4 = timeit([&]() { w4f(4, d_o4); });
+      mn1 = timeit([&]() { w4f(1, d_o4); });
+      tot_n4 += mn4;
+      tot_n1 += mn1;
       tot_2 += m2;
       tot_4 += m4;
       tot_4c += m4c;
@@ -208,10 +229,11 @@ int main(int argc, char** argv) {
     const double fl = 2.0 * l.B * l.T * l.F * l.cin * l.cout * 9;   // direct-conv FLOPs
     const double fl4 = fl * 36.0 / 144.0;                           // F(4,3) matrix-pipe FLOPs (no tile padding)
     printf("%-5s B=%d T=%d  F(2,3) %.4f ms  F(4,3) nhwc %.4f  c4 %.4f ms (MFMA %.1f TF/s = %.3f of 157.3)  x%.2f  "
-           "|w2-ref| %.2e |w4-ref| max %.2e rms %.2e  max|ref| %.2f  checked %zu nonfinite %zu  c4!=nhwc %zu  %s\n",
+           "|w2-ref| %.2e |w4-ref| max %.2e rms %.2e  max|ref| %.2f  checked %zu nonfinite %zu  c4!=nhwc %zu  "
+           "[nt4 %.4f nt1 %.4f ms, differing %zu]  %s\n",
            l.name, l.B, l.T, m2, m4, m4c, m4c > 0 ? fl4 / m4c / 1e9 : 0.0, m4c > 0 ? fl4 / m4c / 1e9 / 157.3 : 0.0,
            m4c > 0 ? m2 / m4c : 0.0, e2max, e4max, std::sqrt(e4sq / std::max<size_t>(1, nchk)), omax, nchk, nan,
-           c4diff, lok ? "OK" : "MISMATCH");
+           c4diff, mn4, mn1, ntdiff, lok ? "OK" : "MISMATCH");
     fflush(stdout);
   }
   // block 1 as the library runs it: the fused F(2,3) launch against conv1
@@ -226,7 +248,7 @@ int main(int argc, char** argv) {
     for (auto& v : bias) v = 0.1f * nd(rng);
     std::vector<double> w((size_t)64 * 64 * 9);
     for (auto& v : w) v = (double)(float)(nd(rng) * std::sqrt(2.f / 576));
-    std::vector<float> U((size_t)64 * 64 * 16), U43((size_t)64 * 64 * 36);
+    std::vector<float> U((size_t)64 * 64 * 16), U43((size_t)2 * 64 * 64 * 36);
     sedx::pack_conv_wino(w.data(), 64, 64, U.data());
     sedx::pack_conv_wino43(w.data(), 64, 64, U43.data());
     float *d_x0, *d_w1, *d_b1, *d_a, *d_a4, *d_ob;
@@ -267,15 +289,16 @@ int main(int argc, char** argv) {
     });
     const float m_c1 = timeit([&]() { sedx::launch_conv1_c4(d_x0, B, T, d_w1, d_b1, d_a4, 0); });
     const float m_c2 = timeit([&]() {
-      sedx::launch_conv3x3_wino43(d_a4, B, T, 64, 64, 64, d_u43, d_bias, d_ob, sedx::EPI_POOL2, d_trash, 0, order, true);
+      sedx::launch_conv3x3_wino43(d_a4, B, T, 64, 64, 64, d_u43, d_bias, d_ob, sedx::EPI_POOL2, d_trash, 0, order, true,
+                                  0);
     });
     printf("block1 B=%d T=%d  fused F(2,3) %.4f ms  conv1_c4 %.4f + F(4,3) conv2 %.4f = %.4f ms  (x%.2f)  "
            "conv1 c4 vs nhwc differing %zu\n",
            B, T, m_f23, m_c1, m_c2, m_c1 + m_c2, m_f23 / (m_c1 + m_c2), ndiff);
     hipFree(d_x0); hipFree(d_w1); hipFree(d_b1); hipFree(d_a); hipFree(d_a4); hipFree(d_ob);
   }
-  printf("total F(2,3) %.4f ms  F(4,3) nhwc %.4f ms  c4 %.4f ms  (x%.2f)  %s  (err=%s, launch=%s)\n", tot_2, tot_4,
-         tot_4c, tot_4c > 0 ? tot_2 / tot_4c : 0.0, ok ? "ALL OK" : "MISMATCH", hipGetErrorString(hipGetLastError()),
+  printf("total F(2,3) %.4f ms  F(4,3) nhwc %.4f ms  c4 %.4f ms  (x%.2f)  [c4 forced nt4 %.4f nt1 %.4f]  %s  "
+         "(err=%s, launch=%s)\n", tot_2, tot_4, tot_4c, tot_4c > 0 ? tot_2 / tot_4c : 0.0, tot_n4, tot_n1, ok ? "ALL OK" : "MISMATCH", hipGetErrorString(hipGetLastError()),
          hipGetErrorString(sedx::take_launch_error()));
   return ok ? 0 : 1;
 }
