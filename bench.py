@@ -483,8 +483,9 @@ def conv_kernel_name(stage, precision):
     if precision == 'winograd' and stage == 'b1c2' and WINO_BLOCK1 == 2 and WINO_F43 != 2:
         return 'sedx::wino_block1_kernel<2, %s>' % c4
     if precision == 'winograd' and stage in wino_stages() and wino_mul(stage) == WINO43_MUL:
-        # (the last argument: 4 channel tiles per item at the bench's B = 32)
-        return 'sedx::conv3x3_wino43_kernel<%d, %d, %s, 4>' % (F, epi, c4)
+        # (the last two arguments: 4 channel tiles and 2 tile groups per item
+        # at the bench's B = 32)
+        return 'sedx::conv3x3_wino43_kernel<%d, %d, %s, 4, 2>' % (F, epi, c4)
     if precision == 'winograd' and stage in wino_stages():
         # 2 tile groups x 64 channels (8 row waves) at the bench shapes
         return 'sedx::conv3x3_wino_kernel<%d, %d, 2, 2>' % (F, epi)
@@ -497,9 +498,12 @@ def profiled(kernel, summary=PROFILE_SUMMARY):
     effective clock GHz) of ``kernel`` from the committed summary."""
     try:
         with open(summary) as f:
-            v = json.load(f).get(kernel, {})
+            d = json.load(f)
     except (OSError, ValueError):
         return None, None, None, None
+    # summaries before round 6 name the F(4x4,3x3) kernels without the tile
+    # group argument (<F, EPI, C4, 4>, the same launch as <..., 4, 2>)
+    v = d.get(kernel) or d.get(kernel.replace(', 4, 2>', ', 4>'), {})
     ns = v.get('avg_ns')
     util, clk = v.get('mfma_util'), v.get('clock_ghz')
     return (v.get('hbm_bytes_corrected'), (round(ns * 1e-6, 4) if ns else None),

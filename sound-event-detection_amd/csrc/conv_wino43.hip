@@ -88,11 +88,14 @@ __device__ unsigned long long g_w43_stamps[8];
 #define W43_MARK(i)
 #endif
 
-template <int F>
+// TG: tile groups per item — 2 (32 tiles, 12 waves; every full-size launch)
+// or 1 (16 tiles, 6 waves: the one-clip grids of the 16-channel items at
+// F = 16 / 8, twice the items of 2 for the same work)
+template <int F, int TG = 2>
 struct W43Geom {
-  static constexpr int WAVES = 12, THREADS = 64 * WAVES;
+  static constexpr int WAVES = 6 * TG, THREADS = 64 * WAVES;
   static constexpr int NT = 4, NCH = 64;             // channel tiles / output channels per item
-  static constexpr int TILES = 32;                   // two tile groups of 16
+  static constexpr int TILES = 16 * TG;              // TG tile groups of 16
   static constexpr int FT = F / 4;                   // tiles per tile row
   static constexpr int TRW = TILES / FT;             // tile rows per item
   // a tile group is TRG tile rows x TFG tile columns (lane n = tr TFG + tf)
@@ -106,11 +109,11 @@ struct W43Geom {
   static constexpr int RS = F == 64 ? 66 : F == 32 ? 36 : F == 16 ? 20 : 10;
   // a plane's halo in 64-dword DMA blocks, one per wave 0..HB-1 (RT RS <= 704
   // for every F); wave 11 issues its four halo DMAs into an LDS trash block,
-  // so every wave has the same DMA count per step
-  static constexpr int HB = 11;
+  // so every wave has the same DMA count per step (TG 1: RT RS <= 384, a
+  // block per wave, no trash wave)
+  static constexpr int HB = TG == 2 ? 11 : 6;
   static constexpr int PS = 64 * HB + 2;             // plane stride, = 2 mod 4 (odd bank pairs for odd k)
   static constexpr int HALO = 4 * PS;                // dwords per halo slot
-  static constexpr int USZ = 36 * 4 * NCH;           // dwords per U slot ([p][k][m][nt])
   static constexpr int USZ1 = 36 * 4 * 16;           // NT 1: one 16-channel tile's slab ([p][k][m]), 9 KiB
   static constexpr int NB = 3;                       // ring depth (U and halo)
   // epilogue exchange per round, per tile group, in the U slot freed by the
@@ -120,6 +123,9 @@ struct W43Geom {
   // ds_read_b64 of its own pair: conflict-free)
   static constexpr int XRS = 4 * 80;
   static constexpr int XTG = 6 * 2 * XRS;
+  // dwords per U slot: the 64-channel slab ([p][k][m][nt]); TG 1 (NT 1 only):
+  // its 9 KiB slab or one tile group's exchange, the larger
+  static constexpr int USZ = TG == 2 ? 36 * 4 * NCH : (USZ1 > XTG ? USZ1 : XTG);
   static constexpr int U_OFF = 0, H_OFF = NB * USZ, BIAS_OFF = H_OFF + NB * HALO, BIAS_MAX = 512;
   static constexpr int HTRASH_OFF = BIAS_OFF + BIAS_MAX;   // 64 dwords: wave 11's halo DMAs
   static constexpr int LDS_BYTES = 4 * (HTRASH_OFF + 64);
@@ -127,9 +133,10 @@ struct W43Geom {
 
   static_assert(F == 64 || F == 32 || F == 16 || F == 8, "F");
   static_assert(RT * RS <= 64 * HB, "halo plane fits its DMA blocks");
-  static_assert(HB == WAVES - 1, "wave 11: trash halo block");
-  static_assert(36 % WAVES == 0, "U units per wave");
-  static_assert(2 * XTG <= USZ, "both tile groups' exchange fits one U slot");
+  static_assert(TG == 1 || TG == 2, "TG");
+  static_assert(TG == 1 ? HB == WAVES : HB == WAVES - 1, "halo blocks: one per wave (TG 2: wave 11 trash)");
+  static_assert(TG == 1 || 36 % WAVES == 0, "U units per wave");
+  static_assert(TG * XTG <= USZ, "the tile groups' exchange fits one U slot");
   static_assert(LDS_BYTES <= 160 * 1024, "LDS per workgroup");
   static_assert(FT * TRW == TILES && TFG * TRG == 16, "tile groups");
 };
@@ -203,17 +210,20 @@ __device__ __forceinline__ void w43_at(const float (&m)[6], float (&z)[4]) {
 // eight XCDs (channel tile g on XCD g mod 8, every tile block of it there):
 // at one clip the 512-channel layers have 2 tile blocks, which the tile
 // block-major decode put on two XCDs.
-template <int F, int EPI, int ROW, bool C4, int NT>
+template <int F, int EPI, int ROW, bool C4, int NT, int TG>
 __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, int T, int Cin, int Cout,
                                          const float* __restrict__ U, int u_bytes, const float* __restrict__ bias,
                                          float* __restrict__ out, float* __restrict__ trash, int tb_per_clip,
                                          int ngroups, int order2d, int wv) {
-  using G = W43Geom<F>;
+  using G = W43Geom<F, TG>;
   constexpr int RS = G::RS, PS = G::PS;
+  static_assert(TG == 2 || (NT == 1 && (F == 16 || F == 8)), "16-tile items: 16-channel, F = 16 / 8 only");
   static_assert(NT == 4 || NT == 1, "channel tiles per item");
   // a U fragment: the lane's words of its NT channel tiles
   using UF = typename std::conditional<NT == 4, w43_f32x4, float>::type;
-  constexpr int VM = NT == 4 ? G::VM : 5;   // DMAs per wave per step: U units + 4 halo planes
+  // DMAs per wave per step: U units + 4 halo planes (NT 1: 9 units over
+  // the waves, TG 1: two per wave)
+  constexpr int VM = NT == 4 ? G::VM : TG == 2 ? 5 : 6;
   extern __shared__ __attribute__((aligned(16))) float smem[];   // G::LDS_BYTES (dynamic)
 
   // the lane from mbcnt (rematerialised where needed) and the wave from one
@@ -222,7 +232,7 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
   // 168-VGPR POOL2 builds put vmcnt(0) drains in the prologue)
   // (wv: the wave, wave-uniform, read once by the kernel entry)
   const int lane = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-  const int tg = wv & 1;
+  const int tg = TG == 2 ? wv & 1 : 0;
   const int kk = lane >> 4, nn = lane & 15;
 
   // XCD-aware item decode (conv_wino.hip): item -> XCD id & 7; on one XCD,
@@ -283,6 +293,7 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
   const uint32_t u_voff = 16 * lane + 1024 * wv;
   // NT 1: waves 9-11 have no unit (out of range: zeros into the slot's tail)
   const uint32_t u_voff1 = wv < 9 ? u_voff : 0x80000000u;
+  const uint32_t u_voff2 = wv + 6 < 9 ? u_voff + 6144 : 0x80000000u;   // TG 1
   const uint32_t bytes_per_chunk_u = 4 * G::USZ;
   // DMA of chunk cc of an item (halo offsets hof, channel group g_) into the
   // given slots; U units wv, wv + 12, wv + 24 and this wave's halo block
@@ -293,6 +304,7 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
           (uint32_t)(u_bytes / 2 + (g_ * nchunks + cc) * (4 * G::USZ1)));
       const uint32_t m0 = __builtin_amdgcn_readfirstlane(w43_lds_addr(smem + G::U_OFF + uslot * G::USZ + 256 * wv));
       w43_dma16(u_voff1, r_u, so, m0);
+      if constexpr (TG == 1) w43_dma16(u_voff2, r_u, so, m0 + 6144);   // unit wv + 6
       return;
     }
     const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)((g_ * nchunks + cc) * bytes_per_chunk_u));
@@ -781,24 +793,25 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
 #endif
 }
 
-#define SEDX_W43_ROWS(F_, EPI_, C4_, NT_, ...)                         \
-  switch (wv >> 1) {                                                  \
-    case 0: w43_body<F_, EPI_, 0, C4_, NT_>(__VA_ARGS__); break;      \
-    case 1: w43_body<F_, EPI_, 1, C4_, NT_>(__VA_ARGS__); break;      \
-    case 2: w43_body<F_, EPI_, 2, C4_, NT_>(__VA_ARGS__); break;      \
-    case 3: w43_body<F_, EPI_, 3, C4_, NT_>(__VA_ARGS__); break;      \
-    case 4: w43_body<F_, EPI_, 4, C4_, NT_>(__VA_ARGS__); break;      \
-    default: w43_body<F_, EPI_, 5, C4_, NT_>(__VA_ARGS__); break;     \
+#define SEDX_W43_ROWS(F_, EPI_, C4_, NT_, TG_, ...)                         \
+  switch (TG_ == 2 ? wv >> 1 : wv) {                                       \
+    case 0: w43_body<F_, EPI_, 0, C4_, NT_, TG_>(__VA_ARGS__); break;      \
+    case 1: w43_body<F_, EPI_, 1, C4_, NT_, TG_>(__VA_ARGS__); break;      \
+    case 2: w43_body<F_, EPI_, 2, C4_, NT_, TG_>(__VA_ARGS__); break;      \
+    case 3: w43_body<F_, EPI_, 3, C4_, NT_, TG_>(__VA_ARGS__); break;      \
+    case 4: w43_body<F_, EPI_, 4, C4_, NT_, TG_>(__VA_ARGS__); break;      \
+    default: w43_body<F_, EPI_, 5, C4_, NT_, TG_>(__VA_ARGS__); break;     \
   }
 
-template <int F, int EPI, bool C4, int NT = 4>
-__global__ __launch_bounds__(768, 1) void conv3x3_wino43_kernel(const float* __restrict__ in, int B, int T, int Cin,
+template <int F, int EPI, bool C4, int NT = 4, int TG = 2>
+__global__ __launch_bounds__(384 * TG, 1) void conv3x3_wino43_kernel(const float* __restrict__ in, int B, int T, int Cin,
                                                                 int Cout, const float* __restrict__ U, int u_bytes,
                                                                 const float* __restrict__ bias, float* __restrict__ out,
                                                                 float* __restrict__ trash, int tb_per_clip,
                                                                 int ngroups, int order2d) {
   const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
-  SEDX_W43_ROWS(F, EPI, C4, NT, in, B, T, Cin, Cout, U, u_bytes, bias, out, trash, tb_per_clip, ngroups, order2d, wv)
+  SEDX_W43_ROWS(F, EPI, C4, NT, TG, in, B, T, Cin, Cout, U, u_bytes, bias, out, trash, tb_per_clip, ngroups, order2d,
+                wv)
 }
 #undef SEDX_W43_ROWS
 
@@ -813,22 +826,17 @@ __global__ __launch_bounds__(768, 1) void conv3x3_wino43_kernel(const float* __r
 #define SEDX_W43_ITEMS 2
 #endif
 
-template <int F>
-static void launch_w43_f(const float* in, int B, int T, int Cin, int Cout, const float* U, const float* bias,
-                         float* out, int epi, float* trash, int order, bool c4, int nt_force, hipStream_t s) {
-  using G = W43Geom<F>;
+// one launch of the F(4x4,3x3) kernel with TG tile groups per item and
+// 16- (nt1) or 64-channel items
+template <int F, int TG>
+static void launch_w43_g(const float* in, int B, int T, int Cin, int Cout, const float* U, const float* bias,
+                         float* out, int epi, float* trash, int order, bool c4, bool nt1, int ncu, hipStream_t s) {
+  using G = W43Geom<F, TG>;
   // output rows the epilogue covers: POOL2 drops an odd last row
   const int rows = epi == EPI_POOL2 ? 2 * (T / 2) : T;
   const int trows = (rows + 3) / 4;
   const int tb_per_clip = (trows + G::TRW - 1) / G::TRW;
   const int64_t tblocks = (int64_t)B * tb_per_clip;
-  int ncu = 256, dev = 0;
-  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-  // 16-channel items (NT 1, bit-identical) when 64-channel ones would give
-  // at most a quarter of the CUs one (measured, profiles/r05q_small_batch.log:
-  // at 128 items — b3c2 at B = 4, b4 at B = 8 — NT 1's four times the items
-  // at a quarter the work each were slower; at <= 64 faster)
-  const bool nt1 = nt_force ? nt_force == 1 : (tblocks + 7) / 8 * 8 * (Cout / G::NCH) <= ncu / 4;
   const int ngroups = Cout / (nt1 ? 16 : G::NCH);
   // NT 1: 8 XCD lanes x ceil(groups / 8) channel tiles x every tile block
   const int64_t nitems = nt1 ? 8 * ((ngroups + 7) / 8) * tblocks : (tblocks + 7) / 8 * 8 * ngroups;
@@ -860,14 +868,23 @@ static void launch_w43_f(const float* in, int B, int T, int Cin, int Cout, const
   // math: a scratch op the compiler inserts only ever ADDS vector-memory ops
   // to a wave's in-order count, so a counted wait then retires more of the
   // older DMAs than it names, never fewer — stricter, not looser.
-#define SEDX_W43_LAUNCH(E)                                                                                 \
-  {                                                                                                        \
-    auto* k_ = nt1 ? (c4 ? conv3x3_wino43_kernel<F, E, true, 1> : conv3x3_wino43_kernel<F, E, false, 1>)   \
-                   : (c4 ? conv3x3_wino43_kernel<F, E, true, 4> : conv3x3_wino43_kernel<F, E, false, 4>);  \
-    if (!launch_info(reinterpret_cast<const void*>(k_), G::THREADS, G::LDS_BYTES, c4).ok) return;          \
-    hipLaunchKernelGGL(k_, dim3((unsigned)nwg), dim3(G::THREADS), G::LDS_BYTES, s, in, B, T, Cin, Cout, U, \
-                       (int)u_bytes, bias, out, trash, tb_per_clip, ngroups, order2d);                     \
-    return;                                                                                                \
+#define SEDX_W43_GO(k_)                                                                                     \
+  {                                                                                                         \
+    if (!launch_info(reinterpret_cast<const void*>(k_), G::THREADS, G::LDS_BYTES, c4).ok) return;           \
+    hipLaunchKernelGGL(k_, dim3((unsigned)nwg), dim3(G::THREADS), G::LDS_BYTES, s, in, B, T, Cin, Cout, U,  \
+                       (int)u_bytes, bias, out, trash, tb_per_clip, ngroups, order2d);                      \
+    return;                                                                                                 \
+  }
+#define SEDX_W43_LAUNCH(E)                                                                                  \
+  {                                                                                                         \
+    if constexpr (TG == 1) {   /* 16-tile items: 16-channel, chunk-of-4 only */                             \
+      if (!nt1 || !c4) return note_launch_error(hipErrorInvalidValue);                                     \
+      SEDX_W43_GO((conv3x3_wino43_kernel<F, E, true, 1, 1>));                                              \
+    } else {                                                                                                \
+      auto* k_ = nt1 ? (c4 ? conv3x3_wino43_kernel<F, E, true, 1> : conv3x3_wino43_kernel<F, E, false, 1>)  \
+                     : (c4 ? conv3x3_wino43_kernel<F, E, true, 4> : conv3x3_wino43_kernel<F, E, false, 4>); \
+      SEDX_W43_GO(k_);                                                                                      \
+    }                                                                                                       \
   }
   if constexpr (F == 64) {   // block 1's conv2 (conv1's output in, 2 x 2 pool)
     if (epi == EPI_POOL2) SEDX_W43_LAUNCH(EPI_POOL2);
@@ -879,7 +896,36 @@ static void launch_w43_f(const float* in, int B, int T, int Cin, int Cout, const
     if (epi == EPI_POOL2) SEDX_W43_LAUNCH(EPI_POOL2);
   }
 #undef SEDX_W43_LAUNCH
+#undef SEDX_W43_GO
   note_launch_error(hipErrorInvalidValue);
+}
+
+// nt_force: 0 = choose; 4 = 64-channel items; 1 = 16-channel items of 32
+// tiles; 2 = 16-channel items of 16 tiles (F = 16 / 8, chunk-of-4)
+template <int F>
+static void launch_w43_f(const float* in, int B, int T, int Cin, int Cout, const float* U, const float* bias,
+                         float* out, int epi, float* trash, int order, bool c4, int nt_force, hipStream_t s) {
+  using G = W43Geom<F>;
+  const int rows = epi == EPI_POOL2 ? 2 * (T / 2) : T;
+  const int64_t tblocks = (int64_t)B * (((rows + 3) / 4 + G::TRW - 1) / G::TRW);
+  int ncu = 256, dev = 0;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  // 16-channel items (NT 1, bit-identical) when 64-channel ones would give
+  // at most a quarter of the CUs one (measured, profiles/r05q_small_batch.log:
+  // at 128 items — b3c2 at B = 4, b4 at B = 8 — NT 1's four times the items
+  // at a quarter the work each were slower; at <= 64 faster)
+  const bool nt1 = nt_force ? nt_force != 4 : (tblocks + 7) / 8 * 8 * (Cout / G::NCH) <= ncu / 4;
+  // 16-channel items of one tile group (16 tiles, 6 waves) where those of
+  // two would leave CUs idle (one clip: the 256- and 512-channel layers, 128
+  // and 64 items of 32 tiles; bit-identical — the same chains per output)
+  constexpr bool tg1_ok = F == 16 || F == 8;
+  const bool tg1 = tg1_ok && c4 && nt1 &&
+                   (nt_force ? nt_force == 2 : 8 * ((Cout / 16 + 7) / 8) * tblocks < ncu);
+  if (nt_force == 2 && !tg1) return note_launch_error(hipErrorInvalidValue);
+  if constexpr (tg1_ok) {
+    if (tg1) return launch_w43_g<F, 1>(in, B, T, Cin, Cout, U, bias, out, epi, trash, order, c4, true, ncu, s);
+  }
+  launch_w43_g<F, 2>(in, B, T, Cin, Cout, U, bias, out, epi, trash, order, c4, nt1, ncu, s);
 }
 
 void launch_conv3x3_wino43(const float* in, int B, int T, int F, int Cin, int Cout, const float* U43,

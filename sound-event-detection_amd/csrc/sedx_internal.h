@@ -129,8 +129,9 @@ void pack_conv_wino(const double* wf, int Cin, int Cout, float* U);   // U: Cin 
 // Same contract as fp32 Winograd F(4x4,3x3) (conv_wino43.hip), blocks 2-4:
 // F in {32, 16, 8}, Cin % 8 == 0 and >= 16, Cout % 64 == 0 and <= 512; U43
 // from pack_conv_wino43 (2 Cin Cout 36 floats: the 64- and the 16-channel
-// item packs); nt_force: 0 = the launcher's choice of 64- or 16-channel
-// items, 4 / 1 = that one (A/B and tests; bit-identical); pixels outside the clip are
+// item packs); nt_force: 0 = the launcher's choice of item shape, 4 =
+// 64-channel items, 1 = 16-channel items of 32 tiles, 2 = 16-channel items of
+// 16 tiles (F = 16 / 8, c4 only) — A/B and tests, all bit-identical; pixels outside the clip are
 // zero-filled by the buffer DMA's range check (no zero block); trash >= 64 x
 // 128 floats of device scratch for the out-of-range epilogue stores.
 // c4: input and output in the chunk-of-4 layout [B][C/4][T][F][4] (the

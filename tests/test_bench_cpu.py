@@ -75,7 +75,7 @@ def test_roofline_winograd_block1(bench):
     stage['b1c1'] = 0.1
     assert bench.WINO_BLOCK1 == 2 and bench.WINO_F43 == 2
     w = bench.roofline(stage, 32, 'winograd')
-    assert w['kernel'] == 'sedx::conv3x3_wino43_kernel<64, 1, true, 4> (b1c2)'
+    assert w['kernel'] == 'sedx::conv3x3_wino43_kernel<64, 1, true, 4, 2> (b1c2)'
     assert w['flops_per_launch'] == bench.conv_flops('b1c2', 32, 1001) * 36.0 / 144.0
     try:
         bench.WINO_F43 = 1
@@ -93,7 +93,7 @@ def test_roofline_winograd_block1(bench):
         bench.WINO_F43 = 2
         bench.WINO_BLOCK1 = 1
         w = bench.roofline(stage, 32, 'winograd')
-        assert w['kernel'] == 'sedx::conv3x3_wino43_kernel<64, 1, false, 4> (b1c2)'
+        assert w['kernel'] == 'sedx::conv3x3_wino43_kernel<64, 1, false, 4, 2> (b1c2)'
     finally:
         bench.WINO_BLOCK1 = 2
         bench.WINO_F43 = 2
@@ -108,11 +108,11 @@ def test_roofline_winograd_f43(bench):
     stage['b4c2'] = 1.0
     assert bench.WINO_F43 == 2
     w = bench.roofline(stage, 32, 'winograd')
-    assert w['kernel'] == 'sedx::conv3x3_wino43_kernel<8, 2, true, 4> (b4c2)'
+    assert w['kernel'] == 'sedx::conv3x3_wino43_kernel<8, 2, true, 4, 2> (b4c2)'
     assert w['flops_per_launch'] == bench.conv_flops('b4c2', 32, 1001) * 36.0 / 144.0
     assert 'b1c2 F(4x4,3x3)' in w['arith'] and 'F(2x2,3x3)' not in w['arith']
-    assert bench.conv_kernel_name('b2c2', 'winograd') == 'sedx::conv3x3_wino43_kernel<32, 1, true, 4>'
-    assert bench.conv_kernel_name('b1c2', 'winograd') == 'sedx::conv3x3_wino43_kernel<64, 1, true, 4>'
+    assert bench.conv_kernel_name('b2c2', 'winograd') == 'sedx::conv3x3_wino43_kernel<32, 1, true, 4, 2>'
+    assert bench.conv_kernel_name('b1c2', 'winograd') == 'sedx::conv3x3_wino43_kernel<64, 1, true, 4, 2>'
     try:
         bench.WINO_F43 = 1
         w = bench.roofline(stage, 32, 'winograd')

@@ -118,7 +118,9 @@ int main(int argc, char** argv) {
     w4();
     w4c();
     size_t ntdiff = 0;
-    for (int ntf : {4, 1}) {   // each forced width against the launcher's choice
+    const bool tg1 = l.F == 16 || l.F == 8;
+    for (int ntf : {4, 1, 2}) {   // each forced item shape against the launcher's choice
+      if (ntf == 2 && !tg1) continue;
       w4f(ntf, d_o4);
       hipDeviceSynchronize();
       std::vector<float> a(nout), b(nout);
@@ -191,7 +193,7 @@ int main(int argc, char** argv) {
     const double tol = 2e-4 * std::max(1.0, omax);
     const bool lok = ke == hipSuccess && nan == 0 && e4max < tol && c4diff == 0 && ntdiff == 0;
     ok = ok && lok;
-    float m2 = 0, m4 = 0, m4c = 0, mn1 = 0, mn4 = 0;
+    float m2 = 0, m4 = 0, m4c = 0, mn1 = 0, mn4 = 0, mt1 = 0;
     if (!l.full) {
       auto timeit = [&](auto fn) {
         fn();
@@ -220,6 +222,7 @@ int main(int argc, char** argv) {
       m4c = timeit(w4c);
       mn4 = timeit([&]() { w4f(4, d_o4); });
       mn1 = timeit([&]() { w4f(1, d_o4); });
+      if (tg1) mt1 = timeit([&]() { w4f(2, d_o4); });
       tot_n4 += mn4;
       tot_n1 += mn1;
       tot_2 += m2;
@@ -230,10 +233,10 @@ int main(int argc, char** argv) {
     const double fl4 = fl * 36.0 / 144.0;                           // F(4,3) matrix-pipe FLOPs (no tile padding)
     printf("%-5s B=%d T=%d  F(2,3) %.4f ms  F(4,3) nhwc %.4f  c4 %.4f ms (MFMA %.1f TF/s = %.3f of 157.3)  x%.2f  "
            "|w2-ref| %.2e |w4-ref| max %.2e rms %.2e  max|ref| %.2f  checked %zu nonfinite %zu  c4!=nhwc %zu  "
-           "[nt4 %.4f nt1 %.4f ms, differing %zu]  %s\n",
+           "[nt4 %.4f nt1 %.4f nt1/16 tiles %.4f ms, differing %zu]  %s\n",
            l.name, l.B, l.T, m2, m4, m4c, m4c > 0 ? fl4 / m4c / 1e9 : 0.0, m4c > 0 ? fl4 / m4c / 1e9 / 157.3 : 0.0,
            m4c > 0 ? m2 / m4c : 0.0, e2max, e4max, std::sqrt(e4sq / std::max<size_t>(1, nchk)), omax, nchk, nan,
-           c4diff, mn4, mn1, ntdiff, lok ? "OK" : "MISMATCH");
+           c4diff, mn4, mn1, mt1, ntdiff, lok ? "OK" : "MISMATCH");
     fflush(stdout);
   }
   // block 1 as the library runs it: the fused F(2,3) launch against conv1
