@@ -425,6 +425,9 @@ def latency_b1(model, dev, reps=20):
                 ts.append((time.perf_counter() - a) * 1e3)
         out[key] = round(statistics.median(ts), 4)
     out['unit'] = 'ms p50'
+    # where the one clip's device time goes (per stage, HIP events, one
+    # forward at a time)
+    out['stage_ms'] = stage_times_isolated(model, wd, dev, reps)
     return out
 
 
@@ -906,7 +909,7 @@ def main():
     ap.add_argument('--gru-kernel', choices=list(GRU_KERNELS), default='auto',
                     help='GRU recurrence kernel (SEDX_TUNE_GRU_KERNEL; A/B runs); auto: the library default '
                          '(16 slices; on a pipelined handle dealt over every XCD)')
-    ap.add_argument('--wino-order', type=int, choices=[0, 1], default=None,
+    ap.add_argument('--wino-order', type=int, choices=[0, 1, 2], default=None,
                     help='SEDX_TUNE_WINO_ORDER (A/B runs): Winograd item order on the 512-channel layers')
     ap.add_argument('--gamma-spec', type=int, choices=[0, 1], default=None,
                     help='SEDX_TUNE_GAMMA_SPEC (A/B runs): gammatone spectrum kernel (config 4)')
@@ -921,9 +924,11 @@ def main():
                     help='N > 1 process-group backend: nccl (= RCCL, the default with GPUs; rank r on GPU r) or '
                          'gloo (every rank on GPU 0, gathers through host copies: a rehearsal of the N-rank path '
                          'with the real model on a one-GPU box)')
-    ap.add_argument('--gru-handoff', choices=['auto', 'global', 'spread'], default=None,
+    ap.add_argument('--gru-handoff', choices=['auto', 'global', 'spread', 'local'], default=None,
                     help='SEDX_TUNE_GRU_HANDOFF (A/B runs): XCD-local when placed on one XCD (auto), always the '
-                         'global protocol, or the global protocol with the slices dealt over every XCD (spread)')
+                         'global protocol, or the global protocol with the slices dealt over every XCD (spread), '
+                         'or one XCD per (group, direction) with the XCD-local hand-off also on a pipelined '
+                         'handle (local)')
     ap.add_argument('--wino-f43', type=int, choices=[0, 1, 2], default=None,
                     help='SEDX_TUNE_WINO_F43 (A/B runs): blocks 1-4 (2, the default) or 2-4 (1) as Winograd '
                          'F(4x4,3x3), or all F(2x2,3x3) (0)')
@@ -961,7 +966,7 @@ def main():
     if args.wino_order is not None:
         model.set_tuning(_lib.TUNE_WINO_ORDER, args.wino_order)
     if args.gru_handoff is not None:
-        model.set_tuning(_lib.TUNE_GRU_HANDOFF, {'auto': 0, 'global': 1, 'spread': 2}[args.gru_handoff])
+        model.set_tuning(_lib.TUNE_GRU_HANDOFF, {'auto': 0, 'global': 1, 'spread': 2, 'local': 3}[args.gru_handoff])
     B = args.batch
     wave = torch.from_numpy(synth.make_waveforms(B, 10.0, 16000, seed=1234 + rank)).to(dev)
 

@@ -295,6 +295,10 @@ sedx_status sedx_set_precision(sedx_handle* h, int32_t mode);
  *                         (group, direction)'s workgroups dealt over every XCD
  *                         (beside a concurrent conv stack no XCD loses a
  *                         quarter of its CUs; bit-identical).
+ *                         SEDX_GRU_HANDOFF_LOCAL: a (group, direction)'s
+ *                         workgroups on one XCD with the XCD-local hand-off
+ *                         when they all landed there, also on a pipelined
+ *                         handle (A/B of the placement; bit-identical).
  *  SEDX_TUNE_MEL_MFMA     (n_fft 512) 0 (default): the log-mel frontend's mel
  *                         projection as VALU band sums; 1: on
  *                         v_mfma_f32_16x16x4_f32, the workgroup's 16 frames x
@@ -330,7 +334,10 @@ sedx_status sedx_set_precision(sedx_handle* h, int32_t mode);
  *                         layers) run each XCD's rounds of 32 concurrent items
  *                         as 8 tile blocks x 4 channel groups of 64 (4 slabs
  *                         per round through the XCD's L2 instead of 8);
- *                         0: tile block major.  Bit-identical outputs.
+ *                         0: tile block major; 2: as 1, and block 1's F(4x4,3x3)
+ *                         conv2 gives each XCD a contiguous range of tile
+ *                         blocks (neighbouring items' shared halo rows read
+ *                         once into that XCD's L2).  Bit-identical outputs.
  *  SEDX_TUNE_WINO_F43     (winograd) 2 (default): block 1's conv2 and the
  *                         six conv layers of blocks 2-4 as fp32 Winograd
  *                         F(4x4,3x3) (36 multiplies per 4x4 tile,
@@ -369,7 +376,7 @@ enum {
   SEDX_GRU_KERNEL_KSPLIT = 6,
   SEDX_GRU_KERNEL_PAIR = 7
 };
-enum { SEDX_GRU_HANDOFF_AUTO = 0, SEDX_GRU_HANDOFF_GLOBAL = 1, SEDX_GRU_HANDOFF_SPREAD = 2 };
+enum { SEDX_GRU_HANDOFF_AUTO = 0, SEDX_GRU_HANDOFF_GLOBAL = 1, SEDX_GRU_HANDOFF_SPREAD = 2, SEDX_GRU_HANDOFF_LOCAL = 3 };
 sedx_status sedx_set_tuning(sedx_handle* h, int32_t knob, int32_t value);
 
 /* Asynchronous failures of forwards already issued: a GRU recurrence whose

@@ -480,7 +480,7 @@ sedx_status run_body(sedx_handle* h, int64_t B, const Geometry& g, float* ws, co
       launch_gru(G, iB, (int)g.T3, w.whhT, w.bhh, Hs, s);
     else
       launch_gru_coop(G, iB, (int)g.T3, w.whh, w.bhh, Hs, LG + align_up((size_t)M * h->nac), !x3,
-                      h->gru_handoff == SEDX_GRU_HANDOFF_AUTO,
+                      h->gru_handoff == SEDX_GRU_HANDOFF_AUTO || h->gru_handoff == SEDX_GRU_HANDOFF_LOCAL,
                       h->gru_kernel == SEDX_GRU_KERNEL_TAG16 ? 0 : h->gru_kernel == SEDX_GRU_KERNEL_TAG8 ? 1
                       : h->gru_kernel == SEDX_GRU_KERNEL_COOP16 ? 3
                       : h->gru_kernel == SEDX_GRU_KERNEL_KSPLIT ? 4
@@ -681,7 +681,9 @@ sedx_status sedx_set_tuning(sedx_handle* h, int32_t knob, int32_t value) {
       h->gru_kernel = value;
       return SEDX_OK;
     case SEDX_TUNE_GRU_HANDOFF:
-      if (value != SEDX_GRU_HANDOFF_AUTO && value != SEDX_GRU_HANDOFF_GLOBAL && value != SEDX_GRU_HANDOFF_SPREAD) break;
+      if (value != SEDX_GRU_HANDOFF_AUTO && value != SEDX_GRU_HANDOFF_GLOBAL && value != SEDX_GRU_HANDOFF_SPREAD &&
+          value != SEDX_GRU_HANDOFF_LOCAL)
+        break;
       h->gru_handoff = value;
       return SEDX_OK;
     case SEDX_TUNE_WINO_BLOCK1:
@@ -697,7 +699,7 @@ sedx_status sedx_set_tuning(sedx_handle* h, int32_t knob, int32_t value) {
       h->gru_spin = (unsigned)value;
       return SEDX_OK;
     case SEDX_TUNE_WINO_ORDER:
-      if (value != 0 && value != 1) break;
+      if (value < 0 || value > 2) break;
       h->wino_order = value;
       return SEDX_OK;
     case SEDX_TUNE_GAMMA_SPEC:

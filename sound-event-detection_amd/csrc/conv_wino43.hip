@@ -249,7 +249,7 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
       t0_ = 4 * G::TRW * (tb - b_ * tb_per_clip);
       return true;
     }
-    if (order2d) {
+    if (order2d > 0) {
       const int tbr = 32 / order2d;
       const int idx = j & 31, r = j >> 5, ncg = ngroups / order2d;
       const int tbg = r / ncg;
@@ -259,7 +259,12 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
       jb = j / ngroups;
       cgi = j - jb * ngroups;
     }
-    const int tb = jb * 8 + xcd;
+    // order2d -1 (block 1, SEDX_TUNE_WINO_ORDER 2): each XCD a contiguous
+    // range of tile blocks, so the halo rows two neighbouring items share are
+    // fetched once into that XCD's L2; else tile block jb * 8 + xcd
+    const int tbx = (B * tb_per_clip + 7) / 8;
+    if (order2d < 0 && jb >= tbx) return false;
+    const int tb = order2d < 0 ? xcd * tbx + jb : jb * 8 + xcd;
     if (tb >= B * tb_per_clip) return false;
     b_ = tb / tb_per_clip;
     t0_ = 4 * G::TRW * (tb - b_ * tb_per_clip);   // first output row of the item
@@ -848,8 +853,8 @@ static void launch_w43_g(const float* in, int B, int T, int Cin, int Cout, const
   const int64_t nwg = std::min<int64_t>(nitems, std::max<int64_t>(std::max<int64_t>(8, resident), (per + 7) / 8 * 8));
   // rounds of 32 / G tile blocks x G channel groups (conv_wino.hip): the G
   // whose round streams the fewest bytes through an XCD's L2
-  int order2d = 0;
-  if (order && !nt1 && nwg % 256 == 0 && (nitems / 8) % 32 == 0) {
+  int order2d = F == 64 && order == 2 && !nt1 ? -1 : 0;
+  if (order && !nt1 && F != 64 && nwg % 256 == 0 && (nitems / 8) % 32 == 0) {
     const int64_t slab = (int64_t)36 * Cin * G::NCH * 4, halo = (int64_t)G::RT * G::CS * Cin * 4;
     int64_t best = (int64_t)ngroups * slab + (32 / std::min(ngroups, 32)) * halo;
     for (int gr = 1; gr <= 8 && gr < ngroups; gr *= 2) {

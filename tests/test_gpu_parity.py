@@ -203,31 +203,46 @@ def _tune(m, knob, value):
 @pytest.mark.parametrize('prec', ['exact', 'x3'])
 def test_gru_handoff_modes_bit_identical(prec):
     """XCD-local and global GRU hand-off protocols — the latter also with the
-    slices dealt over every XCD (SPREAD) — move the same bytes: the outputs
+    slices dealt over every XCD (SPREAD), and LOCAL (one XCD per group and
+    direction even on a pipelined handle) — move the same bytes: the outputs
     must be bit-identical (and the faster one is used by default)."""
     import time
     from sedx import _lib
     m = build(GRU).set_precision(prec)
     wave = synth.make_waveforms(32, seconds=10.0, sample_rate=16000, seed=8)
     outs, times = {}, {}
-    for mode in (1, 2, 0):     # SEDX_GRU_HANDOFF_GLOBAL, _SPREAD, _AUTO
+    for mode in (1, 2, 3, 0):     # SEDX_GRU_HANDOFF_GLOBAL, _SPREAD, _LOCAL, _AUTO
         _tune(m, _lib.TUNE_GRU_HANDOFF, mode)
         run(m, wave)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         outs[mode] = run(m, wave)['framewise_output']
         times[mode] = time.perf_counter() - t0
-    print('GRU hand-off (%s): global %.3f ms, spread %.3f ms, auto %.3f ms (whole forward)' %
-          (prec, times[1] * 1e3, times[2] * 1e3, times[0] * 1e3))
+    print('GRU hand-off (%s): global %.3f ms, spread %.3f ms, local %.3f ms, auto %.3f ms (whole forward)' %
+          (prec, times[1] * 1e3, times[2] * 1e3, times[3] * 1e3, times[0] * 1e3))
     assert np.isfinite(outs[0]).all()
-    assert np.array_equal(outs[1], outs[0])
-    assert np.array_equal(outs[2], outs[0])
-    # spread with the pipelined (8-slice) kernel too, 40 clips (two groups)
-    w40 = synth.make_waveforms(40, seconds=4.0, sample_rate=16000, seed=9)
-    mp = build(GRU).set_precision(prec).set_pipelined(True)
-    ref = run(mp, w40)['framewise_output']
-    _tune(mp, _lib.TUNE_GRU_HANDOFF, 2)
-    assert np.array_equal(run(mp, w40)['framewise_output'], ref)
+    for mode in (1, 2, 3):
+        assert np.array_equal(outs[mode], outs[0]), mode
+
+
+@pytest.mark.parametrize('n_clips,seconds', [(40, 4.0), (160, 1.0)])
+def test_gru_pipelined_placements_bit_identical(n_clips, seconds):
+    """On a pipelined handle every recurrence kernel and placement gives the
+    non-pipelined default's bits: AUTO (16 slices dealt over every XCD), the
+    8-slice kernel (SEDX_GRU_KERNEL_COOP) under SPREAD and LOCAL, and the
+    two-half PAIR kernel under SPREAD — at 40 clips (two groups, the second
+    ragged) and 160 clips (5 groups of 32: more than GRU_MAX_SLOTS = 4, so
+    workgroups run a second group)."""
+    from sedx import _lib
+    w = synth.make_waveforms(n_clips, seconds=seconds, sample_rate=16000, seed=9)
+    ref = run(build(GRU), w)['framewise_output']
+    assert np.isfinite(ref).all()
+    for kern, ho in ((5, 0), (0, 2), (0, 3), (7, 2), (4, 3)):
+        mp = build(GRU).set_pipelined(True)
+        mp.set_tuning(_lib.TUNE_GRU_KERNEL, kern).set_tuning(_lib.TUNE_GRU_HANDOFF, ho)
+        got = run(mp, w)['framewise_output']
+        mp.check_error()
+        assert np.array_equal(got, ref), (kern, ho)
 
 
 @pytest.mark.parametrize('n_clips', [40, 80])
@@ -810,21 +825,22 @@ def test_winograd_block1_knob(wino_block1):
 
 def test_wino_order_bit_identical():
     """SEDX_TUNE_WINO_ORDER 1 (4 tile blocks x 8 channel groups per round of
-    32 items on the 512-channel layers) runs the same items with the same
-    arithmetic: bit-identical to the default order (B = 32 x 10 s, where it
-    applies, and B = 3, where the launcher keeps the default)."""
+    32 items on the 512-channel layers) and 2 (also block 1's tile blocks in
+    one contiguous range per XCD) run the same items with the same
+    arithmetic: bit-identical to tile block major order (B = 32 x 10 s, where
+    they apply, and B = 3, where the launcher keeps the default)."""
     from sedx import _lib
     m = build(GRU).set_precision('winograd')
     for n in (32, 3):
         wave = torch.from_numpy(synth.make_waveforms(n, seconds=10.0, sample_rate=16000, seed=40 + n)).cuda()
         outs = []
-        for order in (0, 1):
+        for order in (0, 1, 2):
             _tune(m, _lib.TUNE_WINO_ORDER, order)
             with torch.no_grad():
                 outs.append(m(wave)['framewise_output'].clone())
-        _tune(m, _lib.TUNE_WINO_ORDER, 0)
+        _tune(m, _lib.TUNE_WINO_ORDER, 1)
         assert torch.isfinite(outs[0]).all()
-        assert torch.equal(outs[0], outs[1]), n
+        assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2]), n
 
 
 def test_wino_block1_knob_errors():

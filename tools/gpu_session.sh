@@ -11,6 +11,7 @@
 #   bench=ARGS     python bench.py ARGS   (',' in ARGS reads as ' ')
 #   w43=B          tools/run/w43_bench B 20 (build first: tools/build_w43.sh)
 #   w43v=NAME:B    tools/run/w43_bench_NAME B 20 (a VARIANTS build)
+#   w43o=ORDER:B   tools/run/w43_bench B 20 with W43_ORDER=ORDER (item order A/B)
 #   prof           tools/profile_round.sh (rocprof kernel trace + PMC passes; env as there)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -37,6 +38,7 @@ for s in "$@"; do
     bench=*) step bench 600 python -u bench.py $arg ;;
     w43=*) step w43_b$arg 200 tools/run/w43_bench $arg 20 ;;
     w43v=*) v=${arg%%:*}; b=${arg#*:}; step w43_${v}_b$b 200 tools/run/w43_bench_$v $b 20 ;;
+    w43o=*) o=${arg%%:*}; b=${arg#*:}; step w43_o${o}_b$b 200 env W43_ORDER=$o tools/run/w43_bench $b 20 ;;
     prof) step prof 1100 tools/profile_round.sh ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
