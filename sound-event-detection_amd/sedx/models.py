@@ -195,6 +195,22 @@ def _ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
 
 
+# generation of the module tree anywhere in the process: bumped whenever a
+# parameter, buffer or submodule is registered (setattr of an nn.Parameter /
+# register_buffer / add_module), so _SedModel._signature re-walks its
+# state_dict only after such a change
+_REG_GEN = [0]
+
+
+def _bump_reg_gen(*_args):
+    _REG_GEN[0] += 1
+
+
+torch.nn.modules.module.register_module_parameter_registration_hook(_bump_reg_gen)
+torch.nn.modules.module.register_module_buffer_registration_hook(_bump_reg_gen)
+torch.nn.modules.module.register_module_module_registration_hook(_bump_reg_gen)
+
+
 class _HandleCache(dict):
     """device index -> _Native, shared by a model and its DataParallel
     replicas.  ``torch.nn.DataParallel`` (pytorch/predict.py:239,
@@ -263,8 +279,21 @@ class _SedModel(nn.Module):
         return cfg
 
     def _signature(self):
-        return tuple((k, v.data_ptr(), v._version, tuple(v.shape))
-                     for k, v in self.state_dict(keep_vars=True).items())
+        """What the packed weights of a handle were made from: every
+        state_dict tensor's key, shape, storage and version counter (an
+        in-place update — load_state_dict, optimizer-free edits — bumps the
+        version).  The state_dict walk (~75 tensors, ~0.1-0.2 ms of Python per
+        call) runs again only when a parameter, buffer or submodule was
+        registered anywhere since (torch's global registration hooks bump
+        _REG_GEN); otherwise the cached tensor list is re-read for storage and
+        version only, so a one-clip forward does not wait on it."""
+        c = self.__dict__.get('_sig_cache')
+        if c is None or c[0] != _REG_GEN[0]:
+            sd = self.state_dict(keep_vars=True)
+            c = (_REG_GEN[0], tuple(sd.keys()), tuple(sd.values()), tuple(tuple(v.shape) for v in sd.values()))
+            self.__dict__['_sig_cache'] = c
+        _, keys, tensors, shapes = c
+        return keys, shapes, tuple([(t.data_ptr(), t._version) for t in tensors])
 
     def _weights_source(self):
         """The module whose parameters a handle is packed from: the source
