@@ -815,6 +815,16 @@ __global__ __launch_bounds__(384 * TG, 1) void conv3x3_wino43_kernel(const float
                                                                 float* __restrict__ trash, int tb_per_clip,
                                                                 int ngroups, int order2d) {
   const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+#ifdef SEDX_W43_DELAY
+  // diagnostic builds only (tools/wino43_bench.cpp): the odd workgroups of
+  // the first resident round start SEDX_W43_DELAY cycles late, so half the
+  // CUs run their epilogues (and its output store bursts) out of phase
+  // with the other half
+  if ((blockIdx.x & 1) && blockIdx.x < 256) {
+    const unsigned long long t0_ = __builtin_amdgcn_s_memtime();
+    while (__builtin_amdgcn_s_memtime() - t0_ < (unsigned long long)SEDX_W43_DELAY) __builtin_amdgcn_s_sleep(8);
+  }
+#endif
   SEDX_W43_ROWS(F, EPI, C4, NT, TG, in, B, T, Cin, Cout, U, u_bytes, bias, out, trash, tb_per_clip, ngroups, order2d,
                 wv)
 }
