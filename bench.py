@@ -321,7 +321,7 @@ def measure(step, args, world, dev, model=None, B=32):
         # conv stacks in issue order (sedx_set_pipelined): without it the
         # batches in flight can fall into lockstep, two conv stacks splitting
         # the chip and the GRUs running side by side on 32 CUs
-        model.set_pipelined(len(streams) > 1 and not args.no_pipeline)
+        model.set_pipelined(getattr(args, 'pipeline_mode', 1) if len(streams) > 1 and not args.no_pipeline else 0)
     sync(dev)
     for i in range(args.warmup):
         with on(streams[i % len(streams)]):
@@ -895,6 +895,9 @@ def main():
                     help='batches in flight per GPU (HIP streams the steps rotate over)')
     ap.add_argument('--no-pipeline', action='store_true',
                     help='streams > 1 without ordering the conv stacks (A/B of sedx_set_pipelined)')
+    ap.add_argument('--pipeline-mode', type=int, choices=[1, 2], default=1,
+                    help='sedx_set_pipelined mode with streams > 1 (A/B runs): 1 = conv stacks in issue order, '
+                         '2 = the same with block 1\'s conv1 issued before the wait')
     ap.add_argument('--model', choices=list(MODEL_NAMES), default='gru')
     ap.add_argument('--mode', choices=['clip', 'window', 'gamma'], default='clip',
                     help="gamma: BASELINE config 4 alone (profiling passes of the gammatone leg)")
@@ -1109,6 +1112,7 @@ def main():
                        'world_size': dist.get_world_size() if world > 1 else 1,
                        'streams': args.streams,
                        'pipelined': args.streams > 1 and not args.no_pipeline,
+                       'pipeline_mode': args.pipeline_mode if args.streams > 1 and not args.no_pipeline else 0,
                        'gru_kernel': args.gru_kernel if args.model == 'gru' else None,
                        'gru_handoff': (args.gru_handoff or 'auto') if args.model == 'gru' else None},
             'ms_per_clip_p99': round(p99, 4) if p99 is not None else None,

@@ -392,7 +392,10 @@ sedx_status sedx_check_error(sedx_handle* h);
  * stack of the previously issued forward finished (a device-side event wait,
  * no host sync), so batch i's GRU / MHA + head overlap batch i+1's conv stack
  * instead of two conv stacks splitting the chip.  Results are unchanged;
- * order = host issue order.  Off by default. */
+ * order = host issue order.  Off by default.  on = 2: the same, with block
+ * 1's first launch (conv1, HBM-bound) issued before the wait, so it may run
+ * beside the previous forward's conv tail (its time then counts in stage 11,
+ * pipeline wait). */
 sedx_status sedx_set_pipelined(sedx_handle* h, int32_t on);
 
 /* Per-stage device timing (the reference only wall-clocks whole loops,

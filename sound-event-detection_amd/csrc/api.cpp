@@ -108,6 +108,7 @@ struct sedx_handle {
   // they are issued on, so the sequence + head of batch i overlap the conv
   // stack of batch i+1 instead of two conv stacks sharing the chip
   bool pipelined = false;
+  bool pipe_conv1_first = false;           // sedx_set_pipelined(h, 2): block 1's conv1 before the wait
   bool conv_done_recorded = false;
   hipEvent_t conv_done = nullptr;
   // host-mapped word the GRU kernel ORs a failure code into when a bounded
@@ -385,14 +386,8 @@ sedx_status run_body(sedx_handle* h, int64_t B, const Geometry& g, float* ws, co
   // the cross-stream wait for the previous forward's conv stack comes before
   // the b1c1 stage event, so stage 1 times only this forward's work
   mark(h, 12, s);   // the frontend's end: the wait below is stage 11, not the frontend's
-  if (h->pipelined && h->conv_done_recorded) HIP_TRY(h, hipStreamWaitEvent(s, h->conv_done, 0));
-  mark(h, 1, s);
-  capture(h, 0, X0, (size_t)B * g.T * 64, s);
   const bool x3 = h->precision == SEDX_PRECISION_X3;
   int* sched = reinterpret_cast<int*>(ws + l.sched);
-  // block 1 as one launch in both modes: conv1 computed inside conv2's halo
-  // staging (the b1c1 stage is just the zero-bordered copy of the bn0 output)
-  if (x3) HIP_TRY(h, hipMemsetAsync(sched, 0, 7 * CONV_SCHED_INTS * sizeof(int), s));
   const bool wb1 = wino_block1_on(h);
   // winograd with F(4x4,3x3): block 1 (one launch) and blocks 2-4 keep their
   // activations in the chunk-of-4 layout [B][C/4][T][F][4] (dense halo DMA)
@@ -402,12 +397,27 @@ sedx_status run_body(sedx_handle* h, int64_t B, const Geometry& g, float* ws, co
   // F(4x4,3x3) block 1 (wino_f43 2): conv1 by its own launch in both (2: in
   // the chunk-of-4 layout), then the F(4x4,3x3) conv2
   const bool b1_43 = wb1 && h->wino_f43 == 2;
-  if (b1_43 && c4)
-    launch_conv1_c4(X0, iB, (int)g.T, w.c1_w, w.c1_b, A, s);
-  else if (wb1 && (h->wino_block1 == 1 || b1_43))
-    launch_conv1_nhwc(X0, iB, (int)g.T, w.c1_w, w.c1_b, A, s);
-  else if (!wb1)
-    launch_pad_x0(X0, iB, (int)g.T, A, s);
+  // block 1's first launch (conv1 / the zero-bordered copy of X0): before
+  // the pipelined wait with sedx_set_pipelined(h, 2) — an HBM-bound launch
+  // that may then overlap the previous forward's compute-bound conv tail —
+  // else after it (stage 1)
+  auto block1_first = [&]() {
+    if (b1_43 && c4)
+      launch_conv1_c4(X0, iB, (int)g.T, w.c1_w, w.c1_b, A, s);
+    else if (wb1 && (h->wino_block1 == 1 || b1_43))
+      launch_conv1_nhwc(X0, iB, (int)g.T, w.c1_w, w.c1_b, A, s);
+    else if (!wb1)
+      launch_pad_x0(X0, iB, (int)g.T, A, s);
+  };
+  const bool first_early = h->pipelined && h->pipe_conv1_first;
+  if (first_early) block1_first();
+  if (h->pipelined && h->conv_done_recorded) HIP_TRY(h, hipStreamWaitEvent(s, h->conv_done, 0));
+  mark(h, 1, s);
+  capture(h, 0, X0, (size_t)B * g.T * 64, s);
+  // block 1 as one launch in both modes: conv1 computed inside conv2's halo
+  // staging (the b1c1 stage is just the zero-bordered copy of the bn0 output)
+  if (x3) HIP_TRY(h, hipMemsetAsync(sched, 0, 7 * CONV_SCHED_INTS * sizeof(int), s));
+  if (!first_early) block1_first();
   struct L {
     const float* in;
     int T, F, cin, cout, idx, epi;
@@ -1183,7 +1193,9 @@ sedx_status sedx_set_pipelined(sedx_handle* h, int32_t on) {
   if (!h) return SEDX_EINVAL;
   DeviceGuard dg(h->device);
   if (on && !h->conv_done) HIP_TRY(h, hipEventCreateWithFlags(&h->conv_done, hipEventDisableTiming));
+  if (on < 0 || on > 2) return fail(h, SEDX_EINVAL, "sedx_set_pipelined: on must be 0, 1 or 2");
   h->pipelined = on != 0;
+  h->pipe_conv1_first = on == 2;
   h->conv_done_recorded = false;
   return SEDX_OK;
 }

@@ -287,12 +287,16 @@ class _SedModel(nn.Module):
         registered anywhere since (torch's global registration hooks bump
         _REG_GEN); otherwise the cached tensor list is re-read for storage and
         version only, so a one-clip forward does not wait on it."""
+        # (keyed on the object too: a DataParallel replica is a shallow
+        # __dict__ copy whose parameter dicts are replaced without
+        # registration, so it must not reuse its source's cache)
         c = self.__dict__.get('_sig_cache')
-        if c is None or c[0] != _REG_GEN[0]:
+        if c is None or c[0] != _REG_GEN[0] or c[1] != id(self):
             sd = self.state_dict(keep_vars=True)
-            c = (_REG_GEN[0], tuple(sd.keys()), tuple(sd.values()), tuple(tuple(v.shape) for v in sd.values()))
+            c = (_REG_GEN[0], id(self), tuple(sd.keys()), tuple(sd.values()),
+                 tuple(tuple(v.shape) for v in sd.values()))
             self.__dict__['_sig_cache'] = c
-        _, keys, tensors, shapes = c
+        _, _, keys, tensors, shapes = c
         return keys, shapes, tuple([(t.data_ptr(), t._version) for t in tensors])
 
     def _weights_source(self):
@@ -361,8 +365,9 @@ class _SedModel(nn.Module):
     def set_pipelined(self, on=True):
         """Several batches in flight on different streams: run the conv
         stacks in issue order so one batch's GRU / MHA + head overlap the next
-        batch's conv stack (sedx_set_pipelined)."""
-        self.pipelined = bool(on)
+        batch's conv stack (sedx_set_pipelined).  on = 2: also issue block 1's
+        conv1 ahead of that wait."""
+        self.pipelined = int(on) if on in (0, 1, 2) else bool(on)
         return self
 
     def check_error(self):

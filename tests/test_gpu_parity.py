@@ -150,13 +150,14 @@ def test_batch_invariance(model):
         assert np.array_equal(one['framewise_output'][0], full['framewise_output'][i])
 
 
-@pytest.mark.parametrize('pipelined', [False, True])
+@pytest.mark.parametrize('pipelined', [0, 1, 2])
 def test_concurrent_streams_bit_identical(model, pipelined):
     """Batches in flight on two HIP streams (bench.py --streams 2: one batch's
     GRU / head overlapping the next batch's conv stack, whose workgroups then
     claim tiles dynamically) give bit-identical outputs to one batch at a time,
     with and without the conv stacks ordered across streams
-    (sedx_set_pipelined).  Unpipelined, the default GRU kernel (AUTO) is the
+    (sedx_set_pipelined 1; 2: block 1's conv1 issued ahead of that wait, so
+    it runs beside the previous batch's conv tail).  Unpipelined, the default GRU kernel (AUTO) is the
     16-slice cooperative one, which needs 32 co-resident workgroups beside the
     other stream's work: no NaN, no reported failure."""
     mt, m = model
