@@ -72,6 +72,10 @@ typedef float w43_f32x4 __attribute__((ext_vector_type(4)));
 #ifndef SEDX_W43_ABL
 #define SEDX_W43_ABL 0
 #endif
+// where a step issues its LDS-DMAs (A/B builds; see the step)
+#ifndef SEDX_W43_DMA_SPLIT
+#define SEDX_W43_DMA_SPLIT 0
+#endif
 
 // Diagnostic builds only (SEDX_W43_STAMPS, tools/wino43_bench.cpp): per-wave
 // s_memtime intervals summed over every wave of every 16th workgroup:
@@ -302,6 +306,25 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
   const uint32_t bytes_per_chunk_u = 4 * G::USZ;
   // DMA of chunk cc of an item (halo offsets hof, channel group g_) into the
   // given slots; U units wv, wv + 12, wv + 24 and this wave's halo block
+  // U units Q0 .. Q1 - 1 of chunk cc (NT 1: its one or two units with Q0 = 0)
+  auto dma_u_units = [&](int g_, int cc, int uslot, auto q0_tag, auto q1_tag) {
+    if constexpr (SEDX_W43_ABL & 2) return;
+    constexpr int Q0 = decltype(q0_tag)::value, Q1 = decltype(q1_tag)::value;
+    if constexpr (NT == 1) {
+      if constexpr (Q0 == 0) {
+        const uint32_t so = __builtin_amdgcn_readfirstlane(
+            (uint32_t)(u_bytes / 2 + (g_ * nchunks + cc) * (4 * G::USZ1)));
+        const uint32_t m0 = __builtin_amdgcn_readfirstlane(w43_lds_addr(smem + G::U_OFF + uslot * G::USZ + 256 * wv));
+        w43_dma16(u_voff1, r_u, so, m0);
+        if constexpr (TG == 1) w43_dma16(u_voff2, r_u, so, m0 + 6144);
+      }
+      return;
+    }
+    const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)((g_ * nchunks + cc) * bytes_per_chunk_u));
+    const uint32_t m0 = __builtin_amdgcn_readfirstlane(w43_lds_addr(smem + G::U_OFF + uslot * G::USZ + 256 * wv));
+#pragma unroll
+    for (int q = Q0; q < Q1; ++q) w43_dma16(u_voff, r_u, so + q * 12288, m0 + q * 12288);
+  };
   auto dma_u = [&](int g_, int cc, int uslot) {
     if constexpr (SEDX_W43_ABL & 2) return;
     if constexpr (NT == 1) {   // unit wv of the 9 KiB slab (the 16-channel pack after the NT 4 pack)
@@ -317,8 +340,10 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
 #pragma unroll
     for (int q = 0; q < 3; ++q) w43_dma16(u_voff, r_u, so + q * 12288, m0 + q * 12288);
   };
-  auto dma_h = [&](uint32_t hof, int cc, int hslot) {
+  // planes P0 .. P1 - 1 of the halo DMA of chunk cc
+  auto dma_h_planes = [&](uint32_t hof, int cc, int hslot, auto p0_tag, auto p1_tag) {
     if constexpr (SEDX_W43_ABL & 1) return;
+    constexpr int P0 = decltype(p0_tag)::value, P1 = decltype(p1_tag)::value;
     const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)(16 * (C4 ? cc * T * F : cc)));
     // wave 11 (no block: its lanes' offsets are all out of range, halo_off)
     // writes its four zero DMAs into the trash block — a select, not a branch
@@ -326,10 +351,11 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
     const uint32_t m0 = __builtin_amdgcn_readfirstlane(
         w43_lds_addr(tw ? smem + G::HTRASH_OFF : smem + G::H_OFF + hslot * G::HALO + 64 * wv));
     const uint32_t pstep = tw ? 0u : 4u * PS;
-    w43_dma4(hof, r_in, so, m0);
-    w43_dma4(hof, r_in, so + 4, m0 + pstep);
-    w43_dma4(hof, r_in, so + 8, m0 + 2 * pstep);
-    w43_dma4(hof, r_in, so + 12, m0 + 3 * pstep);
+#pragma unroll
+    for (int q = P0; q < P1; ++q) w43_dma4(hof, r_in, so + 4 * q, m0 + q * pstep);
+  };
+  auto dma_h = [&](uint32_t hof, int cc, int hslot) {
+    dma_h_planes(hof, cc, hslot, std::integral_constant<int, 0>{}, std::integral_constant<int, 4>{});
   };
 
   // epilogue stores per wave per item (all issued: out-of-range ones go to
@@ -537,11 +563,45 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
       read_u(ua, I0{}, u0);
       read_u(ua, I1{}, u1);
       // group of step c: U(c + 2) -> the U slot of c - 1, halo(c + 3) -> the
-      // halo slot of c (read during step c - 1)
-      if (c + 2 < nchunks) dma_u(grp, c + 2, us2);
-      else dma_u(ng, c + 2 - nchunks, us2);
-      if (c + 3 < nchunks) dma_h(hof, c + 3, hs);
-      else dma_h(nhof, c + 3 - nchunks, hs);
+      // halo slot of c (read during step c - 1); SEDX_W43_DMA_SPLIT places
+      // its DMAs between the step's MFMA positions instead of all at its top
+      // (0: top; 1: U after position 0, halo after 1; 2: U unit q after
+      // position q, halo planes after positions 3 and 4).  Any placement
+      // inside the step keeps VM DMAs per wave between two barriers.
+      // (uniform branches on "this item / the next", not selects: a select
+      // of the per-lane halo offsets costs a VGPR the main loop does not have)
+      auto du = [&](auto q0, auto q1) {
+        if (c + 2 < nchunks) dma_u_units(grp, c + 2, us2, q0, q1);
+        else dma_u_units(ng, c + 2 - nchunks, us2, q0, q1);
+      };
+      auto dh = [&](auto p0, auto p1) {
+        if (c + 3 < nchunks) dma_h_planes(hof, c + 3, hs, p0, p1);
+        else dma_h_planes(nhof, c + 3 - nchunks, hs, p0, p1);
+      };
+      auto dmas_at = [&](auto ph_tag) {
+        constexpr int PH = decltype(ph_tag)::value;   // -1 top, j: after position j
+        using Z = std::integral_constant<int, 0>;
+        using O = std::integral_constant<int, 1>;
+        using W = std::integral_constant<int, 2>;
+        using H = std::integral_constant<int, 3>;
+        using Q = std::integral_constant<int, 4>;
+        if constexpr (SEDX_W43_DMA_SPLIT == 0) {
+          if constexpr (PH == -1) {
+            du(Z{}, H{});
+            dh(Z{}, Q{});
+          }
+        } else if constexpr (SEDX_W43_DMA_SPLIT == 1) {
+          if constexpr (PH == 0) du(Z{}, H{});
+          if constexpr (PH == 1) dh(Z{}, Q{});
+        } else {
+          if constexpr (PH == 0) du(Z{}, O{});
+          if constexpr (PH == 1) du(O{}, W{});
+          if constexpr (PH == 2) du(W{}, H{});
+          if constexpr (PH == 3) dh(Z{}, W{});
+          if constexpr (PH == 4) dh(W{}, Q{});
+        }
+      };
+      dmas_at(std::integral_constant<int, -1>{});
       fence();
       // position 0
       read_u(ua, I2{}, u2);
@@ -551,12 +611,14 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
       }
       wait_u(std::integral_constant<int, 2 + NP0>{}, u0);
       mfma4(0, u0, vc[0]);
+      dmas_at(std::integral_constant<int, 0>{});
       fence();
       // position 1; e from PA (, PB)
       read_u(ua, I3{}, u3);
       if constexpr (!LASTSTEP) read_row(ha, IPC{}, xc);
       wait_u(std::integral_constant<int, 2 + NP0 + NP>{}, u1);
       mfma4(1, u1, vc[1]);
+      dmas_at(std::integral_constant<int, 1>{});
       fence();
       if constexpr (!LASTSTEP) {
         wait_rr(std::integral_constant<int, 1 + NP>{}, xa, xb, u2);
@@ -568,6 +630,7 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
       read_u(ua, I4{}, u4);
       if constexpr (!LASTSTEP) read_row(ha, IPD{}, xd);
       mfma4(2, u2, vc[2]);
+      dmas_at(std::integral_constant<int, 2>{});
       fence();
       if constexpr (!LASTSTEP) {
         wait_r(std::integral_constant<int, 1 + NP>{}, xc, u3);
@@ -578,6 +641,7 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
       // position 3; fold PD
       read_u(ua, I5{}, u5);
       mfma4(3, u3, vc[3]);
+      dmas_at(std::integral_constant<int, 3>{});
       fence();
       if constexpr (!LASTSTEP) {
         wait_r(I1{}, xd, u4);
@@ -587,6 +651,7 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
       }
       // positions 4, 5; the column transform
       mfma4(4, u4, vc[4]);
+      dmas_at(std::integral_constant<int, 4>{});
       fence();
       if constexpr (!LASTSTEP) {
         w43_colt(e, vn);
