@@ -74,7 +74,7 @@ typedef float w43_f32x4 __attribute__((ext_vector_type(4)));
 #endif
 // where a step issues its LDS-DMAs (A/B builds; see the step)
 #ifndef SEDX_W43_DMA_SPLIT
-#define SEDX_W43_DMA_SPLIT 0
+#define SEDX_W43_DMA_SPLIT 5
 #endif
 
 // Diagnostic builds only (SEDX_W43_STAMPS, tools/wino43_bench.cpp): per-wave
@@ -593,6 +593,37 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
         } else if constexpr (SEDX_W43_DMA_SPLIT == 1) {
           if constexpr (PH == 0) du(Z{}, H{});
           if constexpr (PH == 1) dh(Z{}, Q{});
+        } else if constexpr (SEDX_W43_DMA_SPLIT == 3) {
+          if constexpr (PH == 1) du(Z{}, H{});
+          if constexpr (PH == 2) dh(Z{}, Q{});
+        } else if constexpr (SEDX_W43_DMA_SPLIT == 4) {
+          if constexpr (PH == 0) du(Z{}, H{});
+          if constexpr (PH == 2) dh(Z{}, Q{});
+        } else if constexpr (SEDX_W43_DMA_SPLIT == 5) {
+          if constexpr (PH == 0) du(Z{}, H{});
+          if constexpr (PH == 1) dh(Z{}, W{});
+          if constexpr (PH == 2) dh(W{}, Q{});
+        } else if constexpr (SEDX_W43_DMA_SPLIT == 8) {
+          if constexpr (PH == 0) du(Z{}, H{});
+          if constexpr (PH == 1) dh(Z{}, O{});
+          if constexpr (PH == 2) dh(O{}, W{});
+          if constexpr (PH == 3) dh(W{}, H{});
+          if constexpr (PH == 4) dh(H{}, Q{});
+        } else if constexpr (SEDX_W43_DMA_SPLIT == 10) {
+          if constexpr (PH == 0) du(Z{}, H{});
+          if constexpr (PH == 2) dh(Z{}, W{});
+          if constexpr (PH == 3) dh(W{}, Q{});
+        } else if constexpr (SEDX_W43_DMA_SPLIT == 11) {
+          if constexpr (PH == 0) du(Z{}, W{});
+          if constexpr (PH == 1) {
+            du(W{}, H{});
+            dh(Z{}, O{});
+          }
+          if constexpr (PH == 2) dh(O{}, H{});
+          if constexpr (PH == 3) dh(H{}, Q{});
+        } else if constexpr (SEDX_W43_DMA_SPLIT == 6) {
+          if constexpr (PH == 0) dh(Z{}, Q{});
+          if constexpr (PH == 1) du(Z{}, H{});
         } else {
           if constexpr (PH == 0) du(Z{}, O{});
           if constexpr (PH == 1) du(O{}, W{});
