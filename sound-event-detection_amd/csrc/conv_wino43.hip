@@ -73,6 +73,12 @@ typedef float w43_f32x4 __attribute__((ext_vector_type(4)));
 #define SEDX_W43_ABL 0
 #endif
 // where a step issues its LDS-DMAs (A/B builds; see the step)
+#ifndef SEDX_W43_PRIO
+#define SEDX_W43_PRIO 0   // A/B builds: static s_setprio for the later-dispatched waves
+#endif
+#ifndef SEDX_W43_USEL
+#define SEDX_W43_USEL 0
+#endif
 #ifndef SEDX_W43_DMA_SPLIT
 #define SEDX_W43_DMA_SPLIT 5
 #endif
@@ -571,8 +577,16 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
       // (uniform branches on "this item / the next", not selects: a select
       // of the per-lane halo offsets costs a VGPR the main loop does not have)
       auto du = [&](auto q0, auto q1) {
-        if (c + 2 < nchunks) dma_u_units(grp, c + 2, us2, q0, q1);
-        else dma_u_units(ng, c + 2 - nchunks, us2, q0, q1);
+        // SEDX_W43_USEL: the U source by scalar selects (group and chunk are
+        // wave-uniform) instead of two branch arms — not in the freq-mean
+        // build, whose allocation spills with it
+        if constexpr (SEDX_W43_USEL && EPI != EPI_FMEAN) {
+          const bool cur = c + 2 < nchunks;
+          dma_u_units(cur ? grp : ng, cur ? c + 2 : c + 2 - nchunks, us2, q0, q1);
+        } else {
+          if (c + 2 < nchunks) dma_u_units(grp, c + 2, us2, q0, q1);
+          else dma_u_units(ng, c + 2 - nchunks, us2, q0, q1);
+        }
       };
       auto dh = [&](auto p0, auto p1) {
         if (c + 3 < nchunks) dma_h_planes(hof, c + 3, hs, p0, p1);
@@ -603,6 +617,7 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
           if constexpr (PH == 0) du(Z{}, H{});
           if constexpr (PH == 1) dh(Z{}, W{});
           if constexpr (PH == 2) dh(W{}, Q{});
+
         } else if constexpr (SEDX_W43_DMA_SPLIT == 8) {
           if constexpr (PH == 0) du(Z{}, H{});
           if constexpr (PH == 1) dh(Z{}, O{});
@@ -911,6 +926,11 @@ __global__ __launch_bounds__(384 * TG, 1) void conv3x3_wino43_kernel(const float
                                                                 float* __restrict__ trash, int tb_per_clip,
                                                                 int ngroups, int order2d) {
   const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+#if SEDX_W43_PRIO == 1
+  if (wv >= 8) __builtin_amdgcn_s_setprio(1);   // the youngest wave of each SIMD
+#elif SEDX_W43_PRIO == 2
+  if (wv >= 4) __builtin_amdgcn_s_setprio(wv >= 8 ? 2 : 1);
+#endif
 #ifdef SEDX_W43_DELAY
   // diagnostic builds only (tools/wino43_bench.cpp): the odd workgroups of
   // the first resident round start SEDX_W43_DELAY cycles late, so half the
