@@ -929,7 +929,8 @@ __global__ __launch_bounds__(384 * TG, 1) void conv3x3_wino43_kernel(const float
 #if SEDX_W43_PRIO == 1
   if (wv >= 8) __builtin_amdgcn_s_setprio(1);   // the youngest wave of each SIMD
 #elif SEDX_W43_PRIO == 2
-  if (wv >= 4) __builtin_amdgcn_s_setprio(wv >= 8 ? 2 : 1);
+  if (wv >= 8) __builtin_amdgcn_s_setprio(2);
+  else if (wv >= 4) __builtin_amdgcn_s_setprio(1);
 #endif
 #ifdef SEDX_W43_DELAY
   // diagnostic builds only (tools/wino43_bench.cpp): the odd workgroups of
