@@ -74,10 +74,10 @@ typedef float w43_f32x4 __attribute__((ext_vector_type(4)));
 #endif
 // where a step issues its LDS-DMAs (A/B builds; see the step)
 #ifndef SEDX_W43_PRIO
-#define SEDX_W43_PRIO 0   // A/B builds: static s_setprio for the later-dispatched waves
+#define SEDX_W43_PRIO 2   // static s_setprio: waves 4-7 at 1, 8-11 at 2 (the later-dispatched waves of each SIMD)
 #endif
 #ifndef SEDX_W43_USEL
-#define SEDX_W43_USEL 0
+#define SEDX_W43_USEL 1
 #endif
 #ifndef SEDX_W43_DMA_SPLIT
 #define SEDX_W43_DMA_SPLIT 5
@@ -931,6 +931,9 @@ __global__ __launch_bounds__(384 * TG, 1) void conv3x3_wino43_kernel(const float
 #elif SEDX_W43_PRIO == 2
   if (wv >= 8) __builtin_amdgcn_s_setprio(2);
   else if (wv >= 4) __builtin_amdgcn_s_setprio(1);
+#elif SEDX_W43_PRIO == 3
+  if (wv < 4) __builtin_amdgcn_s_setprio(2);
+  else if (wv < 8) __builtin_amdgcn_s_setprio(1);
 #endif
 #ifdef SEDX_W43_DELAY
   // diagnostic builds only (tools/wino43_bench.cpp): the odd workgroups of
