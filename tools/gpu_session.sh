@@ -15,6 +15,8 @@
 #   prof           tools/profile_round.sh (rocprof kernel trace + PMC passes; env as there)
 #   ab=SETS        tools/ab_headline.sh: headline-leg A/B of '|'-separated bench argument sets (',' = ' ')
 #   rank2          python bench.py --gpus 2 --backend gloo (the N > 1 path, both ranks on GPU 0)
+#   sq             three rocprofv3 --pmc SQ passes of the headline (one stream) into gpurun_out/TAG/sq{1,2,3}
+#                  (tools/sq_summary.py input)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 TAG=${1:?tag}; shift
@@ -44,6 +46,14 @@ for s in "$@"; do
     prof) step prof 1100 tools/profile_round.sh ;;
     ab=*) step ab 900 tools/ab_headline.sh "$TAG/ab$n" "${s#*=}" ${AB_ROUNDS:-2} ;;
     rank2) step rank2 600 python -u bench.py --gpus 2 --backend gloo ;;
+    sq)
+      A="--no-cpu-baseline --no-side --streams 1 --steps 3 --warmup 1"
+      step sq1 150 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
+        SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $O/sq1 -o p -- python bench.py $A
+      step sq2 150 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT \
+        SQ_LDS_IDX_ACTIVE SQ_INSTS_SALU --output-format csv -d $O/sq2 -o p -- python bench.py $A
+      step sq3 150 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_MISC SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_VMEM \
+        SQ_ACTIVE_INST_SCA SQ_WAVES --output-format csv -d $O/sq3 -o p -- python bench.py $A ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
