@@ -76,9 +76,6 @@ typedef float w43_f32x4 __attribute__((ext_vector_type(4)));
 #ifndef SEDX_W43_PRIO
 #define SEDX_W43_PRIO 2   // static s_setprio: waves 4-7 at 1, 8-11 at 2 (the later-dispatched waves of each SIMD)
 #endif
-#ifndef SEDX_W43_MIDB
-#define SEDX_W43_MIDB 0
-#endif
 #ifndef SEDX_W43_USEL
 #define SEDX_W43_USEL 1
 #endif
@@ -556,24 +553,12 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
     // item's chunk 0 is computed after the epilogue, which keeps its registers
     // free).  LDS reads in issue order: U0 U1 | U2 PA PB | U3 PC | U4 PD | U5
     // — the counts below are the reads younger than the awaited one.
-    // SEDX_W43_MIDB: a step leaves its position-5 MFMAs (operands already in
-    // registers) to just after the next step's barrier, where every wave
-    // otherwise waits on its first LDS reads with no MFMA to issue
-    // (not in the F = 32 / 16 pooling builds, whose allocation spills with it)
-    constexpr bool MIDB = SEDX_W43_MIDB && !(EPI == EPI_POOL2 && (F == 32 || F == 16));
-    UF upend;
-    auto step = [&](const float (&vc)[6], float (&vn)[6], int c, auto first_tag, auto last_tag,
-                    auto zero_tag) {
+    auto step = [&](const float (&vc)[6], float (&vn)[6], int c, auto first_tag, auto last_tag) {
       constexpr bool FIRST = decltype(first_tag)::value, LASTSTEP = decltype(last_tag)::value;
-      constexpr bool ZERO = decltype(zero_tag)::value;   // the item's chunk 0: nothing pending
       constexpr int NP0 = LASTSTEP ? 0 : (PB >= 0 ? 6 : 3), NP = LASTSTEP ? 0 : 3;
       // U(c) and halo(c + 1) landed: issued two steps ago; younger: the
       // previous step's group (+ the epilogue stores over an item's first two steps)
       w43_bar<VM + (FIRST ? S : 0)>();
-      if constexpr (MIDB && !ZERO) {
-        mfma4(5, upend, vn[5]);   // chunk c - 1's position 5 (vn still holds its V)
-        fence();
-      }
       const int us1 = us == 2 ? 0 : us + 1, us2 = us1 == 2 ? 0 : us1 + 1;
       const int hs1 = hs == 2 ? 0 : hs + 1;
       const uint32_t ua = u_lane + us * (4 * G::USZ);
@@ -719,24 +704,20 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
         pin6(vn);
       }
       wait_u(I0{}, u5);
-      if constexpr (MIDB && !LASTSTEP) {
-        upend = u5;
-      } else {
-        mfma4(5, u5, vc[5]);
-      }
+      mfma4(5, u5, vc[5]);
       us = us1;
       hs = hs1;
     };
     // steps in pairs (ping-pong V); nchunks even (launcher: Cin % 8 == 0, >= 16)
     W43_MARK(0)
-    step(va, vb, 0, std::true_type{}, std::false_type{}, std::true_type{});
-    step(vb, va, 1, std::true_type{}, std::false_type{}, std::false_type{});
+    step(va, vb, 0, std::true_type{}, std::false_type{});
+    step(vb, va, 1, std::true_type{}, std::false_type{});
     for (int c = 2; c < nchunks - 2; c += 2) {
-      step(va, vb, c, std::false_type{}, std::false_type{}, std::false_type{});
-      step(vb, va, c + 1, std::false_type{}, std::false_type{}, std::false_type{});
+      step(va, vb, c, std::false_type{}, std::false_type{});
+      step(vb, va, c + 1, std::false_type{}, std::false_type{});
     }
-    step(va, vb, nchunks - 2, std::false_type{}, std::false_type{}, std::false_type{});
-    step(vb, va, nchunks - 1, std::false_type{}, std::true_type{}, std::false_type{});
+    step(va, vb, nchunks - 2, std::false_type{}, std::false_type{});
+    step(vb, va, nchunks - 1, std::false_type{}, std::true_type{});
 
     W43_MARK(1)
     // ---- epilogue.  Exchange area: the U slot of the last step (us + 2 now);

@@ -16,8 +16,10 @@ for src in conv conv_wino; do
   fi
 done
 [ tools/wino43_bench.cpp -nt $O/wino43_bench.o ] || [ ! -f $O/wino43_bench.o ] && $H -c tools/wino43_bench.cpp -o $O/wino43_bench.o &
-build_variant() {   # name flags
-  $H $2 -c $C/conv_wino43.hip -o $O/w43_$1.o && $H -o $O/w43_bench${1:+_$1} $O/wino43_bench.o $O/conv.o $O/conv_wino.o $O/w43_$1.o
+build_variant() {   # name flags (a SEDX_W43_STAMPS variant gets its own bench object, which prints the stamps)
+  local bo=$O/wino43_bench.o
+  if [[ "$2" == *SEDX_W43_STAMPS* ]]; then bo=$O/wino43_bench_$1.o; $H $2 -c tools/wino43_bench.cpp -o $bo || return 1; fi
+  $H $2 -c $C/conv_wino43.hip -o $O/w43_$1.o && $H -o $O/w43_bench${1:+_$1} $bo $O/conv.o $O/conv_wino.o $O/w43_$1.o
 }
 wait
 pids=()
