@@ -76,6 +76,9 @@ typedef float w43_f32x4 __attribute__((ext_vector_type(4)));
 #ifndef SEDX_W43_PRIO
 #define SEDX_W43_PRIO 2   // static s_setprio: waves 4-7 at 1, 8-11 at 2 (the later-dispatched waves of each SIMD)
 #endif
+#ifndef SEDX_W43_EPI2
+#define SEDX_W43_EPI2 0
+#endif
 #ifndef SEDX_W43_USEL
 #define SEDX_W43_USEL 1
 #endif
@@ -138,7 +141,10 @@ struct W43Geom {
   static constexpr int USZ = TG == 2 ? 36 * 4 * NCH : (USZ1 > XTG ? USZ1 : XTG);
   static constexpr int U_OFF = 0, H_OFF = NB * USZ, BIAS_OFF = H_OFF + NB * HALO, BIAS_MAX = 512;
   static constexpr int HTRASH_OFF = BIAS_OFF + BIAS_MAX;   // 64 dwords: wave 11's halo DMAs
-  static constexpr int LDS_BYTES = 4 * (HTRASH_OFF + 64);
+  // a second exchange area (SEDX_W43_EPI2, pooled / freq-mean epilogues): one
+  // tile group's [row 6][reg 2][z pair 2][lane 64][2] for registers 2, 3
+  static constexpr int X2_OFF = HTRASH_OFF + 64, X2 = SEDX_W43_EPI2 && TG == 2 ? 3072 : 0;
+  static constexpr int LDS_BYTES = 4 * (X2_OFF + X2);
   static constexpr int VM = 7;                       // DMAs per wave per step (3 U units + 4 halo planes)
 
   static_assert(F == 64 || F == 32 || F == 16 || F == 8, "F");
@@ -723,7 +729,15 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
     // ---- epilogue.  Exchange area: the U slot of the last step (us + 2 now);
     // every wave's reads of it are done at the first barrier below. ----
     float* const xfree = smem + G::U_OFF + (us == 0 ? 2 : us - 1) * G::USZ;
-    float* const xbuf0 = xfree + tg * G::XTG;
+    // SEDX_W43_EPI2 (pooled / freq-mean epilogues, two tile groups): all
+    // four registers of a channel tile per exchange round — half the rounds
+    // and barriers.  Registers 0, 1 of tile group tg at xfree + 3072 tg,
+    // registers 2, 3 at xfree + 6144 (tg 0) and in the area past the halo
+    // ring (tg 1); the U slot holds exactly the first three.
+    constexpr bool E2 = SEDX_W43_EPI2 && EPI != EPI_STORE && TG == 2 && !(SEDX_W43_ABL & 4);
+    constexpr int QS = E2 ? 2 : 1, NSR = E2 ? 4 : 2;   // rounds advance by QS; registers per round
+    float* const xbuf0 = E2 ? xfree + tg * 3072 : xfree + tg * G::XTG;
+    float* const xbuf1 = E2 ? (tg == 0 ? xfree + 6144 : smem + G::X2_OFF) : xbuf0;
     // output element base of the item: first output row t0 of clip b
     int le = lane;
     asm volatile("" : "+v"(le));   // opaque: offsets computed here, not hoisted as live registers
@@ -737,7 +751,7 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
     w43_f32x4 ost[NT];             // POOL2 / FMEAN: one 4-channel group per channel tile
     w43_f32x4 ost2[4];             // STORE: the 2 x 2 pixels of the current channel tile
 #pragma unroll
-    for (int q = 0; q < 2 * NT; ++q) {
+    for (int q = 0; q < 2 * NT; q += QS) {
       const int nt = q >> 1;
       if constexpr (SEDX_W43_ABL & 4) {   // timing build: no exchange / output transform
         if constexpr (ROW < 4) {
@@ -778,10 +792,11 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
       // 20-80 spilled VGPRs in the compiler's allocation: one buffer, two
       // barriers per round)
       if constexpr (!(SEDX_W43_ABL & 8)) w43_lds_bar();
-      float* const xb = xbuf0;
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const int r = 2 * (q & 1) + s;
+      for (int s4 = 0; s4 < NSR; ++s4) {
+        const int s = s4 & 1;
+        float* const xb = s4 < 2 ? xbuf0 : xbuf1;
+        const int r = E2 ? s4 : 2 * (q & 1) + s;
         float m[6], z[4];
 #pragma unroll
         for (int j = 0; j < 6; ++j) m[j] = acc[j][nt][r];
@@ -797,8 +812,10 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
       if constexpr (ROW < 4) {
         const int n = grp * 16 * NT + 16 * nt + 4 * kc;   // first of the lane's 4 channels
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          const int r = 2 * (q & 1) + s;
+        for (int s4 = 0; s4 < NSR; ++s4) {
+          const int s = s4 & 1;
+          const float* const xb = s4 < 2 ? xbuf0 : xbuf1;
+          const int r = E2 ? s4 : 2 * (q & 1) + s;
           const float bv = smem[G::BIAS_OFF + n + r];
           if constexpr (EPI == EPI_FMEAN) {
             // output row a = ROW of the tile: Y[ROW][0..3], ReLU, sum over
@@ -874,7 +891,7 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
             }
           }
         } else {   // POOL2 / FMEAN: the channel tile's 4 registers done: one 4-channel group
-          if (q & 1) {
+          if (E2 || (q & 1)) {
             float* dst;
             if constexpr (EPI == EPI_POOL2) {
               const int to = 2 * trg + (ROW >> 1), fo = 2 * tf + (ROW & 1);
