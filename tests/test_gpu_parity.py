@@ -363,11 +363,13 @@ def test_gru_exact_recurrence_is_fp32():
                                           ('winograd', 7.33)])
 def test_small_batch_shapes_bit_identical(prec, seconds):
     """Small batches run other kernel shapes — 32x32-wave-tile convs, the
-    barrier-free small-M linear, and (exact) the VALU fma-chain GRU product for
-    groups of <= 8 clips instead of 32-clip MFMAs.  Each keeps every output's
-    operation sequence, so a clip's outputs are bit-identical whether it runs
-    alone or inside a full 32-clip group (40 clips: a full MFMA group + a
-    ragged 8-clip group)."""
+    barrier-free small-M linear, (exact) the VALU fma-chain GRU product for
+    groups of <= 8 clips instead of 32-clip MFMAs, and (winograd) the
+    F(4x4,3x3) layers' 16-channel items with their own weight pack and, at
+    one or two clips, 16-tile items.  Each keeps every output's operation
+    sequence, so a clip's outputs are bit-identical whether it runs alone,
+    in a pair, in four, or inside a full 32-clip group (40 clips: a full MFMA
+    group + a ragged 8-clip group)."""
     m = build(GRU).set_precision(prec)
     # 7.33 s: odd frame counts after the pools (T 734 -> 367 -> 183 -> 91)
     wave = synth.make_waveforms(40, seconds=seconds, sample_rate=16000, seed=31)
@@ -378,6 +380,8 @@ def test_small_batch_shapes_bit_identical(prec, seconds):
             assert np.array_equal(one[k][0], full[k][i]), (prec, i, k, err(one[k][0], full[k][i]))
     four = run(m, wave[8:12])
     assert np.array_equal(four['framewise_output'], full['framewise_output'][8:12])
+    two = run(m, wave[20:22])
+    assert np.array_equal(two['framewise_output'], full['framewise_output'][20:22])
 
 
 def test_graphed_forward_bit_identical(model):

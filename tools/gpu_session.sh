@@ -7,6 +7,7 @@
 #   smoke          __graft_entry__ build() + smoke()
 #   tests          pytest -m gpu (all GPU tests)
 #   tests=EXPR     pytest -m gpu -k EXPR  (',' in EXPR reads as ' ')
+#   testsp=EXPR    the same with -s (the tests' printed errors in the log)
 #   bench          python bench.py (default command)
 #   bench=ARGS     python bench.py ARGS   (',' in ARGS reads as ' ')
 #   w43=B          tools/run/w43_bench B 20 (build first: tools/build_w43.sh)
@@ -37,6 +38,7 @@ for s in "$@"; do
   case $s in
     smoke) step smoke 300 python -u -c "import __graft_entry__ as g; g.build(); g.smoke()" ;;
     tests) step pytest 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ;;
+    testsp=*) step pytest 1100 python -u -m pytest tests -m gpu -x -v -s --timeout 300 --timeout-method thread -k "$arg" ;;
     tests=*) step pytest 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "$arg" ;;
     bench) step bench 600 python -u bench.py ;;
     bench=*) step bench 600 python -u bench.py $arg ;;
