@@ -41,9 +41,12 @@
 // tile group hit 16 distinct even bank pairs and the odd plane stride puts
 // channels k and k + 1 on the odd ones.  Two rings of 3: the U slab of chunk c
 // is read during step c and the halo of chunk c + 1 (for V of the next chunk)
-// during step c, so at the top of step c the workgroup issues U(c + 2) and
+// during step c, so during step c the workgroup issues U(c + 2) and
 // halo(c + 3) into the slots freed by step c - 1 — two steps of DMA lead for
-// both — behind one counted-vmcnt barrier.
+// both — behind one counted-vmcnt barrier per step.  The DMAs are issued
+// between the step's first MFMA positions, not at its top (round 6: with all
+// twelve waves issuing them right after the barrier the matrix pipes waited
+// on the DMA issue; blocks 1-4 2.27 -> 2.14 ms).
 //
 // Output transform: per register (channel, tile) a wave holds row ROW of M, so
 // z = (M A)_ROW is in-lane; Y = A^T M A sums the six rows' z across waves
@@ -316,9 +319,10 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
   const uint32_t u_voff1 = wv < 9 ? u_voff : 0x80000000u;
   const uint32_t u_voff2 = wv + 6 < 9 ? u_voff + 6144 : 0x80000000u;   // TG 1
   const uint32_t bytes_per_chunk_u = 4 * G::USZ;
-  // DMA of chunk cc of an item (halo offsets hof, channel group g_) into the
-  // given slots; U units wv, wv + 12, wv + 24 and this wave's halo block
-  // U units Q0 .. Q1 - 1 of chunk cc (NT 1: its one or two units with Q0 = 0)
+  // DMAs of chunk cc of an item (halo offsets hof, channel group g_) into
+  // the given slots: U units Q0 .. Q1 - 1 of wv, wv + 12, wv + 24 (NT 1: the
+  // wave's one or two units of the 16-channel slab, with Q0 = 0) and halo
+  // planes P0 .. P1 - 1 of this wave's halo block
   auto dma_u_units = [&](int g_, int cc, int uslot, auto q0_tag, auto q1_tag) {
     if constexpr (SEDX_W43_ABL & 2) return;
     constexpr int Q0 = decltype(q0_tag)::value, Q1 = decltype(q1_tag)::value;
@@ -338,19 +342,7 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
     for (int q = Q0; q < Q1; ++q) w43_dma16(u_voff, r_u, so + q * 12288, m0 + q * 12288);
   };
   auto dma_u = [&](int g_, int cc, int uslot) {
-    if constexpr (SEDX_W43_ABL & 2) return;
-    if constexpr (NT == 1) {   // unit wv of the 9 KiB slab (the 16-channel pack after the NT 4 pack)
-      const uint32_t so = __builtin_amdgcn_readfirstlane(
-          (uint32_t)(u_bytes / 2 + (g_ * nchunks + cc) * (4 * G::USZ1)));
-      const uint32_t m0 = __builtin_amdgcn_readfirstlane(w43_lds_addr(smem + G::U_OFF + uslot * G::USZ + 256 * wv));
-      w43_dma16(u_voff1, r_u, so, m0);
-      if constexpr (TG == 1) w43_dma16(u_voff2, r_u, so, m0 + 6144);   // unit wv + 6
-      return;
-    }
-    const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)((g_ * nchunks + cc) * bytes_per_chunk_u));
-    const uint32_t m0 = __builtin_amdgcn_readfirstlane(w43_lds_addr(smem + G::U_OFF + uslot * G::USZ + 256 * wv));
-#pragma unroll
-    for (int q = 0; q < 3; ++q) w43_dma16(u_voff, r_u, so + q * 12288, m0 + q * 12288);
+    dma_u_units(g_, cc, uslot, std::integral_constant<int, 0>{}, std::integral_constant<int, 3>{});
   };
   // planes P0 .. P1 - 1 of the halo DMA of chunk cc
   auto dma_h_planes = [&](uint32_t hof, int cc, int hslot, auto p0_tag, auto p1_tag) {
@@ -576,10 +568,11 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
       read_u(ua, I1{}, u1);
       // group of step c: U(c + 2) -> the U slot of c - 1, halo(c + 3) -> the
       // halo slot of c (read during step c - 1); SEDX_W43_DMA_SPLIT places
-      // its DMAs between the step's MFMA positions instead of all at its top
-      // (0: top; 1: U after position 0, halo after 1; 2: U unit q after
-      // position q, halo planes after positions 3 and 4).  Any placement
-      // inside the step keeps VM DMAs per wave between two barriers.
+      // them between the step's MFMA positions (5, default: U after position
+      // 0, halo planes 0-1 after 1 and 2-3 after 2; 0: all at the step top,
+      // round 5; 1, 2, 6, 11: the other measured placements, DESIGN.md §4
+      // Step schedule).  Any placement inside the step keeps VM DMAs per
+      // wave between two barriers.  (Placements after positions 3-4 spill.)
       // (uniform branches on "this item / the next", not selects: a select
       // of the per-lane halo offsets costs a VGPR the main loop does not have)
       auto du = [&](auto q0, auto q1) {
@@ -613,27 +606,10 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
         } else if constexpr (SEDX_W43_DMA_SPLIT == 1) {
           if constexpr (PH == 0) du(Z{}, H{});
           if constexpr (PH == 1) dh(Z{}, Q{});
-        } else if constexpr (SEDX_W43_DMA_SPLIT == 3) {
-          if constexpr (PH == 1) du(Z{}, H{});
-          if constexpr (PH == 2) dh(Z{}, Q{});
-        } else if constexpr (SEDX_W43_DMA_SPLIT == 4) {
-          if constexpr (PH == 0) du(Z{}, H{});
-          if constexpr (PH == 2) dh(Z{}, Q{});
         } else if constexpr (SEDX_W43_DMA_SPLIT == 5) {
           if constexpr (PH == 0) du(Z{}, H{});
           if constexpr (PH == 1) dh(Z{}, W{});
           if constexpr (PH == 2) dh(W{}, Q{});
-
-        } else if constexpr (SEDX_W43_DMA_SPLIT == 8) {
-          if constexpr (PH == 0) du(Z{}, H{});
-          if constexpr (PH == 1) dh(Z{}, O{});
-          if constexpr (PH == 2) dh(O{}, W{});
-          if constexpr (PH == 3) dh(W{}, H{});
-          if constexpr (PH == 4) dh(H{}, Q{});
-        } else if constexpr (SEDX_W43_DMA_SPLIT == 10) {
-          if constexpr (PH == 0) du(Z{}, H{});
-          if constexpr (PH == 2) dh(Z{}, W{});
-          if constexpr (PH == 3) dh(W{}, Q{});
         } else if constexpr (SEDX_W43_DMA_SPLIT == 11) {
           if constexpr (PH == 0) du(Z{}, W{});
           if constexpr (PH == 1) {
