@@ -31,6 +31,8 @@ step() {  # name timeout cmd...
   timeout -k 10 "$t" "$@" > "$O/$n.$name.log" 2>&1
   local rc=$?
   echo "== [$n] $name rc=$rc"; tail -n ${TAIL:-12} "$O/$n.$name.log" | cut -c1-400
+  # (w43_bench exits 1 on a numerical MISMATCH — expected of ablation builds — and keeps going)
+  if [ $rc -eq 1 ] && [[ $name == w43* ]]; then return 0; fi
   if [ $rc -ne 0 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
 }
 for s in "$@"; do
