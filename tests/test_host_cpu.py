@@ -269,6 +269,47 @@ def test_dataparallel_replicas_reuse_the_source_handle(monkeypatch):
     torch.save(m, buf)
 
 
+def test_weights_signature_follows_every_change(monkeypatch):
+    """The packed weights of a handle are re-made after any change the forward
+    must see, and only then: the per-call check (models._SedModel._signature)
+    re-walks the state_dict only after a parameter / buffer / submodule was
+    registered anywhere, and otherwise re-reads the cached tensors' storage
+    and version — so an in-place update, a `.data` swap, a replaced Parameter
+    and a new buffer each re-pack once, and a plain repeat does not."""
+    import torch
+    from sedx import models
+
+    loads = []
+
+    class FakeNative(object):          # stands in for the libsedx handle (no GPU here)
+        def __init__(self, cfg, idx):
+            self.device_index, self.signature, self.precision, self.h = idx, None, 'winograd', None
+
+        def load(self, sd):
+            loads.append(sorted(sd))
+
+    monkeypatch.setattr(models, '_Native', FakeNative)
+    m = models.Cnn_9layers_Gru_FrameAtt(16000, 512, 160, 64, 25, 7000, 25, 'logmel').eval()
+    dev = torch.device('cuda', 0)
+
+    def packs():
+        m.native(dev)
+        return len(loads)
+
+    assert packs() == 1 and packs() == 1
+    with torch.no_grad():
+        m.conv_block3.conv2.weight.mul_(0.5)               # in place: version counter
+    assert packs() == 2 and packs() == 2
+    m.bn0.weight.data = m.bn0.weight.data.clone()         # new storage, no registration
+    assert packs() == 3
+    m.att_block.cla.bias = torch.nn.Parameter(torch.zeros(25))   # replaced Parameter (registration hook)
+    assert packs() == 4 and packs() == 4
+    m.bn0.register_buffer('extra', torch.zeros(1))        # new state_dict key
+    assert packs() == 5 and 'bn0.extra' in loads[-1]
+    m.load_state_dict(m.state_dict())                      # copy_ into every tensor
+    assert packs() == 6 and packs() == 6
+
+
 def test_python_tuning_constants_match_the_header():
     """The ctypes mirror's knob numbers (sedx/_lib.py) and bench.py's GRU
     kernel table are the values include/sedx.h declares (a drifted number
