@@ -146,6 +146,13 @@ int main(int argc, char** argv) {
     }
     size_t c4diff = 0;
     for (size_t i = 0; i < nout; ++i) c4diff += std::memcmp(&o2[i], &o3n[i], 4) != 0;
+    // FNV-1a of the chunk-of-4 output's bits: equal across builds that must be bit-identical
+    unsigned long long ohash = 1469598103934665603ull;
+    for (size_t i = 0; i < nout; ++i) {
+      uint32_t u;
+      std::memcpy(&u, &o3[i], 4);
+      ohash = (ohash ^ u) * 1099511628211ull;
+    }
     // float64 reference (conv + bias + ReLU, then the epilogue)
     auto conv_px = [&](int b, int t, int f, int o) {
       double s = 0;
@@ -233,10 +240,10 @@ int main(int argc, char** argv) {
     const double fl4 = fl * 36.0 / 144.0;                           // F(4,3) matrix-pipe FLOPs (no tile padding)
     printf("%-5s B=%d T=%d  F(2,3) %.4f ms  F(4,3) nhwc %.4f  c4 %.4f ms (MFMA %.1f TF/s = %.3f of 157.3)  x%.2f  "
            "|w2-ref| %.2e |w4-ref| max %.2e rms %.2e  max|ref| %.2f  checked %zu nonfinite %zu  c4!=nhwc %zu  "
-           "[nt4 %.4f nt1 %.4f nt1/16 tiles %.4f ms, differing %zu]  %s\n",
+           "[nt4 %.4f nt1 %.4f nt1/16 tiles %.4f ms, differing %zu]  h %016llx  %s\n",
            l.name, l.B, l.T, m2, m4, m4c, m4c > 0 ? fl4 / m4c / 1e9 : 0.0, m4c > 0 ? fl4 / m4c / 1e9 / 157.3 : 0.0,
            m4c > 0 ? m2 / m4c : 0.0, e2max, e4max, std::sqrt(e4sq / std::max<size_t>(1, nchk)), omax, nchk, nan,
-           c4diff, mn4, mn1, mt1, ntdiff, lok ? "OK" : "MISMATCH");
+           c4diff, mn4, mn1, mt1, ntdiff, ohash, lok ? "OK" : "MISMATCH");
     fflush(stdout);
   }
   // block 1 as the library runs it: the fused F(2,3) launch against conv1
