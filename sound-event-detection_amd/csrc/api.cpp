@@ -409,6 +409,11 @@ sedx_status run_body(sedx_handle* h, int64_t B, const Geometry& g, float* ws, co
     else if (!wb1)
       launch_pad_x0(X0, iB, (int)g.T, A, s);
   };
+  // claim counters of the x3 launches and of the F(4x4,3x3) launches (the
+  // workspace comes from the caller: zeroed once per forward, ahead of the
+  // pipelined wait — this forward's memory only)
+  const bool w43 = h->precision == SEDX_PRECISION_WINOGRAD && h->wino_f43;
+  if (x3 || w43) HIP_TRY(h, hipMemsetAsync(sched, 0, 7 * CONV_SCHED_INTS * sizeof(int), s));
   const bool first_early = h->pipelined && h->pipe_conv1_first;
   if (first_early) block1_first();
   if (h->pipelined && h->conv_done_recorded) HIP_TRY(h, hipStreamWaitEvent(s, h->conv_done, 0));
@@ -416,7 +421,6 @@ sedx_status run_body(sedx_handle* h, int64_t B, const Geometry& g, float* ws, co
   capture(h, 0, X0, (size_t)B * g.T * 64, s);
   // block 1 as one launch in both modes: conv1 computed inside conv2's halo
   // staging (the b1c1 stage is just the zero-bordered copy of the bn0 output)
-  if (x3) HIP_TRY(h, hipMemsetAsync(sched, 0, 7 * CONV_SCHED_INTS * sizeof(int), s));
   if (!first_early) block1_first();
   struct L {
     const float* in;
@@ -438,7 +442,7 @@ sedx_status run_body(sedx_handle* h, int64_t B, const Geometry& g, float* ws, co
                              sched, s);
     else if (i == 0 && b1_43)
       launch_conv3x3_wino43(A, iB, c.T, 64, 64, 64, w.wu43[c.idx], w.cb[c.idx], c.out, EPI_POOL2, w.trash, s,
-                            h->wino_order, c4);
+                            h->wino_order, c4, 0, sched);
     else if (i == 0 && wb1 && h->wino_block1 == 2)
       launch_block1_wino(X0, iB, c.T, w.c1_w, w.c1_b, w.wu[c.idx], w.cb[c.idx], c.out, w.zero, w.trash, s, c4);
     else if (i == 0 && wb1)
@@ -450,7 +454,7 @@ sedx_status run_body(sedx_handle* h, int64_t B, const Geometry& g, float* ws, co
                         sched + i * CONV_SCHED_INTS, s);
     else if (h->precision == SEDX_PRECISION_WINOGRAD && h->wino_f43)
       launch_conv3x3_wino43(c.in, iB, c.T, c.F, c.cin, c.cout, w.wu43[c.idx], w.cb[c.idx], c.out, c.epi, w.trash, s,
-                            h->wino_order, c4);
+                            h->wino_order, c4, 0, sched + i * CONV_SCHED_INTS);
     else if (h->precision == SEDX_PRECISION_WINOGRAD)
       launch_conv3x3_wino(c.in, iB, c.T, c.F, c.cin, c.cout, w.wu[c.idx], w.cb[c.idx], c.out, c.epi, w.zero, w.trash,
                           s, h->wino_order);

@@ -88,6 +88,20 @@ typedef float w43_f32x4 __attribute__((ext_vector_type(4)));
 #ifndef SEDX_W43_DMA_SPLIT
 #define SEDX_W43_DMA_SPLIT 5
 #endif
+// Item claims (SEDX_W43_CLAIM 1, the default; launches with more items than
+// CUs): a persistent grid, one workgroup per CU, whose workgroups claim their
+// items from the counter of their XCD lane x = blockIdx & 7 (items 8 v + x,
+// the static decode's XCD mapping), so a workgroup that starts late — its CU
+// held by the other batch's GRU — takes fewer items instead of costing a
+// whole extra round.  The first two items come in one claim at the top; the
+// item after next is claimed at an item's epilogue by its last wave (not a
+// finisher) and lands in LDS before the epilogue's last round, read by every
+// wave at the next item's top.  Counters (sched): 8 ints 128 B apart + a
+// done count at [255], zero at launch; the last workgroup to finish zeroes
+// them again.  0: the static grid-stride order of round 5 (A/B builds).
+#ifndef SEDX_W43_CLAIM
+#define SEDX_W43_CLAIM 1
+#endif
 
 // Diagnostic builds only (SEDX_W43_STAMPS, tools/wino43_bench.cpp): per-wave
 // s_memtime intervals summed over every wave of every 16th workgroup:
@@ -147,7 +161,8 @@ struct W43Geom {
   // a second exchange area (SEDX_W43_EPI2, pooled / freq-mean epilogues): one
   // tile group's [row 6][reg 2][z pair 2][lane 64][2] for registers 2, 3
   static constexpr int X2_OFF = HTRASH_OFF + 64, X2 = SEDX_W43_EPI2 && TG == 2 ? 3072 : 0;
-  static constexpr int LDS_BYTES = 4 * (X2_OFF + X2);
+  static constexpr int CL_OFF = X2_OFF + X2;         // item claims: the landed claim ([0]) and the first item ([1])
+  static constexpr int LDS_BYTES = 4 * (CL_OFF + (SEDX_W43_CLAIM ? 4 : 0));
   static constexpr int VM = 7;                       // DMAs per wave per step (3 U units + 4 halo planes)
 
   static_assert(F == 64 || F == 32 || F == 16 || F == 8, "F");
@@ -233,7 +248,7 @@ template <int F, int EPI, int ROW, bool C4, int NT, int TG>
 __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, int T, int Cin, int Cout,
                                          const float* __restrict__ U, int u_bytes, const float* __restrict__ bias,
                                          float* __restrict__ out, float* __restrict__ trash, int tb_per_clip,
-                                         int ngroups, int order2d, int wv) {
+                                         int ngroups, int order2d, int* __restrict__ sched, int wv) {
   using G = W43Geom<F, TG>;
   constexpr int RS = G::RS, PS = G::PS;
   static_assert(TG == 2 || (NT == 1 && (F == 16 || F == 8)), "16-tile items: 16-channel, F = 16 / 8 only");
@@ -292,7 +307,35 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
   };
   int item = blockIdx.x;
   int b = 0, t0 = 0, grp = 0;
-  if (!decode(item, b, t0, grp)) return;   // uniform
+  // item claims (sched non-null, wave-uniform); static grid-stride otherwise
+  const bool claims = SEDX_W43_CLAIM && sched != nullptr;
+  int* const cl = reinterpret_cast<int*>(smem + G::CL_OFF);
+  const int clx = blockIdx.x & 7;
+  // the workgroup's end: after its last claim landed; the last workgroup
+  // zeroes the counters for the next launch on them
+  auto claim_done = [&]() {
+    if constexpr (SEDX_W43_CLAIM && ROW == 5) {
+      if (claims && wv == G::WAVES - 1 && lane == 0 && atomicAdd(&sched[255], 1) == (int)gridDim.x - 1) {
+#pragma unroll
+        for (int x = 0; x < 8; ++x) __hip_atomic_store(&sched[32 * x], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&sched[255], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  };
+  if (claims) {
+    // the first two items in one claim; all waves wait for it (once per workgroup)
+    if (wv == G::WAVES - 1 && lane == 0) {
+      const int v = atomicAdd(&sched[32 * clx], 2);
+      cl[1] = 8 * v + clx;
+      cl[0] = 8 * (v + 1) + clx;
+    }
+    __syncthreads();
+    item = __builtin_amdgcn_readfirstlane(cl[1]);
+  }
+  if (!decode(item, b, t0, grp)) {   // uniform
+    claim_done();
+    return;
+  }
 
   // this lane's tile within the item
   const int tr = (F == 16 ? 4 * tg : F == 8 ? 8 * tg : F == 64 ? tg : 0) + nn / G::TFG;
@@ -531,7 +574,12 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
     // previous item's step n - 3 and every wave waited for it before that
     // item's last step's barrier: no wait here
     transform(hs, va);
-    const int nitem = item + (int)gridDim.x;
+    int nitem = item + (int)gridDim.x;
+    if (claims) {   // landed by the previous epilogue (or the kernel top)
+      fence();
+      nitem = __builtin_amdgcn_readfirstlane(*reinterpret_cast<volatile int*>(cl));
+      fence();
+    }
     int nb_ = 0, nt0 = 0, ng = 0;
     const bool has_next = decode(nitem, nb_, nt0, ng);
     const uint32_t nhof = has_next ? halo_off(nb_, nt0) : hof;
@@ -705,6 +753,11 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
     // ---- epilogue.  Exchange area: the U slot of the last step (us + 2 now);
     // every wave's reads of it are done at the first barrier below. ----
     float* const xfree = smem + G::U_OFF + (us == 0 ? 2 : us - 1) * G::USZ;
+    // item claims: the item after next, claimed here and landed before the last round
+    int claim_v = 0;
+    if constexpr (SEDX_W43_CLAIM && ROW == 5) {
+      if (claims && has_next && wv == G::WAVES - 1 && lane == 0) claim_v = atomicAdd(&sched[32 * clx], 1);
+    }
     // SEDX_W43_EPI2 (pooled / freq-mean epilogues, two tile groups): all
     // four registers of a channel tile per exchange round — half the rounds
     // and barriers.  Registers 0, 1 of tile group tg at xfree + 3072 tg,
@@ -767,6 +820,9 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
       // (double-buffering the rounds by parity, one barrier per round, cost
       // 20-80 spilled VGPRs in the compiler's allocation: one buffer, two
       // barriers per round)
+      if constexpr (SEDX_W43_CLAIM && ROW == 5) {
+        if (claims && q == 2 * NT - QS && has_next && wv == G::WAVES - 1 && lane == 0) *reinterpret_cast<volatile int*>(cl) = 8 * claim_v + clx;
+      }
       if constexpr (!(SEDX_W43_ABL & 8)) w43_lds_bar();
 #pragma unroll
       for (int s4 = 0; s4 < NSR; ++s4) {
@@ -829,6 +885,8 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
               for (int i = 0; i < 6; ++i) col[i] = src[xs(i, s)];
               w43_at(col, yy);
               ost2[j][r] = fmaxf(yy[ROW] + bv, 0.0f);
+              // (claim builds: one store's chain at a time, else the allocator spills)
+              if constexpr (SEDX_W43_CLAIM) __builtin_amdgcn_sched_barrier(0);
             }
           } else {
             // POOL2: the 2 x 2 block (2A, 2A + 1) x (2B, 2B + 1) of the tile
@@ -893,6 +951,7 @@ __device__ __forceinline__ void w43_body(const float* __restrict__ in, int B, in
     grp = ng;
     hof = nhof;
   }
+  claim_done();
 #ifdef SEDX_W43_STAMPS
   if (lane == 0 && (blockIdx.x & 15) == 0) {
     w43_st[3] = __builtin_amdgcn_s_memtime() - w43_t0;
@@ -917,7 +976,7 @@ __global__ __launch_bounds__(384 * TG, 1) void conv3x3_wino43_kernel(const float
                                                                 int Cout, const float* __restrict__ U, int u_bytes,
                                                                 const float* __restrict__ bias, float* __restrict__ out,
                                                                 float* __restrict__ trash, int tb_per_clip,
-                                                                int ngroups, int order2d) {
+                                                                int ngroups, int order2d, int* __restrict__ sched) {
   const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
 #if SEDX_W43_PRIO == 1
   if (wv >= 8) __builtin_amdgcn_s_setprio(1);   // the youngest wave of each SIMD
@@ -939,7 +998,7 @@ __global__ __launch_bounds__(384 * TG, 1) void conv3x3_wino43_kernel(const float
   }
 #endif
   SEDX_W43_ROWS(F, EPI, C4, NT, TG, in, B, T, Cin, Cout, U, u_bytes, bias, out, trash, tb_per_clip, ngroups, order2d,
-                wv)
+                sched, wv)
 }
 #undef SEDX_W43_ROWS
 
@@ -958,7 +1017,8 @@ __global__ __launch_bounds__(384 * TG, 1) void conv3x3_wino43_kernel(const float
 // 16- (nt1) or 64-channel items
 template <int F, int TG>
 static void launch_w43_g(const float* in, int B, int T, int Cin, int Cout, const float* U, const float* bias,
-                         float* out, int epi, float* trash, int order, bool c4, bool nt1, int ncu, hipStream_t s) {
+                         float* out, int epi, float* trash, int order, bool c4, bool nt1, int ncu, int* sched,
+                         hipStream_t s) {
   using G = W43Geom<F, TG>;
   // output rows the epilogue covers: POOL2 drops an odd last row
   const int rows = epi == EPI_POOL2 ? 2 * (T / 2) : T;
@@ -973,7 +1033,14 @@ static void launch_w43_g(const float* in, int B, int T, int Cin, int Cout, const
     return note_launch_error(hipErrorInvalidValue);
   const int64_t resident = (int64_t)ncu / 8 * 8;
   const int64_t per = (nitems + SEDX_W43_ITEMS - 1) / SEDX_W43_ITEMS;
-  const int64_t nwg = std::min<int64_t>(nitems, std::max<int64_t>(std::max<int64_t>(8, resident), (per + 7) / 8 * 8));
+  int64_t nwg = std::min<int64_t>(nitems, std::max<int64_t>(std::max<int64_t>(8, resident), (per + 7) / 8 * 8));
+  // item claims where there are more than two items per CU: one persistent
+  // workgroup per CU (nwg a multiple of 8: every XCD lane has workgroups).
+  // Below that the first claim's latency is not amortised (B = 4 block 1:
+  // 0.0645 vs 0.0627 ms static, profiles/r06zb_*) and the static order runs.
+  const bool claim = SEDX_W43_CLAIM && sched != nullptr && nitems > 2 * resident && resident >= 8;
+  if (claim) nwg = resident;
+  int* const sched_k = claim ? sched : nullptr;
   // rounds of 32 / G tile blocks x G channel groups (conv_wino.hip): the G
   // whose round streams the fewest bytes through an XCD's L2
   int order2d = F == 64 && order == 2 && !nt1 ? -1 : 0;
@@ -1000,7 +1067,7 @@ static void launch_w43_g(const float* in, int B, int T, int Cin, int Cout, const
   {                                                                                                         \
     if (!launch_info(reinterpret_cast<const void*>(k_), G::THREADS, G::LDS_BYTES, c4).ok) return;           \
     hipLaunchKernelGGL(k_, dim3((unsigned)nwg), dim3(G::THREADS), G::LDS_BYTES, s, in, B, T, Cin, Cout, U,  \
-                       (int)u_bytes, bias, out, trash, tb_per_clip, ngroups, order2d);                      \
+                       (int)u_bytes, bias, out, trash, tb_per_clip, ngroups, order2d, sched_k);             \
     return;                                                                                                 \
   }
 #define SEDX_W43_LAUNCH(E)                                                                                  \
@@ -1032,7 +1099,8 @@ static void launch_w43_g(const float* in, int B, int T, int Cin, int Cout, const
 // tiles; 2 = 16-channel items of 16 tiles (F = 16 / 8, chunk-of-4)
 template <int F>
 static void launch_w43_f(const float* in, int B, int T, int Cin, int Cout, const float* U, const float* bias,
-                         float* out, int epi, float* trash, int order, bool c4, int nt_force, hipStream_t s) {
+                         float* out, int epi, float* trash, int order, bool c4, int nt_force, int* sched,
+                         hipStream_t s) {
   using G = W43Geom<F>;
   const int rows = epi == EPI_POOL2 ? 2 * (T / 2) : T;
   const int64_t tblocks = (int64_t)B * (((rows + 3) / 4 + G::TRW - 1) / G::TRW);
@@ -1051,14 +1119,14 @@ static void launch_w43_f(const float* in, int B, int T, int Cin, int Cout, const
                    (nt_force ? nt_force == 2 : 8 * ((Cout / 16 + 7) / 8) * tblocks < ncu);
   if (nt_force == 2 && !tg1) return note_launch_error(hipErrorInvalidValue);
   if constexpr (tg1_ok) {
-    if (tg1) return launch_w43_g<F, 1>(in, B, T, Cin, Cout, U, bias, out, epi, trash, order, c4, true, ncu, s);
+    if (tg1) return launch_w43_g<F, 1>(in, B, T, Cin, Cout, U, bias, out, epi, trash, order, c4, true, ncu, sched, s);
   }
-  launch_w43_g<F, 2>(in, B, T, Cin, Cout, U, bias, out, epi, trash, order, c4, nt1, ncu, s);
+  launch_w43_g<F, 2>(in, B, T, Cin, Cout, U, bias, out, epi, trash, order, c4, nt1, ncu, sched, s);
 }
 
 void launch_conv3x3_wino43(const float* in, int B, int T, int F, int Cin, int Cout, const float* U43,
                            const float* bias, float* out, int epi, float* trash, hipStream_t s, int order, bool c4,
-                           int nt_force) {
+                           int nt_force, int* sched) {
   if (Cin % 8 != 0 || Cin < 16 || Cout % 64 != 0 || Cout > 512 || B <= 0 || T <= 0)
     return note_launch_error(hipErrorInvalidValue);
   // byte offsets are 32-bit (buffer DMA): batches whose input passes 2^31
@@ -1073,10 +1141,10 @@ void launch_conv3x3_wino43(const float* in, int B, int T, int F, int Cin, int Co
     const float* in_s = in + b0 * in_clip;
     float* out_s = out + b0 * out_clip;
     switch (F) {
-      case 64: launch_w43_f<64>(in_s, bs, T, Cin, Cout, U43, bias, out_s, epi, trash, order, c4, nt_force, s); break;
-      case 32: launch_w43_f<32>(in_s, bs, T, Cin, Cout, U43, bias, out_s, epi, trash, order, c4, nt_force, s); break;
-      case 16: launch_w43_f<16>(in_s, bs, T, Cin, Cout, U43, bias, out_s, epi, trash, order, c4, nt_force, s); break;
-      case 8: launch_w43_f<8>(in_s, bs, T, Cin, Cout, U43, bias, out_s, epi, trash, order, c4, nt_force, s); break;
+      case 64: launch_w43_f<64>(in_s, bs, T, Cin, Cout, U43, bias, out_s, epi, trash, order, c4, nt_force, sched, s); break;
+      case 32: launch_w43_f<32>(in_s, bs, T, Cin, Cout, U43, bias, out_s, epi, trash, order, c4, nt_force, sched, s); break;
+      case 16: launch_w43_f<16>(in_s, bs, T, Cin, Cout, U43, bias, out_s, epi, trash, order, c4, nt_force, sched, s); break;
+      case 8: launch_w43_f<8>(in_s, bs, T, Cin, Cout, U43, bias, out_s, epi, trash, order, c4, nt_force, sched, s); break;
       default: return note_launch_error(hipErrorInvalidValue);
     }
   }

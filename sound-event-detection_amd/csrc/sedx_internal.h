@@ -136,10 +136,12 @@ void pack_conv_wino(const double* wf, int Cin, int Cout, float* U);   // U: Cin 
 // 128 floats of device scratch for the out-of-range epilogue stores.
 // c4: input and output in the chunk-of-4 layout [B][C/4][T][F][4] (the
 // freq-mean output stays [B][T][C]); else NHWC.  Batches are split over whole
-// clips, so B-major offsets hold in both layouts.
+// clips, so B-major offsets hold in both layouts.  sched: CONV_SCHED_INTS
+// zeroed ints (item-claim counters; left zero by the launch) or nullptr =
+// the static item order — the same outputs either way.
 void launch_conv3x3_wino43(const float* in, int B, int T, int F, int Cin, int Cout, const float* U43,
                            const float* bias, float* out, int epi, float* trash, hipStream_t s, int order = 0,
-                           bool c4 = false, int nt_force = 0);
+                           bool c4 = false, int nt_force = 0, int* sched = nullptr);
 // [B][C/4][T][F][4] -> [B][T][F][C] (stage captures of the C4 layers)
 void launch_c4_to_nhwc(const float* src, int B, int T, int F, int C, float* dst, hipStream_t s);
 void pack_conv_wino43(const double* wf, int Cin, int Cout, float* U);   // U: 2 * Cin * Cout * 36 floats

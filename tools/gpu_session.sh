@@ -13,6 +13,7 @@
 #   w43=B          tools/run/w43_bench B 20 (build first: tools/build_w43.sh)
 #   w43v=NAME:B    tools/run/w43_bench_NAME B 20 (a VARIANTS build)
 #   w43o=ORDER:B   tools/run/w43_bench B 20 with W43_ORDER=ORDER (item order A/B)
+#   w43s=B         tools/run/w43_bench B 20 with W43_SCHED=0 (static item order, no claims)
 #   prof           tools/profile_round.sh (rocprof kernel trace + PMC passes; env as there)
 #   ab=SETS        tools/ab_headline.sh: headline-leg A/B of '|'-separated bench argument sets (',' = ' ')
 #   rank2          python bench.py --gpus 2 --backend gloo (the N > 1 path, both ranks on GPU 0)
@@ -47,6 +48,7 @@ for s in "$@"; do
     w43=*) step w43_b$arg 200 tools/run/w43_bench $arg 20 ;;
     w43v=*) v=${arg%%:*}; b=${arg#*:}; step w43_${v}_b$b 200 tools/run/w43_bench_$v $b 20 ;;
     w43o=*) o=${arg%%:*}; b=${arg#*:}; step w43_o${o}_b$b 200 env W43_ORDER=$o tools/run/w43_bench $b 20 ;;
+    w43s=*) step w43_static_b$arg 200 env W43_SCHED=0 tools/run/w43_bench $arg 20 ;;
     prof) step prof 1100 tools/profile_round.sh ;;
     ab=*) step ab 900 tools/ab_headline.sh "$TAG/ab$n" "${s#*=}" ${AB_ROUNDS:-2} ;;
     rank2) step rank2 600 python -u bench.py --gpus 2 --backend gloo ;;

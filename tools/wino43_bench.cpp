@@ -13,9 +13,6 @@
 #include "../sound-event-detection_amd/csrc/sedx_internal.h"
 
 namespace sedx {
-void launch_conv3x3_wino43(const float* in, int B, int T, int F, int Cin, int Cout, const float* U43,
-                           const float* bias, float* out, int epi, float* trash, hipStream_t s, int order, bool c4,
-                           int nt_force);
 void pack_conv_wino43(const double* wf, int Cin, int Cout, float* U);
 #ifdef SEDX_W43_STAMPS
 void w43_stamps_rw(unsigned long long* h, bool reset);
@@ -56,6 +53,11 @@ int main(int argc, char** argv) {
   hipMalloc(&d_bias, 512 * 4); hipMalloc(&d_u, max_w * 4); hipMalloc(&d_u43, max_w * 4);
   hipMalloc(&d_zero, 4096); hipMemset(d_zero, 0, 4096);
   hipMalloc(&d_trash, 64 * 256 * 4);
+  hipMemset(d_trash, 0, 64 * 256 * 4);
+  // the F(4,3) item-claim counters (past the first 32 KiB, zero; every launch
+  // leaves them zero); W43_SCHED=0: the static item order (same outputs)
+  int* const d_sched = getenv("W43_SCHED") && atoi(getenv("W43_SCHED")) == 0 ? nullptr
+                                                                            : reinterpret_cast<int*>(d_trash + 8192);
   hipEvent_t e0, e1;
   hipEventCreate(&e0); hipEventCreate(&e1);
   std::mt19937 rng(7);
@@ -102,17 +104,17 @@ int main(int argc, char** argv) {
     };
     auto w4 = [&]() {
       sedx::launch_conv3x3_wino43(d_in, l.B, l.T, l.F, l.cin, l.cout, d_u43, d_bias, d_o2, l.epi, d_trash, 0, order,
-                                  false, 0);
+                                  false, 0, d_sched);
     };
     auto w4c = [&]() {   // chunk-of-4 layout in and out (the library's F(4,3) chain)
       sedx::launch_conv3x3_wino43(d_in4, l.B, l.T, l.F, l.cin, l.cout, d_u43, d_bias, d_o3, l.epi, d_trash, 0, order,
-                                  true, 0);
+                                  true, 0, d_sched);
     };
     // the C4 launch forced to 64-channel (4) / 16-channel (1) items: the
     // launcher's choice of item width never changes a bit of the output
     auto w4f = [&](int ntf, float* o) {
       sedx::launch_conv3x3_wino43(d_in4, l.B, l.T, l.F, l.cin, l.cout, d_u43, d_bias, o, l.epi, d_trash, 0, order,
-                                  true, ntf);
+                                  true, ntf, d_sched);
     };
     if (with2) w2();
     w4();
@@ -300,7 +302,7 @@ int main(int argc, char** argv) {
     const float m_c1 = timeit([&]() { sedx::launch_conv1_c4(d_x0, B, T, d_w1, d_b1, d_a4, 0); });
     const float m_c2 = timeit([&]() {
       sedx::launch_conv3x3_wino43(d_a4, B, T, 64, 64, 64, d_u43, d_bias, d_ob, sedx::EPI_POOL2, d_trash, 0, order, true,
-                                  0);
+                                  0, d_sched);
     });
     printf("block1 B=%d T=%d  fused F(2,3) %.4f ms  conv1_c4 %.4f + F(4,3) conv2 %.4f = %.4f ms  (x%.2f)  "
            "conv1 c4 vs nhwc differing %zu\n",
