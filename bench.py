@@ -454,13 +454,13 @@ def stage_times_isolated(model, wave, dev, reps):
 # from the rocprofv3 passes of this bench command (tools/profile_round.sh ->
 # tools/pmc_summary.py; FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE),
 # committed under profiles/.
-PROFILE_SUMMARY = os.path.join(REPO, 'profiles', 'r06z_winograd_kernel_summary.json')
+PROFILE_SUMMARY = os.path.join(REPO, 'profiles', 'r06zd_winograd_kernel_summary.json')
 # the same passes over the config-4 leg (bench.py --mode gamma: B = 32 x 10 s
 # @ 32 kHz, T = 994 frames)
-GAMMA_PROFILE_SUMMARY = os.path.join(REPO, 'profiles', 'r06z_config4_kernel_summary.json')
+GAMMA_PROFILE_SUMMARY = os.path.join(REPO, 'profiles', 'r06zd_config4_kernel_summary.json')
 # the same passes over the window-mode leg (bench.py --mode window: B' = 192
 # windows x 501 frames per call)
-WINDOW_PROFILE_SUMMARY = os.path.join(REPO, 'profiles', 'r06z_window_kernel_summary.json')
+WINDOW_PROFILE_SUMMARY = os.path.join(REPO, 'profiles', 'r06zd_window_kernel_summary.json')
 GAMMA_KERNELS = ('sedx::gamma_init_kernel', 'sedx::gamma_spec_kernel<2048>', 'sedx::gamma_erb_kernel',
                  'sedx::gamma_quant_kernel')
 
