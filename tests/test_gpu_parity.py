@@ -848,6 +848,43 @@ def test_wino_order_bit_identical():
         assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2]), n
 
 
+def test_wino43_item_claims_dirty_workspace_and_regimes():
+    """The F(4x4,3x3) launches of a B = 32 forward claim their items from
+    counters in the caller's workspace (more than two items per CU); B = 4
+    runs the static item order.  A workspace filled with 0xFF bytes, two
+    forwards back to back on it, and the same clips inside the two batch
+    sizes all give the same framewise output bit for bit (the forward zeroes
+    its counters; the item order never changes an output)."""
+    import ctypes
+    from sedx import _lib
+    from sedx.models import _ptr
+    m = build(GRU).set_precision('winograd')
+    wave = torch.from_numpy(synth.make_waveforms(32, seconds=10.0, sample_rate=16000, seed=77)).cuda()
+    with torch.no_grad():
+        ref = m(wave)['framewise_output'].clone()
+        small = m(wave[:4].contiguous())['framewise_output'].clone()
+    assert torch.isfinite(ref).all()
+    assert torch.equal(ref[:4], small)
+    nat = m.native(wave.device)
+    L = _lib.lib()
+    B, length = wave.shape
+    wsz = ctypes.c_size_t()
+    _lib.check(L.sedx_workspace_size(nat.h, B, length, ctypes.byref(wsz)), nat.h, 'workspace_size')
+    ws = torch.full((wsz.value,), 255, dtype=torch.uint8, device=wave.device)
+    fw = torch.empty_like(ref)
+    clip = torch.empty((B, ref.shape[2]), dtype=torch.float32, device=wave.device)
+    fr, sl = ctypes.c_int64(), ctypes.c_int64()
+    _lib.check(L.sedx_output_geometry(nat.h, length, ctypes.byref(fr), ctypes.byref(sl)), nat.h, 'geometry')
+    emb = torch.empty((B, ref.shape[2], sl.value), dtype=torch.float32, device=wave.device)
+    stream = ctypes.c_void_p(torch.cuda.current_stream(wave.device).cuda_stream)
+    for _ in range(2):
+        fw.fill_(float('nan'))
+        _lib.check(L.sedx_forward(nat.h, _ptr(wave), B, length, _ptr(fw), _ptr(clip), _ptr(emb), _ptr(ws),
+                                  wsz.value, stream), nat.h, 'forward')
+        torch.cuda.synchronize()
+        assert torch.equal(fw, ref)
+
+
 def test_wino_block1_knob_errors():
     """A bad value for the knob is a loud error, not a silent fallback."""
     from sedx import _lib
