@@ -411,8 +411,12 @@ sedx_status run_body(sedx_handle* h, int64_t B, const Geometry& g, float* ws, co
   };
   // claim counters of the x3 launches and of the F(4x4,3x3) launches (the
   // workspace comes from the caller: zeroed once per forward, ahead of the
-  // pipelined wait — this forward's memory only)
-  const bool w43 = h->precision == SEDX_PRECISION_WINOGRAD && h->wino_f43;
+  // pipelined wait — this forward's memory only).  Below 8 clips the
+  // F(4x4,3x3) launches get no counters (the static item order, same
+  // outputs) and the forward no memset: one fill launch less on the
+  // one-clip latency path
+  const bool w43 = h->precision == SEDX_PRECISION_WINOGRAD && h->wino_f43 && B >= 8;
+  int* const w43_sched = w43 ? sched : nullptr;
   if (x3 || w43) HIP_TRY(h, hipMemsetAsync(sched, 0, 7 * CONV_SCHED_INTS * sizeof(int), s));
   const bool first_early = h->pipelined && h->pipe_conv1_first;
   if (first_early) block1_first();
@@ -442,7 +446,7 @@ sedx_status run_body(sedx_handle* h, int64_t B, const Geometry& g, float* ws, co
                              sched, s);
     else if (i == 0 && b1_43)
       launch_conv3x3_wino43(A, iB, c.T, 64, 64, 64, w.wu43[c.idx], w.cb[c.idx], c.out, EPI_POOL2, w.trash, s,
-                            h->wino_order, c4, 0, sched);
+                            h->wino_order, c4, 0, w43_sched);
     else if (i == 0 && wb1 && h->wino_block1 == 2)
       launch_block1_wino(X0, iB, c.T, w.c1_w, w.c1_b, w.wu[c.idx], w.cb[c.idx], c.out, w.zero, w.trash, s, c4);
     else if (i == 0 && wb1)
@@ -454,7 +458,7 @@ sedx_status run_body(sedx_handle* h, int64_t B, const Geometry& g, float* ws, co
                         sched + i * CONV_SCHED_INTS, s);
     else if (h->precision == SEDX_PRECISION_WINOGRAD && h->wino_f43)
       launch_conv3x3_wino43(c.in, iB, c.T, c.F, c.cin, c.cout, w.wu43[c.idx], w.cb[c.idx], c.out, c.epi, w.trash, s,
-                            h->wino_order, c4, 0, sched + i * CONV_SCHED_INTS);
+                            h->wino_order, c4, 0, w43 ? sched + i * CONV_SCHED_INTS : nullptr);
     else if (h->precision == SEDX_PRECISION_WINOGRAD)
       launch_conv3x3_wino(c.in, iB, c.T, c.F, c.cin, c.cout, w.wu[c.idx], w.cb[c.idx], c.out, c.epi, w.zero, w.trash,
                           s, h->wino_order);
